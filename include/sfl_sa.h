@@ -1,0 +1,187 @@
+/*
+ * sfl_sa.h — C-ABI of the MI355X secure-aggregation hot path (libsfl_sa.so).
+ *
+ * Drop-in boundary for the element-wise core of
+ * secretflow.security.aggregation.SecureAggregator (un-vendored dependency
+ * secretflow-lite==1.13.0b0, /root/reference/pyproject.toml:51).  Each entry
+ * point below cites the reference interface it replaces.  Python reaches it
+ * through ctypes (sfl_amd/_lib.py); INTEGRATION.md shows the binding a
+ * maintainer would add on the reference side.
+ *
+ * Conventions
+ *  - every function returns int: SA_OK (0) or a negative SA_ERR_* code; no
+ *    exception crosses the ABI.  sa_last_error() returns a message.
+ *  - device buffers are caller-owned; launches are asynchronous and ordered
+ *    on the caller's hipStream_t (passed as void*; NULL = legacy stream).
+ *  - the launch functions never allocate, copy or synchronise, so they can be
+ *    captured into a hipGraph.  Re-entrant per stream.
+ *  - mask-stream generator states are numpy PCG64 states (state, inc) as
+ *    128-bit little-endian pairs; the caller advances them between rounds
+ *    with sa_pcg64_advance(), exactly like the reference's persistent
+ *    np.random.Generator objects advance by one draw per masked element.
+ */
+#ifndef SFL_SA_H
+#define SFL_SA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SA_ABI_VERSION 1
+
+/* status codes */
+#define SA_OK 0
+#define SA_ERR_ARG (-1)         /* bad argument (null pointer, size, unsupported combo) */
+#define SA_ERR_HIP (-2)         /* HIP runtime error */
+#define SA_ERR_UNSUPPORTED (-3) /* valid request this build has no kernel for */
+#define SA_ERR_RCCL (-4)        /* RCCL error */
+
+/* element types */
+#define SA_F32 0
+#define SA_F64 1
+#define SA_I64 2
+
+/* bits set in *flags by the kernels */
+#define SA_FLAG_PRG_REJECT 1u /* a PCG64 raw draw was 0: numpy's Lemire bounded
+                                 draw would have rejected it and re-drawn (p=2^-64
+                                 per draw).  The mask stream then differs from
+                                 numpy's from that element on; the host must
+                                 re-run with the stream re-positioned. */
+
+typedef struct sa_u128 {
+  uint64_t lo, hi;
+} sa_u128;
+
+/* numpy PCG64 bit_generator.state['state'] = {state, inc} */
+typedef struct sa_pcg64 {
+  sa_u128 state;
+  sa_u128 inc;
+} sa_pcg64;
+
+/* One pairwise mask stream as seen by ONE client (the owner of the stream
+ * for this call).  sign = +1 when the peer's name sorts after the client's
+ * (q += m), -1 otherwise (q -= m): the `party > self._party` rule of the
+ * masking equation, docs/developer/algorithm/secure_aggregation.ipynb
+ * cell 15. */
+typedef struct sa_mask_stream {
+  sa_pcg64 gen; /* generator state before draw 0 of this call */
+  int32_t sign; /* +1 / -1 */
+  int32_t peer; /* informational (peer client index) */
+} sa_mask_stream;
+
+/* A client co-located on this GPU for the fused kernel. */
+typedef struct sa_local_client {
+  const void* x;        /* n elements of x_type, device pointer */
+  double weight;        /* scalar weight w_c (1.0 = none); applied in the compute type */
+  uint64_t* masked_out; /* optional: this client's masked vector (wire image), n u64 */
+} sa_local_client;
+
+/* ------------------------------------------------------------------ */
+/* library / setup (host only, no GPU needed)                          */
+/* ------------------------------------------------------------------ */
+
+int sa_abi_version(void);
+const char* sa_last_error(void);
+
+/* numpy.random.PCG64(seed) seeding: SeedSequence(entropy) -> generate_state(4,
+ * uint64) -> pcg_setseq_128_srandom.  `words` is the entropy as 32-bit
+ * little-endian words (numpy's _coerce_to_uint32_array of a non-negative int).
+ * Replaces: `np.random.default_rng(seed)` inside the un-vendored _Masker
+ * (secure_aggregation.ipynb cell 15 names numpy.random.PCG64). */
+int sa_pcg64_from_seed(const uint32_t* words, int n_words, sa_pcg64* out);
+
+/* == numpy PCG64.advance(delta): jump the generator by delta draws. */
+int sa_pcg64_advance(sa_pcg64* g, sa_u128 delta);
+
+/* Host-side reference draws, for validating the seeding/jump math only
+ * (tests).  Not used by any hot-path entry point. */
+int sa_pcg64_raw_host(sa_pcg64* g, uint64_t* out, uint64_t n);
+
+/* ------------------------------------------------------------------ */
+/* hot path (device, asynchronous on `stream`)                          */
+/* ------------------------------------------------------------------ */
+
+/* _Masker.mask for ONE client (un-vendored; equation at
+ * secure_aggregation.ipynb cell 15, quantizer pinned by the KAT of cells
+ * 17-18): masked[i] = trunc(x[i]*w*2^fxp) + sum_j sign_j * m_j[i]  (mod 2^64),
+ * m_j = PCG64(gen_j).integers(int64.min, int64.max, n).astype(uint64).
+ *
+ *   x, x_type       input vector (SA_F32/SA_F64/SA_I64).  x == NULL means
+ *                   "continue": start from the current contents of `out`
+ *                   (multi-pass masking when n_streams exceeds one pass).
+ *   compute_type    arithmetic type of x*w*2^fxp (numpy promotion result:
+ *                   SA_F32 for float32 data with a python-scalar weight,
+ *                   SA_F64 for float64 data or array weights, SA_I64 for
+ *                   integer data and weights).
+ *   weight          scalar weight (1.0 = none)
+ *   weight_vec      optional per-element weights (n elements, compute_type)
+ *   out             masked vector, n u64 (required)
+ *   sum_accum       optional: sum_accum[i] += masked[i]
+ *   digest          optional: *digest ^= XOR of all masked[i]
+ *   flags           optional: |= SA_FLAG_*
+ */
+int sa_mask(const void* x, int x_type, int compute_type, uint64_t n, double weight,
+            const void* weight_vec, int fxp_bits, const sa_mask_stream* streams, int n_streams,
+            uint64_t* out, uint64_t* sum_accum, uint64_t* digest, uint32_t* flags, void* stream);
+
+/* Fused single-GPU simulation of C = n_clients co-located clients (config 2
+ * and the 1-GPU headline): quantize every client, expand every internal pair
+ * stream ONCE and apply it +/- to both of its clients, apply each client's
+ * n_cross cross-GPU streams, and write the masked sum.  Each client's masked
+ * vector is formed in registers: it is XOR-folded into digests[c] and, when
+ * clients[c].masked_out != NULL, stored (wire image).
+ *
+ *   pair_gens       n_clients*(n_clients-1)/2 generators, pair (u<v) at
+ *                   index u*(2C-u-1)/2 + (v-u-1)
+ *   pair_sign       +1 when client u adds the pair mask (name_v > name_u)
+ *   cross           n_clients * n_cross streams, client-major
+ *   sum_out         n u64; accumulate != 0 means sum_out[i] += local sum
+ *   digests         n_clients u64 (XOR-accumulated; zero them first)
+ * Replaces: the client-side `mask` calls plus server `_sum`'s
+ * np.sum(..., axis=0) for co-located parties. */
+int sa_fused_clients(const sa_local_client* clients, int n_clients, int x_type, uint64_t n,
+                     int fxp_bits, const sa_pcg64* pair_gens, const int8_t* pair_sign,
+                     const sa_mask_stream* cross, int n_cross, uint64_t* sum_out, int accumulate,
+                     uint64_t* digests, uint32_t* flags, void* stream);
+
+/* Server `_sum`: out[i] = sum_k in[k][i] mod 2^64 (np.sum over uint64,
+ * pattern of sfl/security/aggregation/sparse_plain_aggregator.py:88-94).
+ * `in` is a HOST array of k device pointers; out may alias in[0]. */
+int sa_sum_u64(const uint64_t* const* in, int k, uint64_t n, uint64_t* out, void* stream);
+
+/* Server decode: out[i] = (double)(int64)s[i] / 2^fxp / div, with
+ * div = divisor_vec[i] when divisor_vec != NULL (per-element weights,
+ * CHANGELOG.md:994) else `divisor` (1.0 for sum, C or sum(w) for average).
+ * Division is IEEE (correctly rounded), matching numpy float64. */
+int sa_decode(const uint64_t* s, uint64_t n, int fxp_bits, double divisor,
+              const double* divisor_vec, double* out, void* stream);
+
+/* Element-wise sum of per-client weight arrays for per-element-weight
+ * averages: out[i] = sum_k w[k][i] (float64), `w` a HOST array of k device
+ * pointers. */
+int sa_sum_f64(const double* const* w, int k, uint64_t n, double* out, void* stream);
+
+/* ------------------------------------------------------------------ */
+/* multi-GPU exchange: the masked-sum reduce over RCCL (xGMI)           */
+/* Replaces the RayFed `.to(server)` transfer + server np.sum           */
+/* (sfl/distributed/op_strategy.py:131-141; sparse_plain_aggregator.py:86) */
+/* ------------------------------------------------------------------ */
+
+#define SA_UNIQUE_ID_BYTES 128
+
+int sa_comm_unique_id(void* id_out, int cap);
+int sa_comm_init(void** comm, const void* id, int nranks, int rank, int device);
+/* ncclReduce(ncclUint64, ncclSum): recv (on root) = sum over ranks of send.
+ * Bit-exact for any RCCL algorithm: uint64 add is associative mod 2^64. */
+int sa_comm_reduce_u64(void* comm, const uint64_t* send, uint64_t* recv, uint64_t n, int root,
+                       void* stream);
+int sa_comm_allreduce_u64(void* comm, const uint64_t* send, uint64_t* recv, uint64_t n,
+                          void* stream);
+int sa_comm_destroy(void* comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SFL_SA_H */

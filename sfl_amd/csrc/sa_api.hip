@@ -1,0 +1,351 @@
+// sa_api.hip — extern "C" entry points of libsfl_sa.so (see include/sfl_sa.h)
+// plus the two HBM-streaming server kernels (masked-vector sum, decode).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <mutex>
+#include <unordered_map>
+
+#include "../../include/sfl_sa.h"
+#include "pcg128.h"
+#include "sa_internal.h"
+
+namespace sa {
+
+int occupancy_blocks(const void* kernel) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    sa_set_error("hipGetDevice failed");
+    return -1;
+  }
+  const void* key = (const void*)((uintptr_t)kernel ^ ((uintptr_t)dev << 56));
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlockThreads, 0) !=
+          hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    sa_set_error("occupancy query failed");
+    return -1;
+  }
+  if (per_cu < 1) per_cu = 1;
+  const int blocks = per_cu * cus;
+  cache[key] = blocks;
+  return blocks;
+}
+
+// ---------------------------------------------------------------------------
+// server sum: out = sum_k in[k]  (mod 2^64), 2 u64 per lane per step
+// ---------------------------------------------------------------------------
+constexpr int kSumMaxIn = 32;
+struct SumArgs {
+  const uint64_t* in[kSumMaxIn];
+  uint64_t* out;
+  uint64_t n;
+  int k;
+};
+
+__global__ void __launch_bounds__(256) k_sum_u64(const SumArgs a) {
+  const uint64_t n2 = a.n / 2;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+    ulonglong2 s = reinterpret_cast<const ulonglong2*>(a.in[0])[i];
+    for (int j = 1; j < a.k; j++) {
+      const ulonglong2 v = reinterpret_cast<const ulonglong2*>(a.in[j])[i];
+      s.x += v.x;
+      s.y += v.y;
+    }
+    reinterpret_cast<ulonglong2*>(a.out)[i] = s;
+  }
+  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    uint64_t s = 0;
+    for (int j = 0; j < a.k; j++) s += a.in[j][a.n - 1];
+    a.out[a.n - 1] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// decode: out = (double)(int64)s / 2^fxp / div
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_decode(const uint64_t* __restrict__ s, uint64_t n,
+                                                double inv_scale, double div,
+                                                const double* __restrict__ divv,
+                                                double* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double v = (double)(long long)s[i] * inv_scale;  // exact power-of-two scaling
+    out[i] = v / (divv ? divv[i] : div);                   // IEEE division
+  }
+}
+
+struct SumF64Args {
+  const double* in[kSumMaxIn];
+  double* out;
+  uint64_t n;
+  int k;
+  int accumulate;
+};
+__global__ void __launch_bounds__(256) k_sum_f64(const SumF64Args a) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    double s = a.accumulate ? a.out[i] : a.in[0][i];
+    for (int j = a.accumulate ? 0 : 1; j < a.k; j++) s += a.in[j][i];
+    a.out[i] = s;
+  }
+}
+
+static int stream_grid(uint64_t work_items, const void* kfn) {
+  const int maxb = occupancy_blocks(kfn);
+  if (maxb <= 0) return -1;
+  const uint64_t b = (work_items + 255) / 256;
+  const uint64_t cap = (uint64_t)maxb;
+  return (int)(b < 1 ? 1 : (b < cap ? b : cap));
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+static uint64_t fold_plus() { return kMaskOffset; }        // +m = t + K
+static uint64_t fold_minus() { return 1 - kMaskOffset; }   // -m = t + (1-K), t = ~raw
+
+}  // namespace sa
+
+using namespace sa;
+
+static int check_type(int t, const char* what) {
+  if (t != SA_F32 && t != SA_F64 && t != SA_I64) {
+    sa_set_error("%s: unknown element type %d", what, t);
+    return SA_ERR_ARG;
+  }
+  return SA_OK;
+}
+
+static void fill_stream(StreamArg& s, const sa_pcg64& g, int sign) {
+  s.s_lo = g.state.lo;
+  s.s_hi = g.state.hi;
+  s.inc_lo = g.inc.lo;
+  s.inc_hi = g.inc.hi;
+  s.cj_lo = s.cj_hi = 0;
+  s.smask = sign < 0 ? ~0ULL : 0ULL;
+  s.pad = 0;
+}
+
+extern "C" int sa_mask(const void* x, int x_type, int compute_type, uint64_t n, double weight,
+                       const void* weight_vec, int fxp_bits, const sa_mask_stream* streams,
+                       int n_streams, uint64_t* out, uint64_t* sum_accum, uint64_t* digest,
+                       uint32_t* flags, void* stream) {
+  if (check_type(x_type, "sa_mask x_type") || check_type(compute_type, "sa_mask compute_type"))
+    return SA_ERR_ARG;
+  if (!out || n_streams < 0 || (n_streams > 0 && !streams) || fxp_bits < 0 || fxp_bits > 62) {
+    sa_set_error("sa_mask: bad arguments (out=%p n_streams=%d fxp_bits=%d)", (void*)out,
+                 n_streams, fxp_bits);
+    return SA_ERR_ARG;
+  }
+  if (!aligned16(x) || !aligned16(out) || !aligned16(weight_vec) || !aligned16(sum_accum)) {
+    sa_set_error("sa_mask: device buffers must be 16-byte aligned");
+    return SA_ERR_ARG;
+  }
+  if (n == 0) return SA_OK;
+  // fp32 has kernels for up to 16 streams per pass, the other types 8
+  const int per_pass = (x_type == SA_F32 && compute_type == SA_F32) ? kMaskPass : kMaskPass / 2;
+  const int passes = n_streams == 0 ? 1 : (n_streams + per_pass - 1) / per_pass;
+  for (int p = 0; p < passes; p++) {
+    const int j0 = p * per_pass;
+    const int cnt = n_streams - j0 < per_pass ? n_streams - j0 : per_pass;
+    const bool last = p == passes - 1;
+    KArgs a;
+    memset(&a, 0, sizeof(a));
+    a.n = n;
+    a.fxp_bits = fxp_bits;
+    a.scale_d = (double)((uint64_t)1 << fxp_bits);
+    a.scale_f = (float)a.scale_d;
+    a.continue_mode = (p > 0 || x == nullptr) ? 1 : 0;
+    a.c[0].x = x;
+    a.c[0].wvec = weight_vec;
+    a.c[0].masked_out = out;
+    a.c[0].w = weight;
+    uint64_t bias = 0;
+    for (int j = 0; j < cnt; j++) {
+      const sa_mask_stream& ms = streams[j0 + j];
+      if (ms.sign != 1 && ms.sign != -1) {
+        sa_set_error("sa_mask: stream %d has sign %d (want +1/-1)", j0 + j, ms.sign);
+        return SA_ERR_ARG;
+      }
+      fill_stream(a.s[j], ms.gen, ms.sign);
+      bias += ms.sign > 0 ? fold_plus() : fold_minus();
+    }
+    a.c[0].bias = bias;
+    a.sum_out = last ? sum_accum : nullptr;
+    a.sum_mode = (last && sum_accum) ? 2 : 0;
+    a.digests = last ? digest : nullptr;
+    a.do_digest = (last && digest) ? 1 : 0;
+    a.flags = flags;
+    const int ct = compute_type;
+    LaunchFn fn = find_clients_kernel(x_type, ct, 1, cnt);
+    if (!fn) {
+      sa_set_error("sa_mask: no kernel for x_type=%d compute_type=%d streams=%d", x_type, ct, cnt);
+      return SA_ERR_UNSUPPORTED;
+    }
+    const int rc = fn(a, stream);
+    if (rc) return rc;
+  }
+  return SA_OK;
+}
+
+extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, int x_type,
+                                uint64_t n, int fxp_bits, const sa_pcg64* pair_gens,
+                                const int8_t* pair_sign, const sa_mask_stream* cross,
+                                int n_cross, uint64_t* sum_out, int accumulate,
+                                uint64_t* digests, uint32_t* flags, void* stream) {
+  if (check_type(x_type, "sa_fused_clients x_type")) return SA_ERR_ARG;
+  const int L = n_clients;
+  const int PI = L * (L - 1) / 2;
+  if (!clients || L < 1 || L > kMaxLocal || n_cross < 0 || !sum_out || fxp_bits < 0 ||
+      fxp_bits > 62 || (PI > 0 && (!pair_gens || !pair_sign)) || (n_cross > 0 && !cross)) {
+    sa_set_error("sa_fused_clients: bad arguments (n_clients=%d n_cross=%d)", L, n_cross);
+    return SA_ERR_ARG;
+  }
+  if (PI + L * n_cross > kMaxStreams) {
+    sa_set_error("sa_fused_clients: %d streams exceed the %d per launch", PI + L * n_cross,
+                 kMaxStreams);
+    return SA_ERR_UNSUPPORTED;
+  }
+  if (!aligned16(sum_out)) {
+    sa_set_error("sa_fused_clients: sum_out must be 16-byte aligned");
+    return SA_ERR_ARG;
+  }
+  if (n == 0) return SA_OK;
+  KArgs a;
+  memset(&a, 0, sizeof(a));
+  a.n = n;
+  a.fxp_bits = fxp_bits;
+  a.scale_d = (double)((uint64_t)1 << fxp_bits);
+  a.scale_f = (float)a.scale_d;
+  uint64_t bias[kMaxLocal] = {0};
+  for (int c = 0; c < L; c++) {
+    if (!clients[c].x || !aligned16(clients[c].x) || !aligned16(clients[c].masked_out)) {
+      sa_set_error("sa_fused_clients: client %d x null or buffers not 16-byte aligned", c);
+      return SA_ERR_ARG;
+    }
+    a.c[c].x = clients[c].x;
+    a.c[c].wvec = nullptr;
+    a.c[c].masked_out = clients[c].masked_out;
+    a.c[c].w = clients[c].weight;
+  }
+  int p = 0;
+  for (int u = 0; u < L; u++)
+    for (int v = u + 1; v < L; v++, p++) {
+      const int sg = pair_sign[p];
+      if (sg != 1 && sg != -1) {
+        sa_set_error("sa_fused_clients: pair %d sign %d", p, sg);
+        return SA_ERR_ARG;
+      }
+      fill_stream(a.s[p], pair_gens[p], sg);
+      if (sg > 0) {  // u adds m (t = raw), v subtracts: -t - K
+        bias[u] += kMaskOffset;
+        bias[v] += 0 - kMaskOffset;
+      } else {  // t = ~raw: u gets t + (1-K) = -m; v gets -t + (K-1) = +m
+        bias[u] += 1 - kMaskOffset;
+        bias[v] += kMaskOffset - 1;
+      }
+    }
+  for (int c = 0; c < L; c++)
+    for (int j = 0; j < n_cross; j++) {
+      const sa_mask_stream& ms = cross[c * n_cross + j];
+      if (ms.sign != 1 && ms.sign != -1) {
+        sa_set_error("sa_fused_clients: cross stream (%d,%d) sign %d", c, j, ms.sign);
+        return SA_ERR_ARG;
+      }
+      fill_stream(a.s[PI + c * n_cross + j], ms.gen, ms.sign);
+      bias[c] += ms.sign > 0 ? fold_plus() : fold_minus();
+    }
+  for (int c = 0; c < L; c++) a.c[c].bias = bias[c];
+  a.sum_out = sum_out;
+  a.sum_mode = accumulate ? 2 : 1;
+  a.digests = digests;
+  a.do_digest = digests ? 1 : 0;
+  a.flags = flags;
+  LaunchFn fn = find_clients_kernel(x_type, x_type, L, n_cross);
+  if (!fn) {
+    sa_set_error("sa_fused_clients: no kernel for x_type=%d clients=%d cross=%d", x_type, L,
+                 n_cross);
+    return SA_ERR_UNSUPPORTED;
+  }
+  return fn(a, stream);
+}
+
+extern "C" int sa_sum_u64(const uint64_t* const* in, int k, uint64_t n, uint64_t* out,
+                          void* stream) {
+  if (!in || k < 1 || !out) {
+    sa_set_error("sa_sum_u64: bad arguments (k=%d)", k);
+    return SA_ERR_ARG;
+  }
+  for (int j = 0; j < k; j++)
+    if (!in[j] || !aligned16(in[j])) {
+      sa_set_error("sa_sum_u64: input %d null or not 16-byte aligned", j);
+      return SA_ERR_ARG;
+    }
+  if (!aligned16(out)) {
+    sa_set_error("sa_sum_u64: out not 16-byte aligned");
+    return SA_ERR_ARG;
+  }
+  if (n == 0) return SA_OK;
+  const int grid = stream_grid(n / 2 + 1, (const void*)&k_sum_u64);
+  if (grid < 0) return SA_ERR_HIP;
+  // chain launches of up to 32 inputs; later launches fold the running sum in as input 0
+  for (int j0 = 0; j0 < k;) {
+    SumArgs a;
+    memset(&a, 0, sizeof(a));
+    int m = 0;
+    if (j0 > 0) a.in[m++] = out;
+    while (m < kSumMaxIn && j0 < k) a.in[m++] = in[j0++];
+    a.k = m;
+    a.out = out;
+    a.n = n;
+    hipLaunchKernelGGL(k_sum_u64, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    SA_HIP_CHECK(hipGetLastError());
+  }
+  return SA_OK;
+}
+
+extern "C" int sa_decode(const uint64_t* s, uint64_t n, int fxp_bits, double divisor,
+                         const double* divisor_vec, double* out, void* stream) {
+  if (!s || !out || fxp_bits < 0 || fxp_bits > 62) {
+    sa_set_error("sa_decode: bad arguments");
+    return SA_ERR_ARG;
+  }
+  if (n == 0) return SA_OK;
+  const int grid = stream_grid(n, (const void*)&k_decode);
+  if (grid < 0) return SA_ERR_HIP;
+  const double inv_scale = 1.0 / (double)((uint64_t)1 << fxp_bits);
+  hipLaunchKernelGGL(k_decode, dim3(grid), dim3(256), 0, (hipStream_t)stream, s, n, inv_scale,
+                     divisor, divisor_vec, out);
+  SA_HIP_CHECK(hipGetLastError());
+  return SA_OK;
+}
+
+extern "C" int sa_sum_f64(const double* const* w, int k, uint64_t n, double* out, void* stream) {
+  if (!w || k < 1 || !out) {
+    sa_set_error("sa_sum_f64: bad arguments");
+    return SA_ERR_ARG;
+  }
+  if (n == 0) return SA_OK;
+  const int grid = stream_grid(n, (const void*)&k_sum_f64);
+  if (grid < 0) return SA_ERR_HIP;
+  for (int j0 = 0; j0 < k;) {
+    SumF64Args a;
+    memset(&a, 0, sizeof(a));
+    a.accumulate = j0 > 0;
+    int m = 0;
+    while (m < kSumMaxIn && j0 < k) a.in[m++] = w[j0++];
+    a.k = m;
+    a.out = out;
+    a.n = n;
+    hipLaunchKernelGGL(k_sum_f64, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    SA_HIP_CHECK(hipGetLastError());
+  }
+  return SA_OK;
+}

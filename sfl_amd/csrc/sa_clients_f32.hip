@@ -1,0 +1,29 @@
+// sa_clients_f32.hip — fp32 instantiations of the masking kernel: the
+// single-client path (1 client, 0..16 streams per pass) and the fused
+// co-located-client shapes used by the benches (C clients over W GPUs:
+// L = C/W local clients, X = C - L cross streams each).
+#include "sa_clients_impl.h"
+#include "sa_registry.h"
+
+namespace sa {
+
+LaunchFn find_other_kernel(int xt, int ct, int L, int X);
+
+#define F32(L, X) SA_ENTRY(float, float, SA_F32, SA_F32, L, X)
+LaunchFn find_clients_kernel(int xt, int ct, int L, int X) {
+  static const KernelEntry kEntriesF32[] = {
+    F32(1, 0),  F32(1, 1),  F32(1, 2),  F32(1, 3),  F32(1, 4),  F32(1, 5),  F32(1, 6),
+    F32(1, 7),  F32(1, 8),  F32(1, 9),  F32(1, 10), F32(1, 11), F32(1, 12), F32(1, 13),
+    F32(1, 14), F32(1, 15), F32(1, 16),
+    // fused: C clients on one GPU
+    F32(2, 0), F32(3, 0), F32(4, 0), F32(5, 0), F32(6, 0), F32(7, 0), F32(8, 0),
+    // fused: C = 8 over W = 2 / 4 GPUs, C = 4 over 2 GPUs
+    F32(4, 4), F32(2, 6), F32(2, 2),
+  };
+  for (const KernelEntry& e : kEntriesF32)
+    if (e.xt == xt && e.ct == ct && e.L == L && e.X == X) return e.fn;
+  return find_other_kernel(xt, ct, L, X);
+}
+#undef F32
+
+}  // namespace sa

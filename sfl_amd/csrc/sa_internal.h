@@ -1,0 +1,60 @@
+// sa_internal.h — shared declarations for the libsfl_sa translation units.
+#pragma once
+#include <stdint.h>
+
+void sa_set_error(const char* fmt, ...);
+
+#define SA_HIP_CHECK(expr)                                                              \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      sa_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return SA_ERR_HIP;                                                                \
+    }                                                                                   \
+  } while (0)
+
+namespace sa {
+
+constexpr int kMaxLocal = 8;     // co-located clients per fused launch
+constexpr int kMaxStreams = 32;  // mask streams per launch (kernel-arg resident)
+constexpr int kMaskPass = 16;    // streams per pass of the single-client kernel
+
+// Kernel-argument image (lives in the kernarg segment; read with scalar loads).
+struct StreamArg {
+  uint64_t s_lo, s_hi;      // generator state before draw 0 of this call
+  uint64_t inc_lo, inc_hi;  // PCG64 increment
+  uint64_t cj_lo, cj_hi;    // inc * G_J: constant part of the per-tile jump
+  uint64_t smask;           // 0 (stream added) or ~0 (stream subtracted)
+  uint64_t pad;
+};
+
+struct ClientArg {
+  const void* x;         // input vector (XT); may be null in continue mode
+  const void* wvec;      // optional per-element weights (CT)
+  uint64_t* masked_out;  // optional masked vector out (required in continue mode)
+  double w;              // scalar weight
+  uint64_t bias;         // sum of the folded +/- mask offsets (see sa_kernels.hip)
+};
+
+struct KArgs {
+  ClientArg c[kMaxLocal];
+  StreamArg s[kMaxStreams];
+  uint64_t n;
+  uint64_t aj_lo, aj_hi;  // A^J, J = grid*1024 - 4
+  uint64_t* sum_out;
+  uint64_t* digests;
+  uint32_t* flags;
+  double scale_d;  // 2^fxp
+  float scale_f;
+  int32_t fxp_bits;
+  int32_t sum_mode;       // 0 none, 1 store, 2 accumulate
+  int32_t continue_mode;  // acc starts from masked_out instead of quantize(x)
+  int32_t do_digest;
+};
+
+typedef int (*LaunchFn)(const KArgs& a, void* stream);
+
+// Returns the launcher for (xt, ct, L, X) or nullptr when not instantiated.
+LaunchFn find_clients_kernel(int xt, int ct, int L, int X);
+
+}  // namespace sa

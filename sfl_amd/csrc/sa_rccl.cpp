@@ -1,0 +1,77 @@
+// sa_rccl.cpp — the one exchange step of the multi-GPU path: the masked
+// partial sums (uint64) of every GPU's clients reduced to the server GPU with
+// RCCL over xGMI.  Replaces the RayFed/Ray object-store `.to(server)` transfer
+// of masked arrays plus the server's np.sum (sfl/distributed/op_strategy.py:
+// 131-141, sfl/security/aggregation/sparse_plain_aggregator.py:86-94).
+// uint64 addition is associative mod 2^64, so every RCCL algorithm/order
+// yields the bit-exact masked sum.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include "../../include/sfl_sa.h"
+#include "sa_internal.h"
+
+static_assert(sizeof(ncclUniqueId) <= SA_UNIQUE_ID_BYTES, "unique id size");
+
+#define SA_NCCL_CHECK(expr)                                                          \
+  do {                                                                               \
+    ncclResult_t r_ = (expr);                                                        \
+    if (r_ != ncclSuccess) {                                                         \
+      sa_set_error("%s failed: %s", #expr, ncclGetErrorString(r_));                  \
+      return SA_ERR_RCCL;                                                            \
+    }                                                                                \
+  } while (0)
+
+extern "C" int sa_comm_unique_id(void* id_out, int cap) {
+  if (!id_out || cap < (int)sizeof(ncclUniqueId)) {
+    sa_set_error("sa_comm_unique_id: buffer too small (%d < %d)", cap, (int)sizeof(ncclUniqueId));
+    return SA_ERR_ARG;
+  }
+  ncclUniqueId id;
+  SA_NCCL_CHECK(ncclGetUniqueId(&id));
+  memcpy(id_out, &id, sizeof(id));
+  return SA_OK;
+}
+
+extern "C" int sa_comm_init(void** comm, const void* id, int nranks, int rank, int device) {
+  if (!comm || !id || nranks < 1 || rank < 0 || rank >= nranks) {
+    sa_set_error("sa_comm_init: bad arguments");
+    return SA_ERR_ARG;
+  }
+  SA_HIP_CHECK(hipSetDevice(device));
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  ncclComm_t c = nullptr;
+  SA_NCCL_CHECK(ncclCommInitRank(&c, nranks, uid, rank));
+  *comm = (void*)c;
+  return SA_OK;
+}
+
+extern "C" int sa_comm_reduce_u64(void* comm, const uint64_t* send, uint64_t* recv, uint64_t n,
+                                  int root, void* stream) {
+  if (!comm || !send) {
+    sa_set_error("sa_comm_reduce_u64: bad arguments");
+    return SA_ERR_ARG;
+  }
+  SA_NCCL_CHECK(ncclReduce(send, recv, (size_t)n, ncclUint64, ncclSum, root, (ncclComm_t)comm,
+                           (hipStream_t)stream));
+  return SA_OK;
+}
+
+extern "C" int sa_comm_allreduce_u64(void* comm, const uint64_t* send, uint64_t* recv,
+                                     uint64_t n, void* stream) {
+  if (!comm || !send || !recv) {
+    sa_set_error("sa_comm_allreduce_u64: bad arguments");
+    return SA_ERR_ARG;
+  }
+  SA_NCCL_CHECK(ncclAllReduce(send, recv, (size_t)n, ncclUint64, ncclSum, (ncclComm_t)comm,
+                              (hipStream_t)stream));
+  return SA_OK;
+}
+
+extern "C" int sa_comm_destroy(void* comm) {
+  if (!comm) return SA_OK;
+  SA_NCCL_CHECK(ncclCommDestroy((ncclComm_t)comm));
+  return SA_OK;
+}

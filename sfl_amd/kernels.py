@@ -1,0 +1,137 @@
+"""Tensor-level wrappers of the HIP hot path (libsfl_sa.so via ctypes).
+
+PyTorch is plumbing here: it owns device memory and streams; the work is done
+by the hand-written gfx950 kernels behind the C-ABI.  uint64 buffers are
+carried as ``torch.int64`` tensors (same bits); ``as_u64`` gives numpy views.
+
+Every function launches asynchronously on the current torch stream of the
+tensors' device and raises ``SALibraryError`` on any error.  Nothing here
+falls back to a CPU implementation.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+U64 = torch.int64  # storage dtype for uint64 buffers
+
+_XTYPE = {torch.float32: L.SA_F32, torch.float64: L.SA_F64, torch.int64: L.SA_I64}
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _require_gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("libsfl_sa kernels take device-resident tensors")
+
+
+def as_u64(t: torch.Tensor) -> np.ndarray:
+    """Host numpy uint64 view of a uint64-carrying int64 tensor."""
+    return t.detach().cpu().numpy().view(np.uint64)
+
+
+def xtype_of(dtype: torch.dtype) -> int:
+    try:
+        return _XTYPE[dtype]
+    except KeyError:
+        raise TypeError(f"unsupported element type {dtype}; use float32, float64 or int64") from None
+
+
+def make_streams(entries: Sequence[tuple]) -> C.Array:
+    """entries: (L.PCG64 gen, sign, peer) -> sa_mask_stream[]"""
+    arr = (L.MaskStream * max(1, len(entries)))()
+    for i, (g, sign, peer) in enumerate(entries):
+        arr[i].gen = g
+        arr[i].sign = int(sign)
+        arr[i].peer = int(peer)
+    return arr
+
+
+def mask(x: torch.Tensor | None, out: torch.Tensor, streams: Sequence[tuple], *,
+         weight: float = 1.0, weight_vec: torch.Tensor | None = None, compute_dtype=None,
+         fxp_bits: int = 18, x_dtype=None, sum_accum: torch.Tensor | None = None,
+         digest: torch.Tensor | None = None, flags: torch.Tensor | None = None) -> torch.Tensor:
+    """One client's masked vector: out = trunc(x*w*2^fxp) +/- masks (mod 2^64).
+    ``x=None`` continues from ``out`` (multi-pass).  See sa_mask in include/sfl_sa.h."""
+    _require_gpu(x, out, weight_vec, sum_accum, digest, flags)
+    n = out.numel()
+    if x is not None and x.numel() != n:
+        raise ValueError("x and out sizes differ")
+    xt = xtype_of(x.dtype if x is not None else (x_dtype or torch.float32))
+    ct = xtype_of(compute_dtype) if compute_dtype is not None else xt
+    sarr = make_streams(streams)
+    L.check(L.lib().sa_mask(_ptr(x), xt, ct, n, float(weight), _ptr(weight_vec), int(fxp_bits),
+                            sarr, len(streams), _ptr(out), _ptr(sum_accum), _ptr(digest),
+                            _ptr(flags), C.c_void_p(_stream(out))), "sa_mask")
+    return out
+
+
+def fused_clients(xs: Sequence[torch.Tensor], weights: Sequence[float], pair_gens: Sequence,
+                  pair_signs: Sequence[int], cross: Sequence[tuple], n_cross: int,
+                  sum_out: torch.Tensor, *, fxp_bits: int = 18, accumulate: bool = False,
+                  digests: torch.Tensor | None = None, flags: torch.Tensor | None = None,
+                  masked_outs: Sequence[torch.Tensor | None] | None = None) -> torch.Tensor:
+    """C co-located clients in one launch: quantize, pairwise masks, masked sum.
+    See sa_fused_clients in include/sfl_sa.h."""
+    _require_gpu(sum_out, digests, flags, *xs)
+    nc = len(xs)
+    n = sum_out.numel()
+    clients = (L.LocalClient * nc)()
+    for c, x in enumerate(xs):
+        if x.numel() != n or x.dtype != xs[0].dtype:
+            raise ValueError("fused clients need equal-size vectors of one dtype")
+        clients[c].x = x.data_ptr()
+        clients[c].weight = float(weights[c])
+        mo = masked_outs[c] if masked_outs else None
+        clients[c].masked_out = mo.data_ptr() if mo is not None else None
+    npair = nc * (nc - 1) // 2
+    pg = (L.PCG64 * max(1, npair))(*pair_gens)
+    ps = (C.c_int8 * max(1, npair))(*[int(s) for s in pair_signs])
+    carr = make_streams(cross)
+    L.check(L.lib().sa_fused_clients(clients, nc, xtype_of(xs[0].dtype), n, int(fxp_bits), pg, ps,
+                                     carr, int(n_cross), _ptr(sum_out), int(bool(accumulate)),
+                                     _ptr(digests), _ptr(flags), C.c_void_p(_stream(sum_out))),
+            "sa_fused_clients")
+    return sum_out
+
+
+def sum_u64(ins: Sequence[torch.Tensor], out: torch.Tensor) -> torch.Tensor:
+    """Server sum mod 2^64 of masked vectors."""
+    _require_gpu(out, *ins)
+    n = out.numel()
+    for t in ins:
+        if t.numel() != n or t.device != out.device:
+            raise ValueError("sum_u64 inputs must match out in size and device")
+    ptrs = (C.c_void_p * len(ins))(*[t.data_ptr() for t in ins])
+    L.check(L.lib().sa_sum_u64(ptrs, len(ins), n, _ptr(out), C.c_void_p(_stream(out))), "sa_sum_u64")
+    return out
+
+
+def decode(s: torch.Tensor, out: torch.Tensor, *, fxp_bits: int = 18, divisor: float = 1.0,
+           divisor_vec: torch.Tensor | None = None) -> torch.Tensor:
+    """float64 out = (int64)s / 2^fxp / divisor (or / divisor_vec[i])."""
+    _require_gpu(s, out, divisor_vec)
+    L.check(L.lib().sa_decode(_ptr(s), s.numel(), int(fxp_bits), float(divisor), _ptr(divisor_vec),
+                              _ptr(out), C.c_void_p(_stream(out))), "sa_decode")
+    return out
+
+
+def sum_f64(ins: Sequence[torch.Tensor], out: torch.Tensor) -> torch.Tensor:
+    _require_gpu(out, *ins)
+    ptrs = (C.c_void_p * len(ins))(*[t.data_ptr() for t in ins])
+    L.check(L.lib().sa_sum_f64(ptrs, len(ins), out.numel(), _ptr(out), C.c_void_p(_stream(out))),
+            "sa_sum_f64")
+    return out

@@ -1,0 +1,115 @@
+"""One process per GPU: simulated clients sharded across ranks, the masked
+partial sums reduced to the server rank with RCCL over xGMI.
+
+North-star layout (BASELINE.json): C clients over W GPUs, clients assigned in
+contiguous blocks (rank r owns clients [r*C/W, (r+1)*C/W)).  Each rank runs
+ONE fused launch (``sa_fused_clients``) over its L = C/W local clients:
+internal pair streams are expanded once and applied to both clients, each
+local client additionally applies its C - L cross-rank streams (the peer's
+half of those pairs runs on the peer's rank).  The only exchange is the
+uint64 masked partial sum, reduced to rank 0 (the server) by ``ncclReduce``
+(``sa_comm_reduce_u64``) — bit-exact for any RCCL algorithm because uint64
+addition is associative mod 2^64.  This replaces the RayFed ``.to(server)``
+transfer plus the server ``np.sum`` (sfl/distributed/op_strategy.py:131-141,
+sfl/security/aggregation/sparse_plain_aggregator.py:86-94).
+
+The shard planning here is pure host logic (tested with gloo on CPU); the
+data path is the HIP kernels plus RCCL.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+from . import _lib as L
+
+
+def client_shard(n_clients: int, world: int, rank: int) -> list[int]:
+    """Contiguous block of client indices owned by ``rank``."""
+    if n_clients % world:
+        raise ValueError(f"{n_clients} clients do not split evenly over {world} ranks")
+    per = n_clients // world
+    return list(range(rank * per, (rank + 1) * per))
+
+
+@dataclass
+class LocalPlan:
+    """What one rank launches: pair streams among its clients, cross streams
+    to clients on other ranks (client-major, equal count per client)."""
+
+    clients: list[int]
+    pairs: list[tuple[int, int]] = field(default_factory=list)         # (u, v) global ids, u < v local
+    pair_signs: list[int] = field(default_factory=list)                # sign for u
+    cross: list[tuple[int, int, int]] = field(default_factory=list)    # (client, peer, sign)
+
+    @property
+    def n_cross(self) -> int:
+        return len(self.cross) // max(1, len(self.clients))
+
+
+def plan_rank(names: list[str], world: int, rank: int) -> LocalPlan:
+    """Streams rank ``rank`` must expand.  Signs follow the reference's
+    ``party > self._party`` name rule (secure_aggregation.ipynb cell 15)."""
+    C = len(names)
+    mine = client_shard(C, world, rank)
+    p = LocalPlan(clients=mine)
+    for i, u in enumerate(mine):
+        for v in mine[i + 1:]:
+            p.pairs.append((u, v))
+            p.pair_signs.append(1 if names[v] > names[u] else -1)
+    local = set(mine)
+    for u in mine:
+        for v in range(C):
+            if v not in local:
+                p.cross.append((u, v, 1 if names[v] > names[u] else -1))
+    return p
+
+
+def plan_generators(plan: LocalPlan, seed_of, offset: int = 0):
+    """(pair_gens, pair_signs, cross_streams) for ``kernels.fused_clients``.
+    ``seed_of(u, v)`` returns the pairwise seed (symmetric)."""
+    pg = [L.pcg64_advance(L.pcg64_from_seed(seed_of(u, v)), offset) for (u, v) in plan.pairs]
+    cross = [(L.pcg64_advance(L.pcg64_from_seed(seed_of(u, v)), offset), s, v) for (u, v, s) in plan.cross]
+    return pg, list(plan.pair_signs), cross
+
+
+class RcclComm:
+    """Our own RCCL communicator (C-ABI ``sa_comm_*``), rendezvoused through
+    an existing torch.distributed group (which only carries the unique id)."""
+
+    def __init__(self, rank: int, world: int, device: int, group=None):
+        import torch.distributed as dist
+
+        uid = (C.c_char * L.SA_UNIQUE_ID_BYTES)()
+        if rank == 0:
+            L.check(L.lib().sa_comm_unique_id(uid, L.SA_UNIQUE_ID_BYTES), "sa_comm_unique_id")
+        box = [bytes(uid) if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        uid = (C.c_char * L.SA_UNIQUE_ID_BYTES).from_buffer_copy(box[0])
+        h = C.c_void_p()
+        L.check(L.lib().sa_comm_init(C.byref(h), uid, world, rank, device), "sa_comm_init")
+        self._h = h
+        self.rank, self.world = rank, world
+
+    def reduce_u64(self, send, recv, root: int = 0):
+        import torch
+
+        stream = torch.cuda.current_stream(send.device).cuda_stream
+        L.check(L.lib().sa_comm_reduce_u64(self._h, C.c_void_p(send.data_ptr()),
+                                           C.c_void_p(recv.data_ptr()) if recv is not None else None,
+                                           send.numel(), root, C.c_void_p(stream)), "sa_comm_reduce_u64")
+        return recv
+
+    def allreduce_u64(self, send, recv):
+        import torch
+
+        stream = torch.cuda.current_stream(send.device).cuda_stream
+        L.check(L.lib().sa_comm_allreduce_u64(self._h, C.c_void_p(send.data_ptr()), C.c_void_p(recv.data_ptr()),
+                                              send.numel(), C.c_void_p(stream)), "sa_comm_allreduce_u64")
+        return recv
+
+    def close(self):
+        if self._h:
+            L.check(L.lib().sa_comm_destroy(self._h), "sa_comm_destroy")
+            self._h = None

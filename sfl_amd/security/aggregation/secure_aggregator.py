@@ -1,0 +1,292 @@
+"""SecureAggregator on MI355X: the drop-in for
+``secretflow.security.aggregation.SecureAggregator`` (un-vendored,
+``secretflow-lite==1.13.0b0``; constructor ``(device, participants,
+fxp_bits=18)`` as subclassed at
+``sfl/security/aggregation/stateful_fedgen_aggregator.py:23-33`` and used at
+``docs/developer/algorithm/secure_aggregation.ipynb`` cell 16).
+
+Protocol (notebook cell 15, semi-honest, no dropout): every party quantizes
+``x*w`` to fixed point ``trunc(x*w*2^fxp)`` (int64 viewed as uint64), adds
+``m_uv`` for each peer ``v`` whose name sorts after it and subtracts it
+otherwise, where ``m_uv = PCG64(seed_uv).integers(int64.min, int64.max)``;
+the server sums the masked uint64 vectors mod 2^64 — the masks cancel — and
+decodes ``int64(S) / 2^fxp`` as float64, divided by ``sum(w)`` (or C) for the
+average.  All per-element work (quantize, mask expansion, mod-2^64 sums,
+decode) runs in the hand-written gfx950 kernels of ``libsfl_sa.so``.
+
+Placement: each party is a ``PYU`` bound to a GPU.  When every party sits on
+the server's GPU and the payload is float32 with scalar weights, the clients
+are simulated by ONE fused launch (``sa_fused_clients``) that expands each
+pair stream once and applies it to both clients; otherwise each party masks
+on its own GPU (``sa_mask``), the masked vectors move to the server
+(``.to(server)``, the wire) and are summed there (``sa_sum_u64``).  Both give
+bit-identical sums.
+"""
+
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+import torch
+
+from ... import kernels as K
+from ... import _lib as L
+from ...device import PYU, PYUObject, DeviceObject, reveal
+from .aggregator import Aggregator
+from .masker import Masker
+
+_NP2T = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+         np.dtype(np.int64): torch.int64}
+_T2NP = {v: k for k, v in _NP2T.items()}
+MAX_FUSED_CLIENTS = 8
+
+
+def _layers(payload):
+    if isinstance(payload, (list, tuple)):
+        return list(payload), True
+    return [payload], False
+
+
+def _np_dtype(a) -> np.dtype:
+    if isinstance(a, torch.Tensor):
+        return _T2NP.get(a.dtype) or np.dtype(str(a.dtype).replace("torch.", ""))
+    return np.asarray(a).dtype
+
+
+def _shape(a):
+    return tuple(a.shape) if isinstance(a, torch.Tensor) else np.shape(a)
+
+
+def _compute_dtype(ldt: np.dtype, w, fxp_bits: int) -> np.dtype:
+    """numpy's result dtype of ``(datum * w) * (1 << fxp)`` (NEP 50 rules)."""
+    probe = np.zeros(1, dtype=ldt)
+    if w is not None:
+        if isinstance(w, (bool, int, float)):
+            probe = probe * w
+        else:
+            wa = np.asarray(w)
+            probe = probe * np.zeros(1, dtype=wa.dtype) if wa.ndim else probe * wa.dtype.type(0)
+    return (probe * (1 << fxp_bits)).dtype
+
+
+class SecureAggregator(Aggregator):
+    """Pairwise-mask secure aggregation with the HIP hot path.
+
+    Args:
+        device: the server PYU that receives the masked vectors and decodes.
+        participants: the client PYUs (distinct parties).
+        fxp_bits: fixed-point fraction bits (reference default 18).
+        seeds: optional ``{(party_a, party_b): seed}`` pairwise seeds (both
+            orders accepted); default is a Diffie-Hellman agreement.
+        fused: allow the single-launch simulation of co-located clients.
+        keep_masked: also materialise every party's masked vector (the wire
+            image) and expose the last ones as ``last_masked``.
+    """
+
+    def __init__(self, device: PYU, participants: List[PYU], fxp_bits: int = 18, *,
+                 seeds: dict | None = None, fused: bool = True, keep_masked: bool = False):
+        assert participants, "participants should not be empty"
+        names = [p.party for p in participants]
+        assert len(set(names)) == len(names), f"duplicate participants: {names}"
+        self._device = device
+        self._participants = list(participants)
+        self._fxp_bits = int(fxp_bits)
+        self._fused = fused
+        self._keep_masked = keep_masked
+        self.last_masked = None
+        self.last_digests = None
+        self._maskers = {n: Masker(n, self._fxp_bits) for n in names}
+        if seeds is None:
+            keys = {n: m.public_key for n, m in self._maskers.items()}
+            for m in self._maskers.values():
+                m.agree(keys)
+        else:
+            for a in names:
+                for b in names:
+                    if a != b:
+                        s = seeds.get((a, b), seeds.get((b, a)))
+                        if s is None:
+                            raise ValueError(f"missing seed for pair ({a}, {b})")
+                        self._maskers[a].set_seed(b, int(s))
+
+    @property
+    def device(self) -> PYU:
+        return self._device
+
+    @property
+    def participants(self) -> List[PYU]:
+        return list(self._participants)
+
+    # ------------------------------------------------------------------ API
+    def sum(self, data: List[DeviceObject], axis=None) -> DeviceObject:
+        return self._aggregate(data, axis, weights=None, average=False)
+
+    def average(self, data: List[DeviceObject], axis=None, weights=None) -> DeviceObject:
+        return self._aggregate(data, axis, weights=weights, average=True)
+
+    # ------------------------------------------------------------ internals
+    def _aggregate(self, data, axis, weights, average: bool) -> DeviceObject:
+        assert data, "Data to aggregate should not be None or empty!"
+        if axis not in (0, None):
+            raise NotImplementedError("SecureAggregator aggregates over parties (axis=0)")
+        for d in data:
+            assert isinstance(d, PYUObject), f"expect PYUObject, got {type(d)}"
+            assert d.device.party in self._maskers, f"{d.device} is not a participant"
+        owners = [d.device.party for d in data]
+        assert len(set(owners)) == len(owners), "each party may contribute one object"
+        assert set(owners) == set(self._maskers), (
+            "every participant must contribute (pairwise masks only cancel without dropout, "
+            "secure_aggregation.ipynb cell 15)")
+        if weights is not None:
+            if isinstance(weights, PYUObject):
+                raise TypeError("weights must be a per-party list")
+            assert len(weights) == len(data), (
+                f"Length of the weights does not match the data: {len(weights)} vs {len(data)}.")
+            wl = []
+            for i, w in enumerate(weights):
+                if isinstance(w, PYUObject):
+                    assert w.device == data[i].device, "Device of weight does not match the corresponding data device."
+                    w = reveal(w)
+                if isinstance(w, torch.Tensor):
+                    w = w.detach().cpu().numpy()
+                wl.append(w)
+            weights = wl
+
+        payloads = [d.data for d in data]
+        layer_lists, is_list = zip(*[_layers(p) for p in payloads])
+        is_list = is_list[0]
+        nl = len(layer_lists[0])
+        for ll in layer_lists:
+            assert len(ll) == nl, "parties hold different numbers of arrays"
+        shapes = [_shape(a) for a in layer_lists[0]]
+        for ll in layer_lists:
+            assert [_shape(a) for a in ll] == shapes, "parties hold arrays of different shapes"
+        as_torch = isinstance(layer_lists[0][0], torch.Tensor)
+
+        server = self._device
+        sdev = server.torch_device
+        flags = torch.zeros(1, dtype=torch.int32, device=sdev)
+        out_layers = []
+        masked_keep, digests_keep = [], []
+
+        # layers are masked in order with one stream position per (party, peer),
+        # exactly like the reference's per-layer rng.integers calls
+        for li in range(nl):
+            n = int(np.prod(shapes[li])) if shapes[li] else 1
+            xs, cts, ws, wvecs = [], [], [], []
+            for ci, d in enumerate(data):
+                party = d.device
+                a = layer_lists[ci][li]
+                w = None if weights is None else weights[ci]
+                ldt = _np_dtype(a)
+                ct = _compute_dtype(ldt, w, self._fxp_bits)
+                if ct not in (np.dtype(np.float32), np.dtype(np.float64), np.dtype(np.int64)):
+                    raise NotImplementedError(f"arithmetic type {ct} (data {ldt}) is not supported")
+                xt = ldt if ldt in _NP2T else (np.dtype(np.int64) if ldt.kind in "biu" else np.dtype(np.float64))
+                if ldt.kind in "biu" and ldt != np.dtype(np.int64) and ct.kind == "i":
+                    raise NotImplementedError(f"integer data of type {ldt} is not supported")
+                x = self._to_device(a, xt, party)
+                wv, wscalar = None, 1.0
+                if w is not None:
+                    if np.ndim(w) == 0:
+                        wscalar = float(w) if ct.kind == "f" else int(w)
+                    else:
+                        wb = np.broadcast_to(np.asarray(w), shapes[li]).astype(ct)
+                        wv = torch.from_numpy(np.ascontiguousarray(wb).reshape(-1)).to(party.torch_device)
+                xs.append(x)
+                cts.append(ct)
+                ws.append(wscalar)
+                wvecs.append(wv)
+
+            s = self._masked_sum(data, xs, cts, ws, wvecs, n, flags, masked_keep, digests_keep)
+
+            # decode on the server GPU: / 2^fxp, then / C or / sum(w)
+            dec = torch.empty(n, dtype=torch.float64, device=sdev)
+            divisor, divisor_vec = 1.0, None
+            if average:
+                if weights is None:
+                    divisor = float(len(data))
+                elif all(np.ndim(w) == 0 for w in weights):
+                    divisor = float(sum(weights))
+                else:
+                    wb = [torch.from_numpy(np.ascontiguousarray(
+                        np.broadcast_to(np.asarray(w), shapes[li]).astype(np.float64)).reshape(-1)).to(sdev)
+                        for w in weights]
+                    divisor_vec = K.sum_f64(wb, torch.empty(n, dtype=torch.float64, device=sdev))
+            K.decode(s, dec, fxp_bits=self._fxp_bits, divisor=divisor, divisor_vec=divisor_vec)
+            dec = dec.reshape(shapes[li])
+            out_layers.append(dec if as_torch else dec.cpu().numpy())
+
+        if int(flags.item()) & L.SA_FLAG_PRG_REJECT:
+            raise L.SALibraryError(
+                "a PCG64 raw draw was 0 (p=2^-64): numpy would have re-drawn; re-run with the stream "
+                "re-positioned")
+        if self._keep_masked:
+            self.last_masked = masked_keep
+        self.last_digests = digests_keep
+        result = out_layers if is_list else out_layers[0]
+        if is_list and isinstance(payloads[0], tuple):
+            result = tuple(result)
+        return PYUObject(server, result)
+
+    @staticmethod
+    def _to_device(a, xt: np.dtype, party: PYU) -> torch.Tensor:
+        tdt = _NP2T[xt]
+        if isinstance(a, torch.Tensor):
+            t = a.detach().reshape(-1).to(device=party.torch_device, dtype=tdt)
+        else:
+            t = torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=xt).reshape(-1)).to(party.torch_device)
+        t = t.contiguous()
+        if t.data_ptr() % 16:
+            t = t.clone()
+        return t
+
+    def _masked_sum(self, data, xs, cts, ws, wvecs, n, flags, masked_keep, digests_keep):
+        server = self._device
+        sdev = server.torch_device
+        parties = [d.device for d in data]
+        names = [p.party for p in parties]
+        C = len(names)
+        s = torch.empty(n, dtype=K.U64, device=sdev)
+        digests = torch.zeros(C, dtype=K.U64, device=sdev)
+        fusable = (self._fused and not self._keep_masked and 2 <= C <= MAX_FUSED_CLIENTS
+                   and all(p.gpu == server.gpu for p in parties)
+                   and all(ct == np.dtype(np.float32) for ct in cts)
+                   and all(x.dtype == torch.float32 for x in xs)
+                   and all(wv is None for wv in wvecs)
+                   and set(names) == set(self._maskers))
+        if fusable:
+            pair_gens, pair_signs = [], []
+            for u in range(C):
+                for v in range(u + 1, C):
+                    mu, mv = self._maskers[names[u]], self._maskers[names[v]]
+                    assert mu.position(names[v]) == mv.position(names[u]), "pair streams out of step"
+                    pair_gens.append(mu.generator(names[v]))
+                    pair_signs.append(mu.sign(names[v]))
+            with torch.cuda.device(sdev):
+                K.fused_clients(xs, ws, pair_gens, pair_signs, [], 0, s, fxp_bits=self._fxp_bits,
+                                digests=digests, flags=flags)
+        else:
+            masked = []
+            for ci, p in enumerate(parties):
+                m = self._maskers[p.party]
+                peers = [q for q in m.peers]
+                out = torch.empty(n, dtype=K.U64, device=p.torch_device)
+                dig = torch.zeros(1, dtype=K.U64, device=p.torch_device)
+                fl = flags if p.torch_device == sdev else torch.zeros(1, dtype=torch.int32, device=p.torch_device)
+                with torch.cuda.device(p.torch_device):
+                    K.mask(xs[ci], out, m.streams(peers), weight=ws[ci], weight_vec=wvecs[ci],
+                           compute_dtype=_NP2T[cts[ci]], fxp_bits=self._fxp_bits, digest=dig, flags=fl)
+                if fl is not flags:
+                    flags |= fl.to(sdev)
+                digests[ci] = dig.to(sdev)[0]
+                masked.append(out.to(sdev))   # the wire: masked vector to the server
+            with torch.cuda.device(sdev):
+                K.sum_u64(masked, s)
+            if self._keep_masked:
+                masked_keep.append(masked)
+        for ci, p in enumerate(parties):
+            self._maskers[p.party].consume(n)
+        digests_keep.append(digests)
+        return s

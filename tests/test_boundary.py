@@ -1,0 +1,111 @@
+"""The drop-in boundary on CPU: libsfl_sa.so loads, exports every symbol
+include/sfl_sa.h declares, its host-side setup math equals numpy, and the
+product package never reaches for the oracle or a CPU fallback."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import secagg as o
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    hdr = open(os.path.join(ROOT, "include", "sfl_sa.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(sa_\w+)\s*\(", hdr, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from sfl_amd import _lib as L
+
+    lib = L.lib()
+    declared = _declared()
+    assert len(declared) >= 15
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(declared) == set(L.EXPORTED)
+    assert lib.sa_abi_version() == 1
+
+
+def test_library_is_built_for_gfx950():
+    import subprocess
+
+    so = os.path.join(ROOT, "sfl_amd", "lib", "libsfl_sa.so")
+    out = subprocess.run(["/opt/rocm/bin/roc-obj-ls", so], capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("roc-obj-ls unavailable")
+    assert "gfx950" in out.stdout
+
+
+@pytest.mark.parametrize("seed", [0, 1, 42, o.pair_seed(0, 7), 2**63 + 11, 2**64, 2**127 + 5, 3**100])
+def test_seeding_matches_numpy(seed):
+    from sfl_amd import _lib as L
+
+    g = L.pcg64_from_seed(seed)
+    assert g.pair() == o.pcg64_state(seed)
+
+
+@pytest.mark.parametrize("delta", [0, 1, 3, 1023, 2**32 + 7, 2**70 + 1])
+def test_advance_and_host_draws_match_numpy(delta):
+    from sfl_amd import _lib as L
+
+    seed = o.pair_seed(2, 3)
+    g = L.pcg64_advance(L.pcg64_from_seed(seed), delta)
+    bg = np.random.PCG64(seed)
+    bg.advance(delta)
+    assert g.state.value() == bg.state["state"]["state"]
+    assert np.array_equal(L.pcg64_raw_host(g, 6), bg.random_raw(6))
+
+
+def test_errors_cross_the_abi_as_codes():
+    import ctypes as C
+
+    from sfl_amd import _lib as L
+
+    lib = L.lib()
+    rc = lib.sa_mask(None, 0, 0, 10, 1.0, None, 18, None, 0, None, None, None, None, None)
+    assert rc == L.SA_ERR_ARG
+    assert b"bad arguments" in lib.sa_last_error()
+    rc = lib.sa_sum_u64(None, 0, 10, None, None)
+    assert rc == L.SA_ERR_ARG
+    with pytest.raises(L.SALibraryError):
+        L.check(rc, "sa_sum_u64")
+    arr = (C.c_uint32 * 1)(5)
+    assert lib.sa_pcg64_from_seed(arr, -1, None) == L.SA_ERR_ARG
+
+
+def test_kernels_refuse_host_tensors():
+    import torch
+
+    from sfl_amd import kernels as K
+
+    with pytest.raises(ValueError):
+        K.sum_u64([torch.zeros(4, dtype=torch.int64)], torch.zeros(4, dtype=torch.int64))
+
+
+def test_product_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "sfl_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                src = open(os.path.join(dirpath, f)).read()
+                assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), f
+                assert "oracle/" not in src.replace("oracle/_ref", ""), f
+
+
+def test_missing_library_fails_loudly(tmp_path, monkeypatch):
+    import importlib
+
+    import sfl_amd._lib as L
+
+    monkeypatch.setenv("SFL_SA_LIB", str(tmp_path / "nope.so"))
+    L2 = importlib.reload(L)
+    try:
+        with pytest.raises(L2.SALibraryError):
+            L2.lib()
+    finally:
+        monkeypatch.delenv("SFL_SA_LIB")
+        importlib.reload(L)

@@ -1,0 +1,346 @@
+"""Parity of the HIP path (through the C-ABI) with the CPU oracle.
+
+Bar: bit-exact for every integer output (masked vectors, masked sums, XOR
+digests); decoded float64 equal to the oracle's float64 (same IEEE ops) and
+within C * 2^-fxp of the float sum (the quantization tolerance).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import secagg as o  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd import _lib as L
+
+    L.lib()
+
+
+def _K():
+    from sfl_amd import kernels as K
+
+    return K
+
+
+def _L():
+    from sfl_amd import _lib as L
+
+    return L
+
+
+def _streams(seeds, signs, offset):
+    L = _L()
+    return [(L.pcg64_advance(L.pcg64_from_seed(s), offset), sg, i) for i, (s, sg) in enumerate(zip(seeds, signs))]
+
+
+def _oracle_masked(q, seeds, signs, offset):
+    out = np.array(q, dtype=np.uint64).copy()
+    for s, sg in zip(seeds, signs):
+        m = o.mask_stream(s, out.size, offset)
+        out = out + m if sg > 0 else out - m
+    return out
+
+
+def _u64(t):
+    return _K().as_u64(t)
+
+
+# ---------------------------------------------------------------------------
+# single-client masking (sa_mask): the _Masker.mask replacement
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 37, 1023, 1024, 1025, 4100, 70001])
+@pytest.mark.parametrize("nstreams", [0, 1, 3, 7, 16, 17, 31])
+def test_mask_f32_bit_exact(n, nstreams):
+    K = _K()
+    rng = np.random.default_rng(n * 100 + nstreams)
+    x = (rng.standard_normal(n) * 5).astype(np.float32)
+    seeds = [o.pair_seed(0, j + 1) for j in range(nstreams)]
+    signs = [1 if j % 3 else -1 for j in range(nstreams)]
+    offset = int(rng.integers(0, 1 << 40))
+    exp = _oracle_masked(o.quantize(x), seeds, signs, offset)
+    xt = torch.from_numpy(x).to(DEV)
+    out = torch.empty(n, dtype=torch.int64, device=DEV)
+    dig = torch.zeros(1, dtype=torch.int64, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.mask(xt, out, _streams(seeds, signs, offset), digest=dig, flags=flags)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(out), exp)
+    assert int(_u64(dig)[0]) == o.digest(exp)
+    assert int(flags.item()) == 0
+
+
+@pytest.mark.parametrize("case", ["f64", "i64", "f32_wvec_f64", "f32_scalar_w", "f64_scalar_w", "i64_int_w",
+                                  "i64_float_w"])
+def test_mask_other_types(case):
+    K = _K()
+    n = 2053
+    rng = np.random.default_rng(11)
+    seeds = [o.pair_seed(1, j) for j in (0, 2, 3)]
+    signs = [-1, 1, 1]
+    w, wvec, ct = None, None, None
+    if case.startswith("f64"):
+        x = rng.standard_normal(n) * 100
+    elif case.startswith("i64"):
+        x = rng.integers(-(1 << 20), 1 << 20, n)
+    else:
+        x = (rng.standard_normal(n) * 3).astype(np.float32)
+    if case == "f32_wvec_f64":
+        w = rng.integers(1, 50, n)  # int64 array -> float64 arithmetic
+    elif case in ("f32_scalar_w", "f64_scalar_w"):
+        w = 0.3
+    elif case == "i64_int_w":
+        w = 7
+    elif case == "i64_float_w":
+        w = 0.25
+    q = o.quantize(x, w)
+    ctype = {np.float32: torch.float32, np.float64: torch.float64, np.int64: torch.int64}
+    cdt = (np.zeros(1, x.dtype) * (w if np.ndim(w) == 0 or w is None else np.zeros(1, np.asarray(w).dtype))).dtype \
+        if w is not None else x.dtype
+    ct = ctype[cdt.type]
+    if w is not None and np.ndim(w):
+        wvec = torch.from_numpy(np.asarray(w).astype(cdt)).to(DEV)
+    exp = _oracle_masked(q, seeds, signs, 17)
+    out = torch.empty(n, dtype=torch.int64, device=DEV)
+    K.mask(torch.from_numpy(x).to(DEV), out, _streams(seeds, signs, 17),
+           weight=1.0 if w is None or np.ndim(w) else w, weight_vec=wvec, compute_dtype=ct)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(out), exp)
+
+
+def test_quantize_edge_cases_bit_exact(golden_dir):
+    K = _K()
+    g = np.load(f"{golden_dir}/secagg_small.npz")
+    for key in ("f32", "f64"):
+        x = g[f"q_in_{key}"]
+        out = torch.empty(x.size, dtype=torch.int64, device=DEV)
+        K.mask(torch.from_numpy(x).to(DEV), out, [])
+        torch.cuda.synchronize()
+        assert np.array_equal(_u64(out), g[f"q_out_{key}"]), key
+
+
+def test_golden_round_from_fixture(golden_dir):
+    """3 parties, n=37, second round (offset 5): masked vectors, sum, decode."""
+    K, L = _K(), _L()
+    g = np.load(f"{golden_dir}/secagg_small.npz")
+    names = ["alice", "bob", "carol"]
+    seeds = o.seeds_for(names)
+    off = int(g["round_offset"])
+    n = g["round_x"].shape[1]
+    masked = []
+    for i, name in enumerate(names):
+        peers = [p for p in names if p != name]
+        st = [(L.pcg64_advance(L.pcg64_from_seed(seeds[name][p]), off), 1 if p > name else -1, j)
+              for j, p in enumerate(peers)]
+        out = torch.empty(n, dtype=torch.int64, device=DEV)
+        K.mask(torch.from_numpy(g["round_x"][i]).to(DEV), out, st)
+        masked.append(out)
+    s = K.sum_u64(masked, torch.empty(n, dtype=torch.int64, device=DEV))
+    dec = K.decode(s, torch.empty(n, dtype=torch.float64, device=DEV))
+    torch.cuda.synchronize()
+    assert np.array_equal(np.stack([_u64(m) for m in masked]), g["round_masked"])
+    assert np.array_equal(_u64(s), g["round_sum"])
+    assert np.array_equal(dec.cpu().numpy(), g["round_decoded"])
+
+
+# ---------------------------------------------------------------------------
+# fused co-located clients (sa_fused_clients)
+# ---------------------------------------------------------------------------
+def _fused_setup(C, n, offset, seed=0):
+    L = _L()
+    rng = np.random.default_rng(seed + C * 1000 + n)
+    names = [f"party{c:02d}" for c in range(C)][::-1] if C % 2 else [f"party{c:02d}" for c in range(C)]
+    xs = [(rng.standard_normal(n) * 0.01).astype(np.float32) for _ in range(C)]
+    seeds = o.seeds_for(names)
+    pair_gens, pair_signs = [], []
+    for u in range(C):
+        for v in range(u + 1, C):
+            pair_gens.append(L.pcg64_advance(L.pcg64_from_seed(seeds[names[u]][names[v]]), offset))
+            pair_signs.append(1 if names[v] > names[u] else -1)
+    return names, xs, seeds, pair_gens, pair_signs
+
+
+@pytest.mark.parametrize("C", [2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("n", [5, 1024, 4099, 100003])
+def test_fused_clients_bit_exact(C, n):
+    K = _K()
+    offset = 3 * n
+    names, xs, seeds, pg, ps = _fused_setup(C, n, offset)
+    masked = o.secure_masked(xs, names, seeds=seeds, offset=offset)
+    s_exp = o.server_sum(masked)
+    xt = [torch.from_numpy(x).to(DEV) for x in xs]
+    s = torch.empty(n, dtype=torch.int64, device=DEV)
+    dig = torch.zeros(C, dtype=torch.int64, device=DEV)
+    mo = [torch.empty(n, dtype=torch.int64, device=DEV) for _ in range(C)]
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.fused_clients(xt, [1.0] * C, pg, ps, [], 0, s, digests=dig, flags=flags, masked_outs=mo)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(s), s_exp)
+    for c in range(C):
+        assert np.array_equal(_u64(mo[c]), masked[c]), c
+    assert [int(v) for v in _u64(dig)] == [o.digest(m) for m in masked]
+    assert int(flags.item()) == 0
+    dec = K.decode(s, torch.empty(n, dtype=torch.float64, device=DEV))
+    ref = o.decode(s_exp)
+    assert np.array_equal(dec.cpu().numpy(), ref)
+    assert np.abs(ref - np.sum(np.stack(xs).astype(np.float64), axis=0)).max() < C * 2.0**-18
+
+
+def test_fused_accumulate_and_weights():
+    K = _K()
+    C, n = 4, 3001
+    names, xs, seeds, pg, ps = _fused_setup(C, n, 0, seed=5)
+    w = [128.0 * (c + 1) for c in range(C)]
+    masked = o.secure_masked(xs, names, weights=[int(v) for v in w], seeds=seeds)
+    exp = o.server_sum(masked)
+    base = np.random.default_rng(1).integers(0, 2**63, n).astype(np.uint64)
+    s = torch.from_numpy(base.view(np.int64).copy()).to(DEV)
+    K.fused_clients([torch.from_numpy(x).to(DEV) for x in xs], w, pg, ps, [], 0, s, accumulate=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(s), base + exp)
+
+
+def test_fused_with_cross_streams_matches_per_client():
+    """Shape of one GPU of a 2-GPU split: 2 local clients of 4, 2 cross
+    streams each -- equals the sum of those clients' masked vectors."""
+    K, L = _K(), _L()
+    n = 9999
+    names = ["a", "b", "c", "d"]
+    seeds = o.seeds_for(names)
+    rng = np.random.default_rng(3)
+    xs = [(rng.standard_normal(n)).astype(np.float32) for _ in names]
+    masked = o.secure_masked(xs, names, seeds=seeds, offset=11)
+    local = [0, 1]
+    pg = [L.pcg64_advance(L.pcg64_from_seed(seeds["a"]["b"]), 11)]
+    ps = [1]
+    cross = []
+    for u in local:
+        for p in ("c", "d"):
+            cross.append((L.pcg64_advance(L.pcg64_from_seed(seeds[names[u]][p]), 11),
+                          1 if p > names[u] else -1, 0))
+    s = torch.empty(n, dtype=torch.int64, device=DEV)
+    dig = torch.zeros(2, dtype=torch.int64, device=DEV)
+    K.fused_clients([torch.from_numpy(xs[u]).to(DEV) for u in local], [1.0, 1.0], pg, ps, cross, 2, s,
+                    digests=dig)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(s), masked[0] + masked[1])
+    assert [int(v) for v in _u64(dig)] == [o.digest(masked[0]), o.digest(masked[1])]
+
+
+# ---------------------------------------------------------------------------
+# server kernels
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("k", [1, 2, 8, 33, 70])
+@pytest.mark.parametrize("n", [1, 2, 7, 4096, 12345])
+def test_sum_u64(k, n):
+    K = _K()
+    rng = np.random.default_rng(k * n)
+    ins = [rng.integers(0, 2**64 - 1, n, dtype=np.uint64) for _ in range(k)]
+    ts = [torch.from_numpy(a.view(np.int64).copy()).to(DEV) for a in ins]
+    out = K.sum_u64(ts, torch.empty(n, dtype=torch.int64, device=DEV))
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(out), o.server_sum(ins))
+
+
+def test_decode_and_divisors():
+    K = _K()
+    n = 5003
+    rng = np.random.default_rng(9)
+    s = rng.integers(0, 2**64 - 1, n, dtype=np.uint64)
+    s[:4] = [0, 2**63, 2**63 - 1, 2**64 - 1]
+    st = torch.from_numpy(s.view(np.int64).copy()).to(DEV)
+    for div in (1.0, 3.0, 640.0, 0.1):
+        out = K.decode(st, torch.empty(n, dtype=torch.float64, device=DEV), divisor=div)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), o.decode(s, 18, div if div != 1.0 else None)), div
+    dv = rng.integers(1, 100, n).astype(np.float64)
+    out = K.decode(st, torch.empty(n, dtype=torch.float64, device=DEV), divisor_vec=torch.from_numpy(dv).to(DEV))
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), o.decode(s, 18, dv))
+
+
+def test_prg_zero_draw_is_flagged():
+    """Force a raw PCG64 draw of 0 (hi == lo after the step) at element 5:
+    numpy's Lemire bounded draw would reject it, so the kernel must flag."""
+    K, L = _K(), _L()
+    A = o.PCG64_MULT
+    M = (1 << 128) - 1
+    inc = (12345 << 1) | 1
+    target = (0xDEADBEEF << 64) | 0xDEADBEEF  # hi == lo -> xsl-rr output 0
+    ainv = pow(A, -1, 1 << 128)
+    s = ((target - inc) * ainv) & M  # state before the draw that yields 0
+    # walk back 5 steps so the zero lands on element 5
+    for _ in range(5):
+        s = ((s - inc) * ainv) & M
+    g = L.PCG64.of(s, inc)
+    assert o.pcg64_raw_py(s, inc, 6)[5] == 0
+    out = torch.empty(64, dtype=torch.int64, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.mask(torch.zeros(64, device=DEV), out, [(g, 1, 0)], flags=flags)
+    torch.cuda.synchronize()
+    assert int(flags.item()) & L.SA_FLAG_PRG_REJECT
+
+
+# ---------------------------------------------------------------------------
+# full-size properties (BASELINE configs): too big for the oracle, so check
+# mask cancellation, fused == per-client (wire) path, and oracle spot checks
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("C,n", [(4, 10_000_000), (8, 20_000_000)])
+def test_full_size_properties(C, n):
+    K, L = _K(), _L()
+    names = [f"client{c}" for c in range(C)]
+    seeds = o.seeds_for(names)
+    xs = [torch.randn(n, device=DEV, dtype=torch.float32) * 1e-2 for _ in range(C)]
+    pg, ps = [], []
+    for u in range(C):
+        for v in range(u + 1, C):
+            pg.append(L.pcg64_from_seed(seeds[names[u]][names[v]]))
+            ps.append(1 if names[v] > names[u] else -1)
+    s = torch.empty(n, dtype=torch.int64, device=DEV)
+    dig = torch.zeros(C, dtype=torch.int64, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.fused_clients(xs, [1.0] * C, pg, ps, [], 0, s, digests=dig, flags=flags)
+    # (1) masks cancel: sum of unmasked quantized vectors
+    q_sum = torch.zeros(n, dtype=torch.int64, device=DEV)
+    qbuf = torch.empty(n, dtype=torch.int64, device=DEV)
+    for x in xs:
+        K.mask(x, qbuf, [], sum_accum=q_sum)
+    # (2) the wire path: each client's masked vector, then the server sum
+    wire = []
+    wdig = torch.zeros(C, dtype=torch.int64, device=DEV)
+    for c in range(C):
+        st = [(L.pcg64_from_seed(seeds[names[c]][p]), 1 if p > names[c] else -1, j)
+              for j, p in enumerate(q for q in names if q != names[c])]
+        out = torch.empty(n, dtype=torch.int64, device=DEV)
+        K.mask(xs[c], out, st, digest=wdig[c:c + 1])
+        wire.append(out)
+    s2 = K.sum_u64(wire, torch.empty(n, dtype=torch.int64, device=DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(s, q_sum)
+    assert torch.equal(s, s2)
+    assert torch.equal(dig, wdig)
+    assert int(flags.item()) == 0
+    # (3) oracle spot checks of individual masked elements at far offsets
+    rng = np.random.default_rng(0)
+    idx = np.concatenate([[0, 1, n - 1], rng.integers(0, n, 20)])
+    xh = [x[idx].cpu().numpy() for x in xs]
+    for c in range(C):
+        got = _u64(wire[c][idx])
+        for t, i in enumerate(idx):
+            v = int(o.quantize(xh[c][t:t + 1])[0])
+            for p in names:
+                if p != names[c]:
+                    m = int(o.mask_stream(seeds[names[c]][p], 1, int(i))[0])
+                    v = (v + m) & o.U64 if p > names[c] else (v - m) & o.U64
+            assert int(got[t]) == v
+    # (4) decoded sum within C * 2^-18 of the float sum
+    dec = K.decode(s, torch.empty(n, dtype=torch.float64, device=DEV))
+    fsum = torch.stack(xs).double().sum(0)
+    assert float((dec - fsum).abs().max()) < C * 2.0**-18
