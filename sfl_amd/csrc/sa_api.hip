@@ -226,7 +226,7 @@ extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, i
   a.scale_f = (float)a.scale_d;
   uint64_t bias[kMaxLocal] = {0};
   for (int c = 0; c < L; c++) {
-    if (!clients[c].x || !aligned16(clients[c].x) || !aligned16(clients[c].masked_out)) {
+    if (!clients[c].x || !aligned16(clients[c].x) || ((uintptr_t)clients[c].masked_out & 7)) {
       sa_set_error("sa_fused_clients: client %d x null or buffers not 16-byte aligned", c);
       return SA_ERR_ARG;
     }

@@ -98,6 +98,62 @@ __device__ __forceinline__ void store4_u64(uint64_t* __restrict__ p, uint64_t i,
   }
 }
 
+// Raw buffer descriptors (SGPR, built from kernel arguments only, so hipcc
+// can prove them wave-uniform) + a 32-bit per-lane byte offset: one shared
+// offset VGPR serves every client instead of a 64-bit address per client.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint64_t bytes) {
+  const int nrec = bytes > 0xFFFFFFF0ull ? (int)0xFFFFFFF0u : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, nrec, 0x00020000);
+}
+
+template <typename T>
+__device__ __forceinline__ Vec4<T> bload4(rsrc_t r, uint64_t i, uint64_t n) {
+  Vec4<T> out;
+  const int off = (int)(i * sizeof(T));
+  if (i + 4 <= n) {
+    if constexpr (sizeof(T) == 4) {
+      const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+#pragma unroll
+      for (int k = 0; k < 4; k++) out.v[k] = __builtin_bit_cast(T, (uint32_t)u[k]);
+    } else {
+      const auto u0 = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+      const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0);
+      out.v[0] = __builtin_bit_cast(T, (uint64_t)u0[0] | ((uint64_t)u0[1] << 32));
+      out.v[1] = __builtin_bit_cast(T, (uint64_t)u0[2] | ((uint64_t)u0[3] << 32));
+      out.v[2] = __builtin_bit_cast(T, (uint64_t)u1[0] | ((uint64_t)u1[1] << 32));
+      out.v[3] = __builtin_bit_cast(T, (uint64_t)u1[2] | ((uint64_t)u1[3] << 32));
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (i + k < n) {
+        if constexpr (sizeof(T) == 4) {
+          out.v[k] = __builtin_bit_cast(T, (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * k, 0, 0));
+        } else {
+          const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off + 8 * k, 0, 0);
+          out.v[k] = __builtin_bit_cast(T, (uint64_t)u[0] | ((uint64_t)u[1] << 32));
+        }
+      } else {
+        out.v[k] = T(0);
+      }
+    }
+  }
+  return out;
+}
+
+__device__ __forceinline__ uint64_t bload_u64(rsrc_t r, uint64_t i) {
+  const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8), 0, 0);
+  return (uint64_t)u[0] | ((uint64_t)u[1] << 32);
+}
+__device__ __forceinline__ void bstore_u64(rsrc_t r, uint64_t i, uint64_t v) {
+  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+  v2u d;
+  d[0] = (uint32_t)v;
+  d[1] = (uint32_t)(v >> 32);
+  __builtin_amdgcn_raw_buffer_store_b64(d, r, (int)(i * 8), 0, 0);
+}
+
 // float -> int64 truncation with x86 "integer indefinite" semantics
 // (NaN / inf / |v| >= 2^63 -> INT64_MIN), i.e. numpy's astype(int64) on x86-64.
 __device__ __forceinline__ uint64_t trunc_i64(float v) {
@@ -143,14 +199,6 @@ __device__ __forceinline__ uint64_t draw_signed(u128 s, uint64_t smask) {
   const unsigned r = (unsigned)(hi >> 58);
   return __builtin_rotateright64(x, r);
 }
-
-// Streams whose draws the scheduler may interleave inside one tile; a
-// scheduling fence after each group bounds the live temporaries (unfenced,
-// hipcc issues every stream's constant loads up front and spills past ~9).
-#ifndef SA_SCHED_GROUP
-#define SA_SCHED_GROUP 2
-#endif
-constexpr int kSchedGroup = SA_SCHED_GROUP;
 
 struct StreamLds {
   uint64_t inc_lo, inc_hi, cj_lo, cj_hi, smask, pad;
@@ -199,16 +247,37 @@ struct Pairs {
 // ----------------------------------------------------------------------------
 // the kernel
 // ----------------------------------------------------------------------------
+// Elements per lane per chunk.  A lane walks its run in steps of 4 (one 16-B
+// load per client per step; lanes kRun*4 bytes apart, so each load
+// instruction touches 64 lines that later steps finish consuming), and jumps
+// its streams once per run: the jump costs one multiply-add like a draw, so
+// kRun=4 (fully coalesced) pays 1 extra step per 4 draws, kRun=16 1 per 16.
+#ifndef SA_RUN
+#define SA_RUN 8
+#endif
+constexpr int kRun = SA_RUN;
+// Streams whose draws may interleave between two fences (ILP inside a wave;
+// more streams = more live temporaries).
+#ifndef SA_GROUP
+#define SA_GROUP 1
+#endif
+constexpr int kGroup = SA_GROUP;
+static_assert(kRun % 4 == 0, "run is a multiple of the 4-element step");
+
 template <typename XT, typename CT, int L, int X>
 __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
   constexpr int PI = Pairs<L>::count;
   constexpr int P = PI + L * X;
+  constexpr bool kGeneral = (L == 1);  // continue mode + per-element weights
   static_assert(L >= 1 && L <= kMaxLocal, "L");
   static_assert(P <= kMaxStreams, "P");
 
   const uint64_t n = a.n;
-  const uint64_t first = (uint64_t)blockIdx.x * kTileElems + (uint64_t)threadIdx.x * kElemsPerLane;
-  const uint64_t stride = (uint64_t)gridDim.x * kTileElems;
+  // lane owns a run of kRun consecutive elements per chunk (draw order), the
+  // block a chunk of 256*kRun; the grid strides over chunks.
+  constexpr uint64_t kChunk = (uint64_t)kBlockThreads * kRun;
+  const uint64_t first = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kRun;
+  const uint64_t stride = (uint64_t)gridDim.x * kChunk;
 
   // ---- per-stream constants go to LDS once; the tile loop re-reads them
   // right before each use (a compiler barrier stops LICM from hoisting 7
@@ -238,121 +307,141 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
   }
   const u128 AJ = ld128(a.aj_lo, a.aj_hi);
 
-  uint64_t dig[L];
-#pragma unroll
-  for (int c = 0; c < L; c++) dig[c] = 0;
   uint64_t badmask = 0;  // lanes that saw a raw PCG64 draw of 0 (SGPR pair)
 
-  lds_ptr slp = (lds_ptr)(sl);
-  for (uint64_t i = first; i < n; i += stride) {
-    // Opaque per tile: the stream constants are re-read from LDS (broadcast
-    // ds_read) inside the tile instead of being hoisted into 7*P registers.
-    asm volatile("" : "+v"(slp));
+  // per-lane XOR digests live in LDS (one lane-private slot per client):
+  // ds_xor_b64 per finished element instead of 2 VGPRs per client
+  __shared__ uint64_t dig_lds[L][kBlockThreads];
+#pragma unroll
+  for (int c = 0; c < L; c++) dig_lds[c][threadIdx.x] = 0;
 
-    // ---- issue this tile's loads early; consumed after the PRG work
+  rsrc_t rx[L], rw[kGeneral ? L : 1], rm[L];
+#pragma unroll
+  for (int c = 0; c < L; c++) {
+    rx[c] = make_rsrc(a.c[c].x, n * sizeof(XT));
+    rm[c] = make_rsrc(a.c[c].masked_out, n * 8);
+    if constexpr (kGeneral) rw[c] = make_rsrc(a.c[c].wvec, n * sizeof(CT));
+  }
+  const rsrc_t rs = make_rsrc(a.sum_out, n * 8);
+
+  lds_ptr slp = (lds_ptr)(sl);
+  for (uint64_t run0 = first; run0 < n; run0 += stride) {
+#pragma unroll 1
+   for (int step = 0; step < kRun / 4; step++) {
+    const uint64_t i = run0 + 4 * (uint64_t)step;
+    // ---- issue this step's loads early; consumed as each element finishes
+    // (continue mode and per-element weights exist only for the single-client
+    // kernel; the fused kernel drops them at compile time to save registers)
     Vec4<XT> xv[L];
-    Vec4<CT> wv[L];
-    uint64_t acc[L][4];
+    Vec4<CT> wv[kGeneral ? L : 1];
+    Vec4<uint64_t> pv[kGeneral ? L : 1];
 #pragma unroll
     for (int c = 0; c < L; c++) {
-      if (a.continue_mode) {
-        const Vec4<uint64_t> p = load4<uint64_t>(a.c[c].masked_out, i, n);
-#pragma unroll
-        for (int k = 0; k < 4; k++) acc[c][k] = p.v[k] + a.c[c].bias;
+      if (kGeneral && a.continue_mode) {
+        pv[c] = bload4<uint64_t>(rm[c], i, n);
       } else {
-        xv[c] = load4<XT>(reinterpret_cast<const XT*>(a.c[c].x), i, n);
-        if (a.c[c].wvec) wv[c] = load4<CT>(reinterpret_cast<const CT*>(a.c[c].wvec), i, n);
-#pragma unroll
-        for (int k = 0; k < 4; k++) acc[c][k] = a.c[c].bias;
+        xv[c] = bload4<XT>(rx[c], i, n);
+        if (kGeneral && a.c[c].wvec) wv[c] = bload4<CT>(rw[kGeneral ? c : 0], i, n);
       }
     }
 
-    // ---- mask expansion, stream-outer: each stream's 4 draws back to back,
-    // then its jump to the next tile.  Streams are processed in groups of
-    // kSchedGroup; empty volatile asm statements on the group's states (in)
-    // and on its states + accumulators (out) pin the order, so only one
-    // group's constants and temporaries are live at a time (left alone,
-    // hipcc re-interleaves every stream per element and spills past ~9).
-    if constexpr (P > 0) {
+    // ---- element-outer: one draw per stream per element.  Each stream's
+    // step is fenced (empty volatile asm on its state, the LDS pointer and
+    // the accumulators it touches), so only one stream's constants and
+    // temporaries are live at a time: P*4 state VGPRs + L accumulators.
 #pragma unroll
-      for (int g0 = 0; g0 < P; g0 += kSchedGroup) {
-        constexpr int G = kSchedGroup;
-        uint64_t slo[G], shi[G];
+    for (int k = 0; k < 4; k++) {
+      uint64_t acc[L];
 #pragma unroll
-        for (int g = 0; g < G; g++) {
-          slo[g] = g0 + g < P ? lo64(st[g0 + g]) : 0;
-          shi[g] = g0 + g < P ? hi64(st[g0 + g]) : 0;
-        }
-        if constexpr (G == 1)
-          asm volatile("" : "+v"(slo[0]), "+v"(shi[0]), "+v"(slp));
-        else
-          asm volatile("" : "+v"(slo[0]), "+v"(shi[0]), "+v"(slo[1]), "+v"(shi[1]), "+v"(slp));
+      for (int c = 0; c < L; c++) acc[c] = a.c[c].bias;
+      if constexpr (P > 0) {
 #pragma unroll
-        for (int g = 0; g < G; g++) {
-          const int q = g0 + g;
-          if (q >= P) break;
-          const StreamLds c = read_stream(slp, q);
-          const u128 inc = ld128(c.inc_lo, c.inc_hi);
-          u128 sv = mk128(shi[g], slo[g]);
+        for (int g0 = 0; g0 < P; g0 += kGroup) {
+          // fence in: the group's states and the LDS pointer (ordered after
+          // the previous group's fence out), then the group's draws are free
+          // to interleave (ILP), then fence out states + accumulators.
+          uint64_t slo[kGroup], shi[kGroup], t[kGroup];
 #pragma unroll
-          for (int k = 0; k < 4; k++) {
-            sv = sv * kPcgMult + inc;
-            note_zero_draw(badmask, sv);
-            const uint64_t t = draw_signed(sv, c.smask);
-            if (q < PI) {  // internal pair: one draw, two clients
-              acc[Pairs<L>::u(q)][k] += t;
-              acc[Pairs<L>::v(q)][k] -= t;
-            } else {  // cross-GPU peer: one client
-              acc[(q - PI) / (X > 0 ? X : 1)][k] += t;
+          for (int g = 0; g < kGroup; g++) {
+            if (g0 + g < P) {
+              slo[g] = lo64(st[g0 + g]);
+              shi[g] = hi64(st[g0 + g]);
+              asm volatile("" : "+v"(slo[g]), "+v"(shi[g]), "+v"(slp));
             }
           }
-          sv = sv * AJ + ld128(c.cj_lo, c.cj_hi);
-          slo[g] = lo64(sv);
-          shi[g] = hi64(sv);
-        }
-        // fence out: this group's states and every accumulator it touched
 #pragma unroll
-        for (int g = 0; g < G; g++) {
-          const int q = g0 + g;
-          if (q >= P) break;
-          const int cu = q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1);
-          const int cv = q < PI ? Pairs<L>::v(q) : cu;
-          asm volatile("" : "+v"(slo[g]), "+v"(shi[g]), "+v"(acc[cu][0]), "+v"(acc[cu][1]),
-                       "+v"(acc[cu][2]), "+v"(acc[cu][3]), "+v"(acc[cv][0]), "+v"(acc[cv][1]),
-                       "+v"(acc[cv][2]), "+v"(acc[cv][3]));
-          st[q] = mk128(shi[g], slo[g]);
+          for (int g = 0; g < kGroup; g++) {
+            const int q = g0 + g;
+            if (q < P) {
+              const uint64_t inc_lo = slp[q].inc_lo, inc_hi = slp[q].inc_hi, smask = slp[q].smask;
+              const u128 sv = mk128(shi[g], slo[g]) * kPcgMult + mk128(inc_hi, inc_lo);
+              note_zero_draw(badmask, sv);
+              t[g] = draw_signed(sv, smask);
+              slo[g] = lo64(sv);
+              shi[g] = hi64(sv);
+              const int cu = q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1);
+              const int cv = q < PI ? Pairs<L>::v(q) : cu;
+              acc[cu] += t[g];
+              if (q < PI) acc[cv] -= t[g];
+            }
+          }
+#pragma unroll
+          for (int g = 0; g < kGroup; g++) {
+            const int q = g0 + g;
+            if (q < P) {
+              const int cu = q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1);
+              const int cv = q < PI ? Pairs<L>::v(q) : cu;
+              asm volatile("" : "+v"(slo[g]), "+v"(shi[g]), "+v"(acc[cu]), "+v"(acc[cv]));
+              st[q] = mk128(shi[g], slo[g]);
+            }
+          }
         }
       }
+      // ---- finish element k: add the quantized value (or the prior pass)
+      uint64_t s_k = 0;
+#pragma unroll
+      for (int c = 0; c < L; c++) {
+        if (kGeneral && a.continue_mode) {
+          acc[c] += pv[kGeneral ? c : 0].v[k];
+        } else {
+          const CT w = (kGeneral && a.c[c].wvec) ? wv[kGeneral ? c : 0].v[k] : scalar_weight<CT>(a.c[c]);
+          acc[c] += quantize<XT, CT>(xv[c].v[k], w, a);
+        }
+        s_k += acc[c];
+        if (i + k < n) {
+          __hip_atomic_fetch_xor(&dig_lds[c][threadIdx.x], acc[c], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (a.c[c].masked_out) bstore_u64(rm[c], i + k, acc[c]);
+        }
+      }
+      // the element's masked sum (8-B store; a lane's run fills whole lines)
+      if (a.sum_mode != 0 && i + k < n) {
+        if (a.sum_mode == 2) s_k += bload_u64(rs, i + k);
+        bstore_u64(rs, i + k, s_k);
+      }
     }
+   }
 
-    // ---- finish: add the quantized values, digest, sum, store
-    uint64_t sum[4] = {0, 0, 0, 0};
+    // ---- jump every stream to this lane's next run (same fencing)
+    if constexpr (P > 0) {
 #pragma unroll
-    for (int c = 0; c < L; c++) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        if (!a.continue_mode) {
-          const CT w = a.c[c].wvec ? wv[c].v[k] : scalar_weight<CT>(a.c[c]);
-          acc[c][k] += quantize<XT, CT>(xv[c].v[k], w, a);
-        }
-        sum[k] += acc[c][k];
-        if (i + k < n) dig[c] ^= acc[c][k];
+      for (int q = 0; q < P; q++) {
+        uint64_t slo = lo64(st[q]), shi = hi64(st[q]);
+        asm volatile("" : "+v"(slo), "+v"(shi), "+v"(slp));
+        const u128 sv = mk128(shi, slo) * AJ + mk128(slp[q].cj_hi, slp[q].cj_lo);
+        slo = lo64(sv);
+        shi = hi64(sv);
+        asm volatile("" : "+v"(slo), "+v"(shi));
+        st[q] = mk128(shi, slo);
       }
-      if (a.c[c].masked_out) store4_u64(a.c[c].masked_out, i, n, acc[c]);
     }
-    if (a.sum_mode == 2) {
-      const Vec4<uint64_t> o = load4<uint64_t>(a.sum_out, i, n);
-#pragma unroll
-      for (int k = 0; k < 4; k++) sum[k] += o.v[k];
-    }
-    if (a.sum_mode != 0) store4_u64(a.sum_out, i, n, sum);
   }
 
   // ---- wave-level XOR reduction of the digests, one atomic per wave
   if (a.do_digest) {
 #pragma unroll
     for (int c = 0; c < L; c++) {
-      uint64_t d = dig[c];
+      uint64_t d = dig_lds[c][threadIdx.x];
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) d ^= __shfl_xor(d, off, 64);
       if ((threadIdx.x & 63) == 0 && d) atomicXor((unsigned long long*)&a.digests[c], d);
@@ -372,11 +461,11 @@ int launch_clients(const KArgs& in, void* stream) {
   const void* kfn = reinterpret_cast<const void*>(&k_clients<XT, CT, L, X>);
   const int maxb = occupancy_blocks(kfn);
   if (maxb <= 0) return SA_ERR_HIP;
-  const uint64_t tiles = (in.n + kTileElems - 1) / kTileElems;
+  const uint64_t tiles = (in.n + (uint64_t)kBlockThreads * kRun - 1) / ((uint64_t)kBlockThreads * kRun);
   const int grid = (int)(tiles < (uint64_t)maxb ? tiles : (uint64_t)maxb);
   KArgs a = in;
-  // per-tile jump J = grid*1024 - 4 draws (the lane already consumed 4)
-  const Jump jj = jump_of((uint64_t)grid * kTileElems - kElemsPerLane);
+  // per-run jump J = grid*256*kRun - kRun draws (the lane consumed its run)
+  const Jump jj = jump_of((uint64_t)grid * kBlockThreads * kRun - kRun);
   a.aj_lo = lo64(jj.mult);
   a.aj_hi = hi64(jj.mult);
   for (int j = 0; j < P; j++) {

@@ -1,0 +1,94 @@
+"""The multi-GPU path's host logic on CPU with world_size 2 over gloo.
+
+Each rank takes its block of clients (sfl_amd.parallel_sum.plan_rank), builds
+exactly the streams its fused launch would expand (internal pairs once, cross
+streams per client), emulates that launch with the oracle (CPU checker), and
+the uint64 partial sums are reduced to rank 0 with torch.distributed (the
+role RCCL plays on the GPUs).  Rank 0 compares with the oracle's full
+server sum: the sharding must lose or double no mask.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, C, n, q):
+    import torch
+
+    from oracle import secagg as o
+    from sfl_amd.parallel_sum import client_shard, plan_rank
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    names = [f"client{c}" for c in range(C)][::-1]  # names not in index order: signs matter
+    rng = np.random.default_rng(0)
+    xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
+    seeds = o.seeds_for(names)
+    plan = plan_rank(names, world, rank)
+    assert plan.clients == client_shard(C, world, rank)
+    local = {u: o.quantize(xs[u]).copy() for u in plan.clients}
+    for (u, v), s in zip(plan.pairs, plan.pair_signs):
+        m = o.mask_stream(seeds[names[u]][names[v]], n)
+        local[u] = local[u] + m if s > 0 else local[u] - m
+        local[v] = local[v] - m if s > 0 else local[v] + m
+    for (u, v, s) in plan.cross:
+        m = o.mask_stream(seeds[names[u]][names[v]], n)
+        local[u] = local[u] + m if s > 0 else local[u] - m
+    ref = o.secure_masked(xs, names, seeds=seeds)
+    ok_clients = all(np.array_equal(local[u], ref[u]) for u in plan.clients)
+    part = np.zeros(n, dtype=np.uint64)
+    for u in plan.clients:
+        part += local[u]
+    t = torch.from_numpy(part.view(np.int64).copy())
+    dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)  # int64 add wraps like uint64
+    if rank == 0:
+        full = o.server_sum(ref)
+        q.put((ok_clients, bool(np.array_equal(t.numpy().view(np.uint64), full))))
+    else:
+        q.put((ok_clients, True))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("C", [4, 8])
+def test_sharded_masked_sum_world2(C):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, C, 777, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(a for a, _ in res), "per-client masked vectors differ from the oracle"
+    assert all(b for _, b in res), "reduced masked sum differs from the oracle"
+
+
+def test_plan_covers_every_pair_once():
+    from sfl_amd.parallel_sum import plan_rank
+
+    for C, W in [(8, 1), (8, 2), (8, 4), (8, 8), (32, 8), (4, 2)]:
+        names = [f"p{c}" for c in range(C)]
+        seen = {}
+        for r in range(W):
+            p = plan_rank(names, W, r)
+            assert p.n_cross == C - C // W
+            for u, v in p.pairs:
+                seen[(u, v)] = seen.get((u, v), 0) + 2  # both ends applied in one launch
+            for u, v, s in p.cross:
+                seen[(min(u, v), max(u, v))] = seen.get((min(u, v), max(u, v)), 0) + 1
+                assert s == (1 if names[v] > names[u] else -1)
+        assert len(seen) == C * (C - 1) // 2 and all(c == 2 for c in seen.values())
