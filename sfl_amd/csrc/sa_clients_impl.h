@@ -38,6 +38,13 @@
 
 namespace sa {
 
+// Tuning-only ablations (results are WRONG when nonzero; never shipped):
+// 1 = no zero-draw check, 2 = no quantize conversion, 8 = no global
+// loads/stores, 16 = stream constants as immediates (no LDS reads).
+#ifndef SA_ABLATE
+#define SA_ABLATE 0
+#endif
+
 struct PowTable {
   Jump e[64];
 };
@@ -142,6 +149,26 @@ __device__ __forceinline__ Vec4<T> bload4(rsrc_t r, uint64_t i, uint64_t n) {
   return out;
 }
 
+__device__ __forceinline__ void bstore4_u64(rsrc_t r, uint64_t i, uint64_t n, const uint64_t (&v)[4]) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+  const int off = (int)(i * 8);
+  if (i + 4 <= n) {
+    const v4u d0 = {(uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32)};
+    const v4u d1 = {(uint32_t)v[2], (uint32_t)(v[2] >> 32), (uint32_t)v[3], (uint32_t)(v[3] >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(d0, r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(d1, r, off + 16, 0, 0);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (i + k < n) {
+        const v2u d = {(uint32_t)v[k], (uint32_t)(v[k] >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b64(d, r, off + 8 * k, 0, 0);
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ uint64_t bload_u64(rsrc_t r, uint64_t i) {
   const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8), 0, 0);
   return (uint64_t)u[0] | ((uint64_t)u[1] << 32);
@@ -193,11 +220,37 @@ __device__ __forceinline__ CT scalar_weight(const ClientArg& c) {
 __device__ __forceinline__ u128 ld128(uint64_t lo, uint64_t hi) { return mk128(hi, lo); }
 
 // XSL-RR of the state with the stream's sign mask folded into the XOR.
-__device__ __forceinline__ uint64_t draw_signed(u128 s, uint64_t smask) {
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 v = {lo, hi};
+  return __builtin_bit_cast(uint64_t, v);
+}
+// XSL-RR output of state s with the sign mask m (0 / ~0) folded into the
+// XOR (it commutes with the rotation).  32-bit form: two 3-input XORs
+// (v_bitop3, gfx950) and a funnel-shift rotation (two v_alignbit + a swap
+// when r >= 32), all full-rate, where the 64-bit shifts of the generic form
+// issue at half rate.  Also folds the raw==0 test (raw == 0 <=> hi == lo <=>
+// xl == xh == m, a 3-input "all equal" LUT) into a running per-lane minimum.
+__device__ __forceinline__ uint64_t draw_signed(u128 s, uint32_t m, uint32_t& zmin) {
   const uint64_t hi = hi64(s), lo = lo64(s);
-  const uint64_t x = hi ^ lo ^ smask;
-  const unsigned r = (unsigned)(hi >> 58);
-  return __builtin_rotateright64(x, r);
+  const uint32_t s3 = (uint32_t)(hi >> 32);
+  const uint32_t xl = xor3((uint32_t)lo, (uint32_t)hi, m);
+  const uint32_t xh = xor3((uint32_t)(lo >> 32), s3, m);
+  if (!(SA_ABLATE & 1)) {
+    uint32_t z;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x7e" : "=v"(z) : "v"(xl), "v"(xh), "v"(m));
+    zmin = zmin < z ? zmin : z;
+  }
+  const uint32_t r = s3 >> 26;                       // alignbit uses r & 31
+  const uint32_t a = __builtin_amdgcn_alignbit(xh, xl, r);
+  const uint32_t b = __builtin_amdgcn_alignbit(xl, xh, r);
+  const bool big = (int32_t)s3 < 0;                  // r >= 32: halves swap
+  return big ? pack64(b, a) : pack64(a, b);
 }
 
 struct StreamLds {
@@ -205,20 +258,6 @@ struct StreamLds {
 };
 
 typedef __attribute__((address_space(3))) const StreamLds* lds_ptr;  // 32-bit LDS address
-__device__ __forceinline__ StreamLds read_stream(lds_ptr p, int j) {
-  return StreamLds{p[j].inc_lo, p[j].inc_hi, p[j].cj_lo, p[j].cj_hi, p[j].smask, 0};
-}
-
-// raw == 0  <=>  hi == lo.  One v_cmp + one s_or into a wave-wide SGPR mask;
-// written as volatile asm so hipcc cannot sink the compare to the loop latch
-// (it did, keeping every intermediate state of the tile live).
-__device__ __forceinline__ void note_zero_draw(uint64_t& badmask, u128 s) {
-  const uint64_t hi = hi64(s), lo = lo64(s);
-  asm volatile("v_cmp_eq_u64 vcc, %1, %2\n\ts_or_b64 %0, %0, vcc"
-               : "+s"(badmask)
-               : "v"(hi), "v"(lo)
-               : "vcc");
-}
 
 // Compile-time enumeration of the internal pairs (u < v) of L clients.
 template <int L>
@@ -247,22 +286,6 @@ struct Pairs {
 // ----------------------------------------------------------------------------
 // the kernel
 // ----------------------------------------------------------------------------
-// Elements per lane per chunk.  A lane walks its run in steps of 4 (one 16-B
-// load per client per step; lanes kRun*4 bytes apart, so each load
-// instruction touches 64 lines that later steps finish consuming), and jumps
-// its streams once per run: the jump costs one multiply-add like a draw, so
-// kRun=4 (fully coalesced) pays 1 extra step per 4 draws, kRun=16 1 per 16.
-#ifndef SA_RUN
-#define SA_RUN 8
-#endif
-constexpr int kRun = SA_RUN;
-// Streams whose draws may interleave between two fences (ILP inside a wave;
-// more streams = more live temporaries).
-#ifndef SA_GROUP
-#define SA_GROUP 1
-#endif
-constexpr int kGroup = SA_GROUP;
-static_assert(kRun % 4 == 0, "run is a multiple of the 4-element step");
 
 template <typename XT, typename CT, int L, int X>
 __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
@@ -273,15 +296,12 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
   static_assert(P <= kMaxStreams, "P");
 
   const uint64_t n = a.n;
-  // lane owns a run of kRun consecutive elements per chunk (draw order), the
-  // block a chunk of 256*kRun; the grid strides over chunks.
-  constexpr uint64_t kChunk = (uint64_t)kBlockThreads * kRun;
-  const uint64_t first = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kRun;
-  const uint64_t stride = (uint64_t)gridDim.x * kChunk;
+  // lane t of block b owns elements [b*1024 + 4t, +4) of each tile; tiles
+  // stride by the grid (16-B loads: 1 KiB contiguous per wave-instruction).
+  const uint64_t first = (uint64_t)blockIdx.x * kTileElems + (uint64_t)threadIdx.x * kElemsPerLane;
+  const uint64_t stride = (uint64_t)gridDim.x * kTileElems;
 
-  // ---- per-stream constants go to LDS once; the tile loop re-reads them
-  // right before each use (a compiler barrier stops LICM from hoisting 7
-  // dwords x P streams into registers, which spills at P > 8).
+  // ---- per-stream constants go to LDS once (broadcast ds_read per use)
   __shared__ StreamLds sl[P > 0 ? P : 1];
   if constexpr (P > 0) {
     for (int j = threadIdx.x; j < P; j += blockDim.x) {
@@ -305,12 +325,14 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
       st[j] = apply(jl, ld128(s.s_lo, s.s_hi), ld128(s.inc_lo, s.inc_hi));
     }
   }
-  const u128 AJ = ld128(a.aj_lo, a.aj_hi);
+  // The tile-to-tile jump is merged into the first draw of the next tile:
+  // S_{i+4} -> S_{i+stride+1} is ONE affine step (A^(stride-3), inc*G_(stride-3)),
+  // so moving to the next tile costs no multiply beyond the draw itself.
+  const u128 AJ1 = ld128(a.aj_lo, a.aj_hi);
 
-  uint64_t badmask = 0;  // lanes that saw a raw PCG64 draw of 0 (SGPR pair)
+  uint32_t zmin = 0xFFFFFFFFu;  // 0 iff some raw PCG64 draw of this lane was 0
 
-  // per-lane XOR digests live in LDS (one lane-private slot per client):
-  // ds_xor_b64 per finished element instead of 2 VGPRs per client
+  // per-lane XOR digests live in LDS (one lane-private slot per client)
   __shared__ uint64_t dig_lds[L][kBlockThreads];
 #pragma unroll
   for (int c = 0; c < L; c++) dig_lds[c][threadIdx.x] = 0;
@@ -324,23 +346,56 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
   }
   const rsrc_t rs = make_rsrc(a.sum_out, n * 8);
 
+  // Co-located clients (L > 1): each tile's inputs are staged in LDS by
+  // LDS-DMA (global_load_lds_dwordx4: lane l's 16 B land at slot l of its
+  // wave's 1 KiB), read back one element at a time when that element is
+  // finished -- L*4 VGPRs of inputs never sit in registers across the tile.
+  constexpr bool kStage = false;  // measured: staging = 0.98x of register loads at L=8 (r01); kept for L-heavy shapes
+  __shared__ XT xs_lds[kStage ? L : 1][kStage ? kTileElems : 1];
+  const int wave = threadIdx.x >> 6;
+  typedef __attribute__((address_space(3))) void* lds_vp;
+  typedef __attribute__((address_space(1))) const void* glb_vp;
+
   lds_ptr slp = (lds_ptr)(sl);
-  for (uint64_t run0 = first; run0 < n; run0 += stride) {
-#pragma unroll 1
-   for (int step = 0; step < kRun / 4; step++) {
-    const uint64_t i = run0 + 4 * (uint64_t)step;
-    // ---- issue this step's loads early; consumed as each element finishes
-    // (continue mode and per-element weights exist only for the single-client
-    // kernel; the fused kernel drops them at compile time to save registers)
-    Vec4<XT> xv[L];
+  int tile = 0;
+  for (uint64_t i = first; i < n; i += stride, tile++) {
+    const bool jstep = tile > 0;             // uniform: this tile's k=0 draws jump
+    const u128 M0 = jstep ? AJ1 : kPcgMult;
+    const int add0 = jstep ? 2 : 0;          // u64 offset of C_J1 vs inc in StreamLds
+
+    // ---- issue this tile's loads early; consumed as each element finishes
+    if constexpr (kStage) {
+      static_assert(sizeof(XT) == 4, "staged inputs are fp32");
+      if (i + 4 <= n) {
+#pragma unroll
+        for (int c = 0; c < L; c++)
+          __builtin_amdgcn_global_load_lds((glb_vp)(reinterpret_cast<const XT*>(a.c[c].x) + i),
+                                           (lds_vp)(&xs_lds[c][wave * 256]), 16, 0, 0);
+      } else {  // ragged tail lane: plain loads into its own slot
+#pragma unroll
+        for (int c = 0; c < L; c++) {
+          const Vec4<XT> t = bload4<XT>(rx[c], i, n);
+#pragma unroll
+          for (int k = 0; k < 4; k++) xs_lds[c][threadIdx.x * 4 + k] = t.v[k];
+        }
+      }
+    }
+    Vec4<XT> xv[kStage ? 1 : L];
     Vec4<CT> wv[kGeneral ? L : 1];
     Vec4<uint64_t> pv[kGeneral ? L : 1];
 #pragma unroll
     for (int c = 0; c < L; c++) {
-      if (kGeneral && a.continue_mode) {
+      if constexpr (kStage) {
+        // inputs come from LDS (above)
+      } else if (kGeneral && a.continue_mode) {
         pv[c] = bload4<uint64_t>(rm[c], i, n);
       } else {
-        xv[c] = bload4<XT>(rx[c], i, n);
+        if (SA_ABLATE & 8) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) xv[c].v[k] = (XT)(int)(i + k + c);
+        } else {
+          xv[c] = bload4<XT>(rx[c], i, n);
+        }
         if (kGeneral && a.c[c].wvec) wv[c] = bload4<CT>(rw[kGeneral ? c : 0], i, n);
       }
     }
@@ -349,6 +404,8 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
     // step is fenced (empty volatile asm on its state, the LDS pointer and
     // the accumulators it touches), so only one stream's constants and
     // temporaries are live at a time: P*4 state VGPRs + L accumulators.
+    uint64_t sum[4];
+    uint64_t fin[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       uint64_t acc[L];
@@ -356,48 +413,29 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
       for (int c = 0; c < L; c++) acc[c] = a.c[c].bias;
       if constexpr (P > 0) {
 #pragma unroll
-        for (int g0 = 0; g0 < P; g0 += kGroup) {
-          // fence in: the group's states and the LDS pointer (ordered after
-          // the previous group's fence out), then the group's draws are free
-          // to interleave (ILP), then fence out states + accumulators.
-          uint64_t slo[kGroup], shi[kGroup], t[kGroup];
-#pragma unroll
-          for (int g = 0; g < kGroup; g++) {
-            if (g0 + g < P) {
-              slo[g] = lo64(st[g0 + g]);
-              shi[g] = hi64(st[g0 + g]);
-              asm volatile("" : "+v"(slo[g]), "+v"(shi[g]), "+v"(slp));
-            }
-          }
-#pragma unroll
-          for (int g = 0; g < kGroup; g++) {
-            const int q = g0 + g;
-            if (q < P) {
-              const uint64_t inc_lo = slp[q].inc_lo, inc_hi = slp[q].inc_hi, smask = slp[q].smask;
-              const u128 sv = mk128(shi[g], slo[g]) * kPcgMult + mk128(inc_hi, inc_lo);
-              note_zero_draw(badmask, sv);
-              t[g] = draw_signed(sv, smask);
-              slo[g] = lo64(sv);
-              shi[g] = hi64(sv);
-              const int cu = q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1);
-              const int cv = q < PI ? Pairs<L>::v(q) : cu;
-              acc[cu] += t[g];
-              if (q < PI) acc[cv] -= t[g];
-            }
-          }
-#pragma unroll
-          for (int g = 0; g < kGroup; g++) {
-            const int q = g0 + g;
-            if (q < P) {
-              const int cu = q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1);
-              const int cv = q < PI ? Pairs<L>::v(q) : cu;
-              asm volatile("" : "+v"(slo[g]), "+v"(shi[g]), "+v"(acc[cu]), "+v"(acc[cv]));
-              st[q] = mk128(shi[g], slo[g]);
-            }
-          }
+        for (int q = 0; q < P; q++) {
+          uint64_t slo = lo64(st[q]), shi = hi64(st[q]);
+          asm volatile("" : "+v"(slo), "+v"(shi), "+v"(slp));
+          typedef __attribute__((address_space(3))) const uint64_t* lds_u64;
+          const lds_u64 cp = (lds_u64)(slp + q) + (k == 0 ? add0 : 0);
+          const u128 add = (SA_ABLATE & 16) ? mk128(q, 2 * q + 1) : mk128(cp[1], cp[0]);
+          const uint32_t m = (SA_ABLATE & 16) ? 0u : (uint32_t)slp[q].smask;
+          const u128 sv = mk128(shi, slo) * (k == 0 ? M0 : kPcgMult) + add;
+          const uint64_t t = draw_signed(sv, m, zmin);
+          slo = lo64(sv);
+          shi = hi64(sv);
+          const int cu = q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1);
+          const int cv = q < PI ? Pairs<L>::v(q) : cu;
+          acc[cu] += t;
+          if (q < PI) acc[cv] -= t;
+          asm volatile("" : "+v"(slo), "+v"(shi), "+v"(acc[cu]), "+v"(acc[cv]), "+v"(zmin));
+          st[q] = mk128(shi, slo);
         }
       }
       // ---- finish element k: add the quantized value (or the prior pass)
+      if constexpr (kStage) {
+        if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's LDS-DMA landed
+      }
       uint64_t s_k = 0;
 #pragma unroll
       for (int c = 0; c < L; c++) {
@@ -405,36 +443,35 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
           acc[c] += pv[kGeneral ? c : 0].v[k];
         } else {
           const CT w = (kGeneral && a.c[c].wvec) ? wv[kGeneral ? c : 0].v[k] : scalar_weight<CT>(a.c[c]);
-          acc[c] += quantize<XT, CT>(xv[c].v[k], w, a);
+          const XT xk = kStage ? xs_lds[c][threadIdx.x * 4 + k] : xv[kStage ? 0 : c].v[k];
+          if (SA_ABLATE & 2)
+            acc[c] += __builtin_bit_cast(uint32_t, (float)xk);
+          else
+            acc[c] += quantize<XT, CT>(xk, w, a);
         }
         s_k += acc[c];
-        if (i + k < n) {
+        if (i + k < n)
           __hip_atomic_fetch_xor(&dig_lds[c][threadIdx.x], acc[c], __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (a.c[c].masked_out) bstore_u64(rm[c], i + k, acc[c]);
+        if constexpr (kGeneral) {
+          fin[k] = acc[c];
+        } else {
+          if (a.c[c].masked_out && i + k < n) bstore_u64(rm[c], i + k, acc[c]);
         }
       }
-      // the element's masked sum (8-B store; a lane's run fills whole lines)
-      if (a.sum_mode != 0 && i + k < n) {
-        if (a.sum_mode == 2) s_k += bload_u64(rs, i + k);
-        bstore_u64(rs, i + k, s_k);
-      }
+      sum[k] = s_k;
     }
-   }
 
-    // ---- jump every stream to this lane's next run (same fencing)
-    if constexpr (P > 0) {
-#pragma unroll
-      for (int q = 0; q < P; q++) {
-        uint64_t slo = lo64(st[q]), shi = hi64(st[q]);
-        asm volatile("" : "+v"(slo), "+v"(shi), "+v"(slp));
-        const u128 sv = mk128(shi, slo) * AJ + mk128(slp[q].cj_hi, slp[q].cj_lo);
-        slo = lo64(sv);
-        shi = hi64(sv);
-        asm volatile("" : "+v"(slo), "+v"(shi));
-        st[q] = mk128(shi, slo);
-      }
+    // ---- outputs: 16-B stores (a wave writes 2 KiB contiguous per pair)
+    if constexpr (kGeneral) {
+      if (a.c[0].masked_out) bstore4_u64(rm[0], i, n, fin);
     }
+    if (a.sum_mode == 2) {
+      const Vec4<uint64_t> o = bload4<uint64_t>(rs, i, n);
+#pragma unroll
+      for (int k = 0; k < 4; k++) sum[k] += o.v[k];
+    }
+    if (a.sum_mode != 0 && (!(SA_ABLATE & 8) || sum[0] == 0x123456789ull)) bstore4_u64(rs, i, n, sum);
   }
 
   // ---- wave-level XOR reduction of the digests, one atomic per wave
@@ -447,7 +484,8 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
       if ((threadIdx.x & 63) == 0 && d) atomicXor((unsigned long long*)&a.digests[c], d);
     }
   }
-  if (a.flags && badmask != 0 && (threadIdx.x & 63) == 0) atomicOr(a.flags, SA_FLAG_PRG_REJECT);
+  if (a.flags && !(SA_ABLATE & 1) && __any(zmin == 0) && (threadIdx.x & 63) == 0)
+    atomicOr(a.flags, SA_FLAG_PRG_REJECT);
 }
 
 // ----------------------------------------------------------------------------
@@ -461,11 +499,11 @@ int launch_clients(const KArgs& in, void* stream) {
   const void* kfn = reinterpret_cast<const void*>(&k_clients<XT, CT, L, X>);
   const int maxb = occupancy_blocks(kfn);
   if (maxb <= 0) return SA_ERR_HIP;
-  const uint64_t tiles = (in.n + (uint64_t)kBlockThreads * kRun - 1) / ((uint64_t)kBlockThreads * kRun);
+  const uint64_t tiles = (in.n + kTileElems - 1) / kTileElems;
   const int grid = (int)(tiles < (uint64_t)maxb ? tiles : (uint64_t)maxb);
   KArgs a = in;
-  // per-run jump J = grid*256*kRun - kRun draws (the lane consumed its run)
-  const Jump jj = jump_of((uint64_t)grid * kBlockThreads * kRun - kRun);
+  // merged jump-step: S_{i+4} -> S_{i+stride+1}, i.e. stride - 3 draws
+  const Jump jj = jump_of((uint64_t)grid * kTileElems - (kElemsPerLane - 1));
   a.aj_lo = lo64(jj.mult);
   a.aj_hi = hi64(jj.mult);
   for (int j = 0; j < P; j++) {

@@ -101,10 +101,41 @@ def fused_clients(xs: Sequence[torch.Tensor], weights: Sequence[float], pair_gen
     pg = (L.PCG64 * max(1, npair))(*pair_gens)
     ps = (C.c_int8 * max(1, npair))(*[int(s) for s in pair_signs])
     carr = make_streams(cross)
-    L.check(L.lib().sa_fused_clients(clients, nc, xtype_of(xs[0].dtype), n, int(fxp_bits), pg, ps,
-                                     carr, int(n_cross), _ptr(sum_out), int(bool(accumulate)),
-                                     _ptr(digests), _ptr(flags), C.c_void_p(_stream(sum_out))),
-            "sa_fused_clients")
+    rc = L.lib().sa_fused_clients(clients, nc, xtype_of(xs[0].dtype), n, int(fxp_bits), pg, ps,
+                                  carr, int(n_cross), _ptr(sum_out), int(bool(accumulate)),
+                                  _ptr(digests), _ptr(flags), C.c_void_p(_stream(sum_out)))
+    if rc == L.SA_ERR_UNSUPPORTED:
+        # shapes without a fused instantiation (e.g. 32 clients, 4 per GPU):
+        # every client masks with its own streams (both ends of each internal
+        # pair) and accumulates into the sum -- same result, no pair sharing
+        return _fused_fallback(xs, weights, pair_gens, pair_signs, cross, n_cross, sum_out, fxp_bits,
+                               accumulate, digests, flags, masked_outs)
+    L.check(rc, "sa_fused_clients")
+    return sum_out
+
+
+def _fused_fallback(xs, weights, pair_gens, pair_signs, cross, n_cross, sum_out, fxp_bits, accumulate,
+                    digests, flags, masked_outs):
+    nc = len(xs)
+    per = [[] for _ in range(nc)]
+    p = 0
+    for u in range(nc):
+        for v in range(u + 1, nc):
+            per[u].append((pair_gens[p], int(pair_signs[p]), v))
+            per[v].append((pair_gens[p], -int(pair_signs[p]), u))
+            p += 1
+    for c in range(nc):
+        per[c].extend(cross[c * n_cross:(c + 1) * n_cross])
+    if not accumulate:
+        sum_out.zero_()
+    scratch = None
+    for c in range(nc):
+        out = masked_outs[c] if masked_outs and masked_outs[c] is not None else None
+        if out is None:
+            scratch = scratch if scratch is not None else torch.empty_like(sum_out)
+            out = scratch
+        mask(xs[c], out, per[c], weight=weights[c], fxp_bits=fxp_bits, sum_accum=sum_out,
+             digest=None if digests is None else digests[c:c + 1], flags=flags)
     return sum_out
 
 

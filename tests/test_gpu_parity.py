@@ -344,3 +344,31 @@ def test_full_size_properties(C, n):
     dec = K.decode(s, torch.empty(n, dtype=torch.float64, device=DEV))
     fsum = torch.stack(xs).double().sum(0)
     assert float((dec - fsum).abs().max()) < C * 2.0**-18
+
+
+def test_fused_fallback_for_uninstantiated_shape():
+    """32 clients, 4 on this GPU (config 5 per-rank shape): 6 internal pairs +
+    28 cross streams each exceed one fused launch; the wrapper falls back to
+    per-client masking with accumulation -- bit-identical to the oracle."""
+    K = _K()
+    from sfl_amd.parallel_sum import plan_generators, plan_rank
+
+    C, W, n = 32, 8, 5003
+    names = [f"c{i:02d}" for i in range(C)]
+    seeds = o.seeds_for(names)
+    plan = plan_rank(names, W, 3)
+    seed_of = lambda u, v: seeds[names[u]][names[v]]  # noqa: E731
+    pg, ps, cross = plan_generators(plan, seed_of, offset=7)
+    rng = np.random.default_rng(2)
+    xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
+    masked = o.secure_masked(xs, names, seeds=seeds, offset=7)
+    s = torch.empty(n, dtype=torch.int64, device=DEV)
+    dig = torch.zeros(len(plan.clients), dtype=torch.int64, device=DEV)
+    K.fused_clients([torch.from_numpy(xs[c]).to(DEV) for c in plan.clients], [1.0] * len(plan.clients), pg, ps,
+                    cross, plan.n_cross, s, digests=dig)
+    torch.cuda.synchronize()
+    exp = np.zeros(n, dtype=np.uint64)
+    for c in plan.clients:
+        exp += masked[c]
+    assert np.array_equal(_u64(s), exp)
+    assert [int(v) for v in _u64(dig)] == [o.digest(masked[c]) for c in plan.clients]
