@@ -74,6 +74,32 @@ def cpu_baseline(C: int, fxp_bits: int, seconds: float) -> dict:
             "seconds": round(t, 3)}
 
 
+PMC_DIR = os.path.join(ROOT, "profiles", "r01")
+
+
+def pmc_traffic(kernel: str) -> dict | None:
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (tools/gpu_r01_profile.sh: separate FETCH_SIZE / WRITE_SIZE runs of
+    tools/kernel_bench.py on this workload).  Units are KiB; gfx950 reports
+    FETCH_SIZE at half the bytes of 16-B/lane streaming reads, so it is
+    doubled (MI355X_MICROARCH.md, HBM); both corrections were checked on the
+    k_sum_u64 calibration launch in the same runs (known bytes)."""
+    import csv
+
+    vals = {}
+    for counter, fname, scale in (("FETCH_SIZE", "pmc_fetch_size.csv", 2.0), ("WRITE_SIZE", "pmc_write_size.csv", 1.0)):
+        path = os.path.join(PMC_DIR, fname)
+        if not os.path.exists(path):
+            return None
+        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+             if r["Kernel_Name"].startswith(kernel) and r["Counter_Name"] == counter]
+        if not v:
+            return None
+        vals[counter] = scale * 1024.0 * sum(v) / len(v)
+    return {"bytes": vals["FETCH_SIZE"] + vals["WRITE_SIZE"], "read": vals["FETCH_SIZE"], "write": vals["WRITE_SIZE"],
+            "source": os.path.relpath(PMC_DIR, ROOT) + "/pmc_{fetch,write}_size.csv"}
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -160,6 +186,8 @@ def main():
     draws = (len(plan.pairs) + len(plan.cross)) * N
     bytes_alg = 4 * Lc * N + 8 * N  # fp32 reads of the local clients + one u64 sum write
     achieved = bytes_alg / (kern_ms / 1e3) / 1e9
+    # PMC bytes were collected on the default single-GPU workload only
+    pmc = pmc_traffic("void sa::k_clients<float, float, 8, 0>") if (world, C, N) == (1, 8, 100_000_000) else None
     out = {
         "metric": "grad elems/s device-resident: 100M-float quantize+mask+sum, 8 clients",
         "value": value,
@@ -178,7 +206,8 @@ def main():
                    "clients": C, "elems_per_client": N, "clients_per_gpu": Lc,
                    "parallelism": f"clients{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBPS,
+                     "traffic": pmc["bytes"] if pmc else None, "traffic_detail": pmc,
                      "kernel": "k_clients (sa_fused_clients)", "kernel_ms": kern_ms,
                      "algorithmic_bytes_per_launch": bytes_alg,
                      "valu": {"pcg64_draws_per_launch": draws, "draws_per_s": draws / (kern_ms / 1e3),

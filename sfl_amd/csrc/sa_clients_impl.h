@@ -149,29 +149,51 @@ __device__ __forceinline__ Vec4<T> bload4(rsrc_t r, uint64_t i, uint64_t n) {
   return out;
 }
 
-__device__ __forceinline__ void bstore4_u64(rsrc_t r, uint64_t i, uint64_t n, const uint64_t (&v)[4]) {
-  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-  const int off = (int)(i * 8);
-  if (i + 4 <= n) {
-    const v4u d0 = {(uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32)};
-    const v4u d1 = {(uint32_t)v[2], (uint32_t)(v[2] >> 32), (uint32_t)v[3], (uint32_t)(v[3] >> 32)};
-    __builtin_amdgcn_raw_buffer_store_b128(d0, r, off, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(d1, r, off + 16, 0, 0);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      if (i + k < n) {
-        const v2u d = {(uint32_t)v[k], (uint32_t)(v[k] >> 32)};
-        __builtin_amdgcn_raw_buffer_store_b64(d, r, off + 8 * k, 0, 0);
-      }
-    }
-  }
-}
-
 __device__ __forceinline__ uint64_t bload_u64(rsrc_t r, uint64_t i) {
   const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8), 0, 0);
   return (uint64_t)u[0] | ((uint64_t)u[1] << 32);
+}
+struct Vec2u64 {
+  uint64_t a, b;
+};
+// elements i, i+1 (either may lie past n: reads as 0)
+__device__ __forceinline__ Vec2u64 bload2_u64(rsrc_t r, uint64_t i, uint64_t n) {
+  Vec2u64 o{0, 0};
+  if (i + 2 <= n) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 8), 0, 0);
+    o.a = (uint64_t)u[0] | ((uint64_t)u[1] << 32);
+    o.b = (uint64_t)u[2] | ((uint64_t)u[3] << 32);
+  } else if (i < n) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8), 0, 0);
+    o.a = (uint64_t)u[0] | ((uint64_t)u[1] << 32);
+  }
+  return o;
+}
+__device__ __forceinline__ void bstore2_u64(rsrc_t r, uint64_t i, uint64_t n, uint64_t v0, uint64_t v1) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+  if (i + 2 <= n) {
+    const v4u d = {(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)(i * 8), 0, 0);
+  } else if (i < n) {
+    const v2u d = {(uint32_t)v0, (uint32_t)(v0 >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b64(d, r, (int)(i * 8), 0, 0);
+  }
+}
+// Wave-level transpose through the wave's 256 LDS slots: lane l holds
+// elements 4l..4l+3 of the wave's chunk in `in`, gets 2l, 2l+1, 128+2l,
+// 129+2l in `out`.  LDS ops of one wave complete in order; the wave barriers
+// keep the compiler from moving them across the exchange.
+__device__ __forceinline__ void wave_transpose(uint64_t* tw, int lane, const uint64_t (&in)[4],
+                                               uint64_t (&out)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) tw[4 * lane + k] = in[k];
+  __builtin_amdgcn_wave_barrier();
+  out[0] = tw[2 * lane];
+  out[1] = tw[2 * lane + 1];
+  out[2] = tw[128 + 2 * lane];
+  out[3] = tw[129 + 2 * lane];
+  __builtin_amdgcn_wave_barrier();
 }
 __device__ __forceinline__ void bstore_u64(rsrc_t r, uint64_t i, uint64_t v) {
   typedef unsigned int v2u __attribute__((ext_vector_type(2)));
@@ -346,48 +368,28 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
   }
   const rsrc_t rs = make_rsrc(a.sum_out, n * 8);
 
-  // Co-located clients (L > 1): each tile's inputs are staged in LDS by
-  // LDS-DMA (global_load_lds_dwordx4: lane l's 16 B land at slot l of its
-  // wave's 1 KiB), read back one element at a time when that element is
-  // finished -- L*4 VGPRs of inputs never sit in registers across the tile.
-  constexpr bool kStage = false;  // measured: staging = 0.98x of register loads at L=8 (r01); kept for L-heavy shapes
-  __shared__ XT xs_lds[kStage ? L : 1][kStage ? kTileElems : 1];
-  const int wave = threadIdx.x >> 6;
-  typedef __attribute__((address_space(3))) void* lds_vp;
-  typedef __attribute__((address_space(1))) const void* glb_vp;
+  // wave-private LDS slots for the output transpose (see below)
+  __shared__ uint64_t tr_lds[kBlockThreads * kElemsPerLane];
+  const int lane = threadIdx.x & 63;
+  uint64_t* const tw = tr_lds + (threadIdx.x & ~63) * kElemsPerLane;
 
   lds_ptr slp = (lds_ptr)(sl);
   int tile = 0;
-  for (uint64_t i = first; i < n; i += stride, tile++) {
+  // wave-uniform trip count: every lane of a wave runs the wave's last tile
+  // (out-of-range elements are masked at load/store) so the transpose has
+  // all 64 lanes.
+  for (uint64_t i = first; i - 4 * (uint64_t)lane < n; i += stride, tile++) {
     const bool jstep = tile > 0;             // uniform: this tile's k=0 draws jump
     const u128 M0 = jstep ? AJ1 : kPcgMult;
     const int add0 = jstep ? 2 : 0;          // u64 offset of C_J1 vs inc in StreamLds
 
     // ---- issue this tile's loads early; consumed as each element finishes
-    if constexpr (kStage) {
-      static_assert(sizeof(XT) == 4, "staged inputs are fp32");
-      if (i + 4 <= n) {
-#pragma unroll
-        for (int c = 0; c < L; c++)
-          __builtin_amdgcn_global_load_lds((glb_vp)(reinterpret_cast<const XT*>(a.c[c].x) + i),
-                                           (lds_vp)(&xs_lds[c][wave * 256]), 16, 0, 0);
-      } else {  // ragged tail lane: plain loads into its own slot
-#pragma unroll
-        for (int c = 0; c < L; c++) {
-          const Vec4<XT> t = bload4<XT>(rx[c], i, n);
-#pragma unroll
-          for (int k = 0; k < 4; k++) xs_lds[c][threadIdx.x * 4 + k] = t.v[k];
-        }
-      }
-    }
-    Vec4<XT> xv[kStage ? 1 : L];
+    Vec4<XT> xv[L];
     Vec4<CT> wv[kGeneral ? L : 1];
     Vec4<uint64_t> pv[kGeneral ? L : 1];
 #pragma unroll
     for (int c = 0; c < L; c++) {
-      if constexpr (kStage) {
-        // inputs come from LDS (above)
-      } else if (kGeneral && a.continue_mode) {
+      if (kGeneral && a.continue_mode) {
         pv[c] = bload4<uint64_t>(rm[c], i, n);
       } else {
         if (SA_ABLATE & 8) {
@@ -433,9 +435,6 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
         }
       }
       // ---- finish element k: add the quantized value (or the prior pass)
-      if constexpr (kStage) {
-        if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's LDS-DMA landed
-      }
       uint64_t s_k = 0;
 #pragma unroll
       for (int c = 0; c < L; c++) {
@@ -443,7 +442,7 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
           acc[c] += pv[kGeneral ? c : 0].v[k];
         } else {
           const CT w = (kGeneral && a.c[c].wvec) ? wv[kGeneral ? c : 0].v[k] : scalar_weight<CT>(a.c[c]);
-          const XT xk = kStage ? xs_lds[c][threadIdx.x * 4 + k] : xv[kStage ? 0 : c].v[k];
+          const XT xk = xv[c].v[k];
           if (SA_ABLATE & 2)
             acc[c] += __builtin_bit_cast(uint32_t, (float)xk);
           else
@@ -462,16 +461,34 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
       sum[k] = s_k;
     }
 
-    // ---- outputs: 16-B stores (a wave writes 2 KiB contiguous per pair)
+    // ---- outputs.  A lane finishes 4 consecutive u64 (32 B); stored as is,
+    // each 16-B store instruction would leave every 128-B line half written.
+    // The wave's 256 results are transposed through LDS instead, so lane l
+    // stores elements (2l, 2l+1) and (128+2l, 129+2l): each store instruction
+    // writes 1 KiB contiguous.
+    const uint64_t e0 = i - 4 * (uint64_t)lane + 2 * (uint64_t)lane;  // wave base + 2l
+    const uint64_t e1 = e0 + 128;
     if constexpr (kGeneral) {
-      if (a.c[0].masked_out) bstore4_u64(rm[0], i, n, fin);
+      if (a.c[0].masked_out) {
+        uint64_t v[4];
+        wave_transpose(tw, lane, fin, v);
+        bstore2_u64(rm[0], e0, n, v[0], v[1]);
+        bstore2_u64(rm[0], e1, n, v[2], v[3]);
+      }
     }
-    if (a.sum_mode == 2) {
-      const Vec4<uint64_t> o = bload4<uint64_t>(rs, i, n);
-#pragma unroll
-      for (int k = 0; k < 4; k++) sum[k] += o.v[k];
+    if (a.sum_mode != 0 && (!(SA_ABLATE & 8) || sum[0] == 0x123456789ull)) {
+      uint64_t v[4];
+      wave_transpose(tw, lane, sum, v);
+      if (a.sum_mode == 2) {
+        const Vec2u64 o0 = bload2_u64(rs, e0, n), o1 = bload2_u64(rs, e1, n);
+        v[0] += o0.a;
+        v[1] += o0.b;
+        v[2] += o1.a;
+        v[3] += o1.b;
+      }
+      bstore2_u64(rs, e0, n, v[0], v[1]);
+      bstore2_u64(rs, e1, n, v[2], v[3]);
     }
-    if (a.sum_mode != 0 && (!(SA_ABLATE & 8) || sum[0] == 0x123456789ull)) bstore4_u64(rs, i, n, sum);
   }
 
   // ---- wave-level XOR reduction of the digests, one atomic per wave
@@ -493,27 +510,49 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
 // ----------------------------------------------------------------------------
 int occupancy_blocks(const void* kernel);  // sa_api.hip
 
+// Buffer offsets are 32-bit byte offsets, so one launch covers at most
+// kChunkElems elements (4 GiB of u64); longer vectors are cut into chunks
+// whose streams start kChunkElems draws further on.
+constexpr uint64_t kChunkElems = (1ull << 29) - kTileElems;
+
 template <typename XT, typename CT, int L, int X>
 int launch_clients(const KArgs& in, void* stream) {
   constexpr int P = Pairs<L>::count + L * X;
   const void* kfn = reinterpret_cast<const void*>(&k_clients<XT, CT, L, X>);
   const int maxb = occupancy_blocks(kfn);
   if (maxb <= 0) return SA_ERR_HIP;
-  const uint64_t tiles = (in.n + kTileElems - 1) / kTileElems;
-  const int grid = (int)(tiles < (uint64_t)maxb ? tiles : (uint64_t)maxb);
-  KArgs a = in;
-  // merged jump-step: S_{i+4} -> S_{i+stride+1}, i.e. stride - 3 draws
-  const Jump jj = jump_of((uint64_t)grid * kTileElems - (kElemsPerLane - 1));
-  a.aj_lo = lo64(jj.mult);
-  a.aj_hi = hi64(jj.mult);
-  for (int j = 0; j < P; j++) {
-    const u128 cj = jj.gsum * mk128(a.s[j].inc_hi, a.s[j].inc_lo);
-    a.s[j].cj_lo = lo64(cj);
-    a.s[j].cj_hi = hi64(cj);
+  for (uint64_t off = 0; off < in.n; off += kChunkElems) {
+    KArgs a = in;
+    a.n = in.n - off < kChunkElems ? in.n - off : kChunkElems;
+    if (off) {
+      for (int c = 0; c < L; c++) {
+        if (a.c[c].x) a.c[c].x = static_cast<const XT*>(a.c[c].x) + off;
+        if (a.c[c].wvec) a.c[c].wvec = static_cast<const CT*>(a.c[c].wvec) + off;
+        if (a.c[c].masked_out) a.c[c].masked_out += off;
+      }
+      if (a.sum_out) a.sum_out += off;
+      const Jump jo = jump_of(off);
+      for (int j = 0; j < P; j++) {
+        const u128 s = apply(jo, mk128(a.s[j].s_hi, a.s[j].s_lo), mk128(a.s[j].inc_hi, a.s[j].inc_lo));
+        a.s[j].s_lo = lo64(s);
+        a.s[j].s_hi = hi64(s);
+      }
+    }
+    const uint64_t tiles = (a.n + kTileElems - 1) / kTileElems;
+    const int grid = (int)(tiles < (uint64_t)maxb ? tiles : (uint64_t)maxb);
+    // merged jump-step: S_{i+4} -> S_{i+stride+1}, i.e. stride - 3 draws
+    const Jump jj = jump_of((uint64_t)grid * kTileElems - (kElemsPerLane - 1));
+    a.aj_lo = lo64(jj.mult);
+    a.aj_hi = hi64(jj.mult);
+    for (int j = 0; j < P; j++) {
+      const u128 cj = jj.gsum * mk128(a.s[j].inc_hi, a.s[j].inc_lo);
+      a.s[j].cj_lo = lo64(cj);
+      a.s[j].cj_hi = hi64(cj);
+    }
+    hipLaunchKernelGGL((k_clients<XT, CT, L, X>), dim3(grid), dim3(kBlockThreads), 0,
+                       (hipStream_t)stream, a);
+    SA_HIP_CHECK(hipGetLastError());
   }
-  hipLaunchKernelGGL((k_clients<XT, CT, L, X>), dim3(grid), dim3(kBlockThreads), 0,
-                     (hipStream_t)stream, a);
-  SA_HIP_CHECK(hipGetLastError());
   return SA_OK;
 }
 

@@ -372,3 +372,37 @@ def test_fused_fallback_for_uninstantiated_shape():
         exp += masked[c]
     assert np.array_equal(_u64(s), exp)
     assert [int(v) for v in _u64(dig)] == [o.digest(masked[c]) for c in plan.clients]
+
+
+def test_chunked_launch_past_4gib():
+    """Vectors longer than one launch's 32-bit buffer offsets (2^29 - 1024
+    u64) are cut into chunks whose streams resume at the chunk offset: the
+    masked elements either side of the boundary and at the tail match the
+    oracle, and the fused sum equals the per-client masked sum."""
+    K, L = _K(), _L()
+    chunk = (1 << 29) - 1024
+    n = (1 << 29) + 3001
+    names = ["p0", "p1"]
+    seeds = o.seeds_for(names)
+    sd = seeds["p0"]["p1"]
+    xs = [torch.randn(n, device=DEV, dtype=torch.float32) * 1e-2 for _ in names]
+    outs = [torch.empty(n, dtype=torch.int64, device=DEV) for _ in names]
+    wsum = torch.zeros(n, dtype=torch.int64, device=DEV)
+    wdig = torch.zeros(2, dtype=torch.int64, device=DEV)
+    for c, sign in ((0, 1), (1, -1)):
+        K.mask(xs[c], outs[c], [(L.pcg64_from_seed(sd), sign, 0)], sum_accum=wsum, digest=wdig[c:c + 1])
+    s = torch.empty(n, dtype=torch.int64, device=DEV)
+    dig = torch.zeros(2, dtype=torch.int64, device=DEV)
+    mo = [torch.empty(n, dtype=torch.int64, device=DEV) for _ in names]
+    K.fused_clients(xs, [1.0, 1.0], [L.pcg64_from_seed(sd)], [1], [], 0, s, digests=dig, masked_outs=mo)
+    torch.cuda.synchronize()
+    assert torch.equal(s, wsum)
+    assert torch.equal(dig, wdig)
+    for c in range(2):
+        assert torch.equal(mo[c], outs[c])
+    for lo in (0, chunk - 40, n - 40):
+        m = o.mask_stream(sd, 40, lo)
+        q0 = o.quantize(xs[0][lo:lo + 40].cpu().numpy())
+        assert np.array_equal(_u64(outs[0][lo:lo + 40]), q0.view(np.uint64) + m), lo
+    del xs, outs, mo
+    torch.cuda.empty_cache()

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--shapes", default="8:1,8:2,8:4,8:8", help="C:W pairs")
+    ap.add_argument("--calib", type=int, default=0,
+                    help="also launch sa_sum_u64 over this many u64 inputs (known bytes, for PMC calibration)")
     args = ap.parse_args()
     import torch
 
@@ -56,6 +58,13 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             cs["times"].append(e0.elapsed_time(e1) / args.reps)
+    if args.calib:
+        ins = [torch.randint(0, 1 << 62, (N,), device=dev) for _ in range(args.calib)]
+        so = torch.empty(N, dtype=torch.int64, device=dev)
+        for _ in range(args.reps):
+            K.sum_u64(ins, so)
+        torch.cuda.synchronize()
+        del ins
     out = []
     for cs in cases:
         t = sorted(cs["times"])
