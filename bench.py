@@ -110,6 +110,8 @@ def main():
     ap.add_argument("--fxp-bits", type=int, default=18)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0, help="0 disables")
     ap.add_argument("--extra", action="store_true", help="also time the wire chain and H2D/D2H-inclusive rate")
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="N>1: masking/reduce pipeline depth (default 4; 1 = reduce after the whole launch)")
     args = ap.parse_args()
 
     import torch
@@ -117,7 +119,7 @@ def main():
 
     from sfl_amd import _lib
     from sfl_amd import kernels as K
-    from sfl_amd.parallel_sum import RcclComm, plan_generators, plan_rank
+    from sfl_amd.parallel_sum import PipelinedMaskedSum, RcclComm, plan_generators, plan_rank
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -141,23 +143,20 @@ def main():
         g = torch.Generator(device=dev).manual_seed(20260116 + c)
         xs.append(torch.randn(N, generator=g, device=dev, dtype=torch.float32) * 1e-2)
     total_steps = args.warmup + args.steps
-    gens = [plan_generators(plan, pair_seed, offset=i * N) for i in range(total_steps)]
+    chunks = args.chunks if args.chunks is not None else (4 if world > 1 else 1)
+    pipe = PipelinedMaskedSum(comm, dev, N, chunks)
+    # every step is a new round: streams start i*N draws in, chunk j at +lo_j
+    gens = [[plan_generators(plan, pair_seed, offset=i * N + lo) for lo, _ in pipe.bounds]
+            for i in range(total_steps)]
     sum_buf = torch.empty(N, dtype=torch.int64, device=dev)
     recv = torch.empty(N, dtype=torch.int64, device=dev) if (rank == 0 and world > 1) else None
     digests = torch.zeros(Lc, dtype=torch.int64, device=dev)
     flags = torch.zeros(1, dtype=torch.int32, device=dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    kev = []  # (start, end) events around every masking launch of the timed steps (compute stream)
 
     def step(i, timed_idx=None):
-        pg, ps, cross = gens[i]
-        if timed_idx is not None:
-            ev[timed_idx][0].record()
-        K.fused_clients(xs, [1.0] * Lc, pg, ps, cross, plan.n_cross, sum_buf, fxp_bits=args.fxp_bits,
-                        digests=digests, flags=flags)
-        if timed_idx is not None:
-            ev[timed_idx][1].record()
-        if comm is not None:
-            comm.reduce_u64(sum_buf, recv, root=0)
+        pipe.run(xs, [1.0] * Lc, gens[i], plan.n_cross, sum_buf, recv, fxp_bits=args.fxp_bits,
+                 digests=digests, flags=flags, kernel_events=kev if timed_idx is not None else None)
 
     for i in range(args.warmup):
         step(i)
@@ -173,7 +172,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    kern_ms = sum(a.elapsed_time(b) for a, b in kev) / args.steps  # masking kernel time per step
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -204,11 +203,12 @@ def main():
         "config": {"workload": f"{C} clients x {N} fp32 grad elems, fxp {args.fxp_bits}, ring 2^64, "
                                f"{'1 GPU fused' if world == 1 else f'{Lc} clients/GPU + RCCL reduce'}",
                    "clients": C, "elems_per_client": N, "clients_per_gpu": Lc,
-                   "parallelism": f"clients{world}"},
+                   "parallelism": f"clients{world}", "pipeline_chunks": len(pipe.bounds)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": pmc["bytes"] if pmc else None, "traffic_detail": pmc,
                      "kernel": "k_clients (sa_fused_clients)", "kernel_ms": kern_ms,
+                     "launches_per_step": len(pipe.bounds),
                      "algorithmic_bytes_per_launch": bytes_alg,
                      "valu": {"pcg64_draws_per_launch": draws, "draws_per_s": draws / (kern_ms / 1e3),
                               "peak_draws_per_s": PCG_PEAK_DRAWS,

@@ -113,3 +113,67 @@ class RcclComm:
         if self._h:
             L.check(L.lib().sa_comm_destroy(self._h), "sa_comm_destroy")
             self._h = None
+
+
+def chunk_bounds(n: int, chunks: int, align: int = 1024) -> list[tuple[int, int]]:
+    """Split [0, n) into ``chunks`` ranges whose starts are multiples of
+    ``align`` elements (keeps every chunk's buffers 16-B aligned)."""
+    chunks = max(1, chunks)
+    step = -(-n // chunks)
+    step = -(-step // align) * align
+    out = []
+    lo = 0
+    while lo < n:
+        out.append((lo, min(n, lo + step)))
+        lo += step
+    return out or [(0, 0)]
+
+
+class PipelinedMaskedSum:
+    """One rank's share of a secure-aggregation round with the exchange
+    overlapped: the fused masking launch of chunk j (compute stream) runs
+    while chunk j-1's uint64 partial sum is reduced to the server rank
+    (``ncclReduce`` on a separate comm stream, ordered by an event per
+    chunk).  Chunk j's streams start ``lo_j`` draws into the round, so the
+    result is bit-identical to one launch over the whole vector.
+
+    ``chunk_gens[j]`` = ``plan_generators(plan, seed_of, offset=round_offset + lo_j)``."""
+
+    def __init__(self, comm: RcclComm | None, device, n: int, chunks: int):
+        import torch
+
+        self.comm = comm
+        self.device = device
+        self.bounds = chunk_bounds(n, chunks)
+        self.comm_stream = torch.cuda.Stream(device) if comm is not None else None
+        self.events = [torch.cuda.Event() for _ in self.bounds]
+
+    def run(self, xs, weights, chunk_gens, n_cross: int, sum_buf, recv=None, *, root: int = 0,
+            fxp_bits: int = 18, digests=None, flags=None, kernel_events: list | None = None):
+        """``kernel_events``: if given, a timing-event pair recorded around
+        each chunk's masking launch is appended (kernel time without the
+        exchange)."""
+        import torch
+
+        from . import kernels as K
+
+        if len(chunk_gens) != len(self.bounds):
+            raise ValueError(f"{len(chunk_gens)} generator sets for {len(self.bounds)} chunks")
+        compute = torch.cuda.current_stream(self.device)
+        for j, (lo, hi) in enumerate(self.bounds):
+            pg, ps, cross = chunk_gens[j]
+            if kernel_events is not None:
+                kernel_events.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                kernel_events[-1][0].record(compute)
+            K.fused_clients([x[lo:hi] for x in xs], weights, pg, ps, cross, n_cross, sum_buf[lo:hi],
+                            fxp_bits=fxp_bits, digests=digests, flags=flags)
+            if kernel_events is not None:
+                kernel_events[-1][1].record(compute)
+            if self.comm is not None:
+                self.events[j].record(compute)
+                self.comm_stream.wait_event(self.events[j])
+                with torch.cuda.stream(self.comm_stream):
+                    self.comm.reduce_u64(sum_buf[lo:hi], recv[lo:hi] if recv is not None else None, root=root)
+        if self.comm is not None:
+            compute.wait_stream(self.comm_stream)
+        return recv if recv is not None else sum_buf

@@ -92,3 +92,14 @@ def test_plan_covers_every_pair_once():
                 seen[(min(u, v), max(u, v))] = seen.get((min(u, v), max(u, v)), 0) + 1
                 assert s == (1 if names[v] > names[u] else -1)
         assert len(seen) == C * (C - 1) // 2 and all(c == 2 for c in seen.values())
+
+
+@pytest.mark.parametrize("n,chunks", [(0, 4), (1, 4), (1023, 2), (1024, 2), (50_001, 3), (10**8, 4), (10**8, 7)])
+def test_chunk_bounds_cover_and_align(n, chunks):
+    from sfl_amd.parallel_sum import chunk_bounds
+
+    b = chunk_bounds(n, chunks)
+    assert b[0][0] == 0 and b[-1][1] == n
+    assert all(lo % 1024 == 0 for lo, _ in b)
+    assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+    assert len(b) <= max(1, chunks)

@@ -1,6 +1,7 @@
 """Our RCCL communicator (sa_comm_*) on one MI355X: world size 1 exercises
-init / reduce / allreduce / destroy through the C-ABI (multi-rank runs need
-the 8-GPU node the driver uses; the sharding logic is covered by gloo tests)."""
+init / reduce / allreduce / destroy through the C-ABI, and the pipelined
+masking + reduce of one rank (multi-rank runs need the 8-GPU node the driver
+uses; the sharding logic is covered by gloo tests)."""
 import os
 import socket
 
@@ -11,7 +12,8 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 
-def test_rccl_world1_reduce_is_identity():
+@pytest.fixture(scope="module")
+def comm():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import torch.distributed as dist
@@ -24,17 +26,53 @@ def test_rccl_world1_reduce_is_identity():
     s.close()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=0, world_size=1)
-    try:
-        comm = RcclComm(0, 1, 0)
-        rng = np.random.default_rng(1)
-        a = rng.integers(0, 2**64 - 1, 100_003, dtype=np.uint64)
-        send = torch.from_numpy(a.view(np.int64).copy()).cuda()
-        recv = torch.empty_like(send)
-        comm.reduce_u64(send, recv, root=0)
-        recv2 = torch.empty_like(send)
-        comm.allreduce_u64(send, recv2)
-        torch.cuda.synchronize()
-        assert torch.equal(recv, send) and torch.equal(recv2, send)
-        comm.close()
-    finally:
-        dist.destroy_process_group()
+    c = RcclComm(0, 1, 0)
+    yield c
+    c.close()
+    dist.destroy_process_group()
+
+
+def test_rccl_world1_reduce_is_identity(comm):
+    rng = np.random.default_rng(1)
+    a = rng.integers(0, 2**64 - 1, 100_003, dtype=np.uint64)
+    send = torch.from_numpy(a.view(np.int64).copy()).cuda()
+    recv = torch.empty_like(send)
+    comm.reduce_u64(send, recv, root=0)
+    recv2 = torch.empty_like(send)
+    comm.allreduce_u64(send, recv2)
+    torch.cuda.synchronize()
+    assert torch.equal(recv, send) and torch.equal(recv2, send)
+
+
+@pytest.mark.parametrize("chunks", [1, 3, 7])
+def test_pipelined_masked_sum_matches_oracle(comm, chunks):
+    """Rank 0 of 8 clients over 2 GPUs (4 local clients + 4 cross streams
+    each), masking of chunk j overlapped with the reduce of chunk j-1: equals
+    the oracle's sum of those clients' masked vectors, bit for bit."""
+    from oracle import secagg as o
+    from sfl_amd.parallel_sum import PipelinedMaskedSum, plan_generators, plan_rank
+
+    C, W, n, offset = 8, 2, 50_001, 123
+    names = [f"client{c}" for c in range(C)]
+    seeds = o.seeds_for(names)
+    plan = plan_rank(names, W, 0)
+    rng = np.random.default_rng(chunks)
+    xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
+    masked = o.secure_masked(xs, names, seeds=seeds, offset=offset)
+    exp = np.zeros(n, dtype=np.uint64)
+    for c in plan.clients:
+        exp += masked[c]
+    dev = torch.device("cuda", 0)
+    pipe = PipelinedMaskedSum(comm, dev, n, chunks)
+    seed_of = lambda u, v: seeds[names[u]][names[v]]  # noqa: E731
+    gens = [plan_generators(plan, seed_of, offset=offset + lo) for lo, _ in pipe.bounds]
+    s = torch.empty(n, dtype=torch.int64, device=dev)
+    recv = torch.empty(n, dtype=torch.int64, device=dev)
+    dig = torch.zeros(len(plan.clients), dtype=torch.int64, device=dev)
+    kev = []
+    pipe.run([torch.from_numpy(xs[c]).to(dev) for c in plan.clients], [1.0] * len(plan.clients), gens,
+             plan.n_cross, s, recv, digests=dig, kernel_events=kev)
+    torch.cuda.synchronize()
+    assert len(kev) == len(pipe.bounds)
+    assert np.array_equal(recv.cpu().numpy().view(np.uint64), exp)
+    assert [int(v) for v in dig.cpu().numpy().view(np.uint64)] == [o.digest(masked[c]) for c in plan.clients]
