@@ -1,0 +1,286 @@
+"""Loopback-socket party runtime for secure aggregation.
+
+Every party is its own OS process; parties talk only through TCP sockets on
+127.0.0.1 using the framed raw wire format (``sfl_amd.wire``), replacing the
+RayFed actor transport of the reference (``sfl/distributed/op_strategy.py:131-141``):
+
+1. handshake -- each client sends HELLO (party name, index, DH public key);
+   the server relays the key table (KEYS) and every client derives its
+   pairwise seeds (``Masker.agree``, the a1 setup of SURVEY.md §8a);
+2. round -- each client copies its host gradient to its GPU, quantizes and
+   masks it there (``sa_mask``), copies the masked uint64 vector back to
+   pinned host memory and sends it (META with its weight, then MASKED); the
+   server receives all C frames concurrently straight into pinned buffers,
+   copies each to its GPU as soon as it lands, sums them mod 2^64
+   (``sa_sum_u64``), decodes (``sa_decode``) and sends the float64 result
+   back to every client (RESULT).
+
+This is the path that "starts and ends in host memory" (BASELINE north
+star): the per-round rate here includes H2D, D2H and the loopback copies.
+The GPU kernels are the product path; nothing here falls back to the CPU.
+"""
+
+from __future__ import annotations
+
+import json
+import socket
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from . import wire as W
+from .wire import META
+
+
+class LoopbackServer:
+    """The aggregation server party (binds 127.0.0.1)."""
+
+    def __init__(self, n_clients: int, *, host: str = "127.0.0.1", port: int = 0, gpu: int = 0,
+                 fxp_bits: int = 18):
+        self.n_clients = n_clients
+        self.gpu = gpu
+        self.fxp_bits = fxp_bits
+        self.sock = socket.create_server((host, port))
+        self.port = self.sock.getsockname()[1]
+        self.conns: list[socket.socket] = []
+        self.names: list[str] = []
+        self._bufs = None
+        self.last_masked = None
+
+    def accept(self, timeout: float = 300.0) -> dict:
+        """Accept every client, collect HELLOs, relay the key table."""
+        self.sock.settimeout(timeout)
+        hello = {}
+        for _ in range(self.n_clients):
+            conn, _ = self.sock.accept()
+            conn.settimeout(timeout)
+            conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            _, mv = W.recv_frame(conn, expect_kind=W.HELLO)
+            info = json.loads(bytes(mv))
+            hello[int(info["index"])] = (conn, info)
+        if sorted(hello) != list(range(self.n_clients)):
+            raise W.WireError(f"client indices {sorted(hello)} are not 0..{self.n_clients - 1}")
+        self.conns = [hello[i][0] for i in range(self.n_clients)]
+        self.names = [hello[i][1]["party"] for i in range(self.n_clients)]
+        if len(set(self.names)) != len(self.names):
+            raise W.WireError(f"duplicate party names {self.names}")
+        keys = {hello[i][1]["party"]: hello[i][1]["public_key"] for i in range(self.n_clients)}
+        blob = json.dumps(keys).encode()
+        for c in self.conns:
+            W.send_frame(c, W.KEYS, blob)
+        return keys
+
+    def _buffers(self, n: int):
+        import torch
+
+        if self._bufs is None or self._bufs[0] != n:
+            dev = torch.device("cuda", self.gpu)
+            host = [torch.empty(n, dtype=torch.int64).pin_memory() for _ in self.conns]
+            devb = [torch.empty(n, dtype=torch.int64, device=dev) for _ in self.conns]
+            streams = [torch.cuda.Stream(dev) for _ in self.conns]
+            self._bufs = (n, host, devb, streams)
+        return self._bufs[1:]
+
+    def round(self, n: int, rnd: int, *, average: bool = False, verify_digest: bool = False,
+              keep_masked: bool = False):
+        """One aggregation round over n-element vectors -> (float64 result, timings)."""
+        import torch
+
+        from . import kernels as K
+
+        dev = torch.device("cuda", self.gpu)
+        host, devb, streams = self._buffers(n)
+        t0 = time.perf_counter()
+        weights = [None] * len(self.conns)
+
+        def receive(i):
+            conn = self.conns[i]
+            _, mv = W.recv_frame(conn, expect_kind=META)
+            weights[i] = json.loads(bytes(mv)).get("weight")
+            h, _ = W.recv_frame(conn, into=host[i], expect_kind=W.MASKED)
+            if h.count != n or h.round != rnd:
+                raise W.WireError(f"client {i}: frame of {h.count} elems for round {h.round}, want {n} / {rnd}")
+            if verify_digest and h.digest != W.xor_digest(host[i].numpy()):
+                raise W.WireError(f"client {i}: payload digest mismatch")
+            with torch.cuda.stream(streams[i]):
+                devb[i].copy_(host[i], non_blocking=True)
+            return time.perf_counter()
+
+        with ThreadPoolExecutor(len(self.conns)) as ex:
+            t_recv = max(ex.map(receive, range(len(self.conns))))
+        main = torch.cuda.current_stream(dev)
+        for s in streams:
+            main.wait_stream(s)
+        t1 = time.perf_counter()
+        s_sum = K.sum_u64(devb, torch.empty(n, dtype=torch.int64, device=dev))
+        div = 1.0
+        if average:
+            div = float(len(self.conns)) if all(w is None for w in weights) else float(
+                sum(1.0 if w is None else w for w in weights))
+        dec = K.decode(s_sum, torch.empty(n, dtype=torch.float64, device=dev), fxp_bits=self.fxp_bits, divisor=div)
+        out = dec.cpu().numpy()
+        t2 = time.perf_counter()
+        if keep_masked:
+            self.last_masked = [h.numpy().view(np.uint64).copy() for h in host]
+        for c in self.conns:
+            W.send_frame(c, W.RESULT, out, rnd=rnd)
+        t3 = time.perf_counter()
+        return out, {"recv_h2d_s": t_recv - t0, "sum_decode_d2h_s": t2 - t1, "broadcast_s": t3 - t2,
+                     "round_s": t3 - t0}
+
+    def close(self):
+        for c in self.conns:
+            try:
+                W.send_frame(c, W.BYE)
+                c.close()
+            except OSError:
+                pass
+        self.sock.close()
+
+
+class LoopbackClient:
+    """One client party: masks its host vector on its GPU and ships it."""
+
+    def __init__(self, party: str, index: int, port: int, *, host: str = "127.0.0.1", gpu: int = 0,
+                 fxp_bits: int = 18, seeds: dict | None = None):
+        from .security.aggregation.masker import Masker
+
+        self.party, self.index, self.gpu = party, index, gpu
+        self.masker = Masker(party, fxp_bits)
+        self.fxp_bits = fxp_bits
+        self._seeds = seeds
+        self.sock = socket.create_connection((host, port), timeout=300)
+        self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        self._bufs = None
+
+    def handshake(self):
+        hello = {"party": self.party, "index": self.index, "public_key": self.masker.public_key}
+        W.send_frame(self.sock, W.HELLO, json.dumps(hello).encode(), sender=self.index)
+        _, mv = W.recv_frame(self.sock, expect_kind=W.KEYS)
+        keys = {k: int(v) for k, v in json.loads(bytes(mv)).items()}
+        if self._seeds is not None:  # explicit pair seeds (tests / benches)
+            for peer in keys:
+                if peer != self.party:
+                    self.masker.set_seed(peer, int(self._seeds[peer]))
+        else:
+            self.masker.agree(keys)
+        return sorted(keys)
+
+    def _buffers(self, n: int):
+        import torch
+
+        if self._bufs is None or self._bufs[0] != n:
+            dev = torch.device("cuda", self.gpu)
+            self._bufs = (n, torch.empty(n, dtype=torch.float32).pin_memory(),
+                          torch.empty(n, dtype=torch.int64).pin_memory(),
+                          torch.empty(n, dtype=torch.float32, device=dev),
+                          torch.empty(n, dtype=torch.int64, device=dev))
+        return self._bufs[1:]
+
+    def submit(self, x: np.ndarray, rnd: int, weight=None) -> dict:
+        """Mask ``x`` (host float32) for round ``rnd`` and send it."""
+        import torch
+
+        from . import _lib as L
+        from . import kernels as K
+
+        n = x.size
+        hx, hm, dx, dm = self._buffers(n)
+        dev = dx.device
+        t0 = time.perf_counter()
+        hx.numpy()[:] = np.asarray(x, dtype=np.float32).reshape(-1)
+        dx.copy_(hx, non_blocking=True)
+        dig = torch.zeros(1, dtype=torch.int64, device=dev)
+        flags = torch.zeros(1, dtype=torch.int32, device=dev)
+        with torch.cuda.device(dev):
+            K.mask(dx, dm, self.masker.streams(), weight=1.0 if weight is None else weight,
+                   fxp_bits=self.fxp_bits, digest=dig, flags=flags)
+        hm.copy_(dm, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        if int(flags.item()) & L.SA_FLAG_PRG_REJECT:
+            raise L.SALibraryError("a PCG64 raw draw was 0 (p=2^-64): re-position the streams")
+        self.masker.consume(n)
+        t1 = time.perf_counter()
+        W.send_frame(self.sock, META, json.dumps({"weight": weight}).encode(), sender=self.index, rnd=rnd)
+        W.send_frame(self.sock, W.MASKED, hm, dtype=W.U64, sender=self.index, rnd=rnd,
+                     digest=int(dig.cpu().numpy().view(np.uint64)[0]))
+        t2 = time.perf_counter()
+        return {"h2d_mask_d2h_s": t1 - t0, "send_s": t2 - t1}
+
+    def result(self) -> np.ndarray:
+        h, mv = W.recv_frame(self.sock, expect_kind=W.RESULT)
+        return W.as_array(h, mv).copy()
+
+    def close(self):
+        try:
+            self.sock.close()
+        except OSError:
+            pass
+
+
+# ---------------------------------------------------------------------------
+# process orchestration (spawned client processes, server in the caller)
+# ---------------------------------------------------------------------------
+def synthetic_gradient(c: int, n: int, rnd: int = 0) -> np.ndarray:
+    """SURVEY.md §8(d) synthetic input: N(0, 0.01^2) float32, seeded per client."""
+    g = np.random.default_rng(20260116 + c + 1000 * rnd)
+    return (g.standard_normal(n, dtype=np.float32) * np.float32(1e-2)).astype(np.float32)
+
+
+def client_process(party: str, index: int, port: int, n: int, rounds: int, seeds, weight, gpu: int, fxp_bits: int,
+                   out_q) -> None:
+    """Entry point of one spawned client party."""
+    try:
+        cl = LoopbackClient(party, index, port, gpu=gpu, fxp_bits=fxp_bits, seeds=seeds)
+        cl.handshake()
+        stats = []
+        for r in range(rounds):
+            st = cl.submit(synthetic_gradient(index, n, r), r, weight)
+            res = cl.result()
+            st["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))
+            stats.append(st)
+        h, _ = W.recv_frame(cl.sock, expect_kind=W.BYE)
+        cl.close()
+        out_q.put((index, "ok", stats))
+    except Exception as e:  # reported to the parent, which fails loudly
+        out_q.put((index, "error", repr(e)))
+
+
+def run_loopback(names: list[str], n: int, rounds: int = 1, *, seeds: dict | None = None, weights=None,
+                 average: bool = False, gpu: int = 0, fxp_bits: int = 18, keep_masked: bool = False,
+                 verify_digest: bool = False, timeout: float = 600.0):
+    """Spawn one process per client, run ``rounds`` rounds with this process
+    as the server.  Returns (results per round, server timings, client stats)."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    srv = LoopbackServer(len(names), gpu=gpu, fxp_bits=fxp_bits)
+    q = ctx.Queue()
+    procs = []
+    for i, p in enumerate(names):
+        ps = None if seeds is None else {v: seeds[p][v] for v in names if v != p}
+        w = None if weights is None else weights[i]
+        pr = ctx.Process(target=client_process, args=(p, i, srv.port, n, rounds, ps, w, gpu, fxp_bits, q))
+        pr.start()
+        procs.append(pr)
+    results, timings, masked = [], [], []
+    try:
+        srv.accept(timeout=timeout)
+        for r in range(rounds):
+            out, t = srv.round(n, r, average=average, keep_masked=keep_masked, verify_digest=verify_digest)
+            results.append(out)
+            timings.append(t)
+            if keep_masked:
+                masked.append(srv.last_masked)
+    finally:
+        srv.close()
+    stats = {}
+    for _ in procs:
+        idx, status, payload = q.get(timeout=timeout)
+        if status != "ok":
+            raise RuntimeError(f"client {idx} failed: {payload}")
+        stats[idx] = payload
+    for pr in procs:
+        pr.join(timeout=60)
+    return results, timings, stats, masked

@@ -1,0 +1,225 @@
+"""Horizontal-FL round around the secure aggregator (SURVEY.md §8f row 1,
+BASELINE config 4): the caller side of the hot path, mirrored from the
+reference so the aggregator can be swapped in exactly where FLModel uses it.
+
+Reference interfaces followed:
+
+* ``FLModel.fit`` aggregation hook -- every ``aggregate_freq`` local steps the
+  clients' ``train_step`` outputs go to ``aggregator.average(params, axis=0,
+  weights=sample_nums)`` and the result is sent back to every party
+  (``sfl/ml/nn/fl/fl_model.py:492-517``, ``:578-583``); the last batch of an
+  epoch is applied with ``apply_weights`` (``:585-589``);
+* ``FedAvgW.train_step`` -- set the global weights, run ``train_steps``
+  batches, return ``(get_weights(return_numpy=True), num_sample)``
+  (``sfl/ml/nn/fl/backend/torch/strategy/fed_avg_w.py:36-87``);
+* torch payload packing -- ``state_dict`` values as a list of host numpy
+  arrays, written back with ``torch.Tensor(np.copy(v))``
+  (``sfl/ml/nn/core/torch/mixins.py:74-89``);
+* ``TorchModel(model_fn, loss_fn, optim_fn, metrics)`` and ``optim_wrapper``
+  (``sfl/ml/nn/core/torch/module.py:247``, ``sfl/ml/nn/core/torch/utils.py:23``);
+  each worker seeds torch with ``random_seed`` before building its model
+  (``sfl/ml/nn/fl/backend/torch/fl_base.py:51-52``), so every client starts
+  from the same initial weights.
+
+Parties are ``PYU``s (``sfl_amd.device``); local training runs on
+``train_device`` (the party's GPU by default, or the CPU).  Out of scope:
+the reference's dataset builders, callbacks, DP accountant hooks,
+compression strategies and the other strategies (fed_prox, scaffold, ...).
+"""
+
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..device import PYU, PYUObject, reveal
+
+
+def optim_wrapper(func, *args, **kwargs):
+    """``optim_wrapper(optim.Adam, lr=1e-2)(params)`` (reference utils.py:23)."""
+
+    def make(params):
+        return func(params, *args, **kwargs)
+
+    return make
+
+
+@dataclass
+class TorchModel:
+    """Model builder record (reference module.py:247)."""
+
+    model_fn: Callable[[], torch.nn.Module]
+    loss_fn: Callable[[], torch.nn.Module]
+    optim_fn: Callable
+    metrics: list = field(default_factory=list)
+
+
+class FedAvgW:
+    """One party's worker for the ``fed_avg_w`` strategy."""
+
+    def __init__(self, builder: TorchModel, device: PYU, random_seed: Optional[int] = None,
+                 train_device: Optional[torch.device] = None):
+        if random_seed is not None:
+            torch.manual_seed(random_seed)
+        self.device = device
+        self.exe_device = torch.device(train_device) if train_device is not None else device.torch_device
+        self.model = builder.model_fn().to(self.exe_device)
+        self.optimizer = builder.optim_fn(self.model.parameters())
+        self.loss_fn = builder.loss_fn()
+        self._x = self._y = None
+        self._batch = 32
+        self._pos = 0
+
+    # ----------------------------------------------------------- data
+    def set_data(self, x: np.ndarray, y: np.ndarray, batch_size: int):
+        self._x = torch.as_tensor(np.asarray(x, dtype=np.float32))
+        self._y = torch.as_tensor(np.asarray(y))
+        self._batch = int(batch_size)
+        self._pos = 0
+
+    def steps_per_epoch(self) -> int:
+        return math.ceil(len(self._x) / self._batch)
+
+    def _reset_data_iter(self):
+        self._pos = 0
+
+    def next_batch(self):
+        if self._pos >= len(self._x):
+            self._pos = 0
+        lo, hi = self._pos, min(len(self._x), self._pos + self._batch)
+        self._pos = hi
+        return self._x[lo:hi].to(self.exe_device), self._y[lo:hi].to(self.exe_device)
+
+    # -------------------------------------------------------- weights
+    def get_weights(self, return_numpy: bool = True):
+        if not return_numpy:
+            return {k: v.cpu() for k, v in self.model.state_dict().items()}
+        return [v.detach().cpu().numpy().copy() for v in self.model.state_dict().values()]
+
+    def set_weights(self, weights):
+        sd = self.model.state_dict()
+        new = {}
+        for (k, v), w in zip(sd.items(), weights):
+            w = w.detach().cpu().numpy() if isinstance(w, torch.Tensor) else np.asarray(w)
+            # reference: torch.Tensor(np.copy(v)) -> float32 for float params
+            new[k] = torch.from_numpy(np.array(w, copy=True)).to(dtype=v.dtype)
+        self.model.load_state_dict(new)
+
+    # ------------------------------------------------------- training
+    def train_step(self, weights, cur_steps: int, train_steps: int, refresh_data: bool = False, **kwargs):
+        self.model.train()
+        if refresh_data:
+            self._reset_data_iter()
+        if weights is not None:
+            self.set_weights(weights)
+        num_sample = 0
+        loss = None
+        for _ in range(train_steps):
+            x, y = self.next_batch()
+            num_sample += x.shape[0]
+            self.optimizer.zero_grad()
+            loss = self.loss_fn(self.model(x), y)
+            loss.backward()
+            self.optimizer.step()
+        self.last_loss = float(loss.item()) if loss is not None else float("nan")
+        return self.get_weights(return_numpy=True), num_sample
+
+    def apply_weights(self, weights, **kwargs):
+        if weights is not None:
+            self.set_weights(weights)
+
+    @torch.no_grad()
+    def evaluate(self, x, y):
+        self.model.eval()
+        xt = torch.as_tensor(np.asarray(x, dtype=np.float32)).to(self.exe_device)
+        yt = torch.as_tensor(np.asarray(y)).to(self.exe_device)
+        out = self.model(xt)
+        loss = float(self.loss_fn(out, yt).item())
+        acc = float((out.argmax(1) == yt).float().mean().item())
+        return loss, acc
+
+
+_STRATEGIES = {("fed_avg_w", "torch"): FedAvgW}
+
+
+class FLModel:
+    """Horizontal FL over ``device_list`` with ``aggregator`` (any object with
+    the ``Aggregator`` surface: ``average(data, axis, weights)``)."""
+
+    def __init__(self, server: Optional[PYU] = None, device_list: List[PYU] = (), model: TorchModel = None,
+                 aggregator=None, strategy: str = "fed_avg_w", backend: str = "torch",
+                 random_seed: Optional[int] = None, train_device=None, **kwargs):
+        if (strategy, backend) not in _STRATEGIES:
+            raise NotImplementedError(f"strategy {strategy!r} / backend {backend!r}")
+        if aggregator is None:
+            raise ValueError("this build aggregates through an Aggregator (server_agg_method is out of scope)")
+        self.server = server
+        self.device_list = list(device_list)
+        self._aggregator = aggregator
+        self.strategy = strategy
+        self._workers: Dict[PYU, FedAvgW] = {
+            d: _STRATEGIES[(strategy, backend)](model, d, random_seed, train_device) for d in self.device_list}
+
+    def initialize_weights(self):
+        """Average the clients' initial weights and install them everywhere
+        (reference fl_model.py:126-137)."""
+        ws = [PYUObject(d, w.get_weights()) for d, w in self._workers.items()]
+        init = self._aggregator.average(ws, axis=0)
+        for d, w in self._workers.items():
+            w.set_weights(reveal(init.to(d)))
+        return init
+
+    def fit(self, x: Dict[PYU, np.ndarray], y: Dict[PYU, np.ndarray], batch_size: int = 32, epochs: int = 1,
+            aggregate_freq: int = 1, validation_data=None, round_hook: Callable | None = None) -> dict:
+        """``round_hook(round_index, aggregated_params)`` is called after every
+        aggregation (the test oracle checks rounds with it)."""
+        for d, w in self._workers.items():
+            w.set_data(x[d], y[d], batch_size)
+        steps = max(w.steps_per_epoch() for w in self._workers.values())
+        history = {"train_loss": [], "val_loss": [], "val_accuracy": [], "aggregation_s": [], "round_s": []}
+        rnd = 0
+        for epoch in range(epochs):
+            model_params_list = None
+            for step in range(0, steps, aggregate_freq):
+                t_round = time.perf_counter()
+                params, nums = [], []
+                for idx, (d, w) in enumerate(self._workers.items()):
+                    cp = reveal(model_params_list[idx]) if model_params_list is not None else None
+                    n_steps = aggregate_freq if step + aggregate_freq < steps else steps - step
+                    p, n = w.train_step(cp, epoch * steps + step, n_steps, refresh_data=(step == 0))
+                    params.append(PYUObject(d, p))
+                    nums.append(n)
+                t_agg = time.perf_counter()
+                model_params = self._aggregator.average(params, axis=0, weights=nums)
+                agg_data = reveal(model_params)
+                if isinstance(agg_data, list) and agg_data and isinstance(agg_data[0], torch.Tensor):
+                    torch.cuda.synchronize()
+                history["aggregation_s"].append(time.perf_counter() - t_agg)
+                model_params_list = [model_params.to(d) for d in self.device_list]
+                history["round_s"].append(time.perf_counter() - t_round)
+                if round_hook is not None:
+                    round_hook(rnd, agg_data)
+                rnd += 1
+            for idx, (d, w) in enumerate(self._workers.items()):
+                w.apply_weights(reveal(model_params_list[idx]))
+            history["train_loss"].append(float(np.mean([w.last_loss for w in self._workers.values()])))
+            if validation_data is not None:
+                vl, va = self.evaluate(*validation_data)
+                history["val_loss"].append(vl)
+                history["val_accuracy"].append(va)
+        return history
+
+    def evaluate(self, x, y):
+        """Global model metrics: after ``fit`` every party holds the same
+        aggregated weights, so the first worker evaluates."""
+        w = next(iter(self._workers.values()))
+        return w.evaluate(x, y)
+
+    def get_weights(self, device: Optional[PYU] = None):
+        d = device or self.device_list[0]
+        return self._workers[d].get_weights()

@@ -167,39 +167,57 @@ class SecureAggregator(Aggregator):
         server = self._device
         sdev = server.torch_device
         flags = torch.zeros(1, dtype=torch.int32, device=sdev)
-        out_layers = []
         masked_keep, digests_keep = [], []
 
         # layers are masked in order with one stream position per (party, peer),
         # exactly like the reference's per-layer rng.integers calls
-        for li in range(nl):
-            n = int(np.prod(shapes[li])) if shapes[li] else 1
-            xs, cts, ws, wvecs = [], [], [], []
-            for ci, d in enumerate(data):
-                party = d.device
-                a = layer_lists[ci][li]
-                w = None if weights is None else weights[ci]
-                ldt = _np_dtype(a)
-                ct = _compute_dtype(ldt, w, self._fxp_bits)
-                if ct not in (np.dtype(np.float32), np.dtype(np.float64), np.dtype(np.int64)):
-                    raise NotImplementedError(f"arithmetic type {ct} (data {ldt}) is not supported")
-                xt = ldt if ldt in _NP2T else (np.dtype(np.int64) if ldt.kind in "biu" else np.dtype(np.float64))
-                if ldt.kind in "biu" and ldt != np.dtype(np.int64) and ct.kind == "i":
-                    raise NotImplementedError(f"integer data of type {ldt} is not supported")
-                x = self._to_device(a, xt, party)
-                wv, wscalar = None, 1.0
-                if w is not None:
-                    if np.ndim(w) == 0:
-                        wscalar = float(w) if ct.kind == "f" else int(w)
-                    else:
-                        wb = np.broadcast_to(np.asarray(w), shapes[li]).astype(ct)
-                        wv = torch.from_numpy(np.ascontiguousarray(wb).reshape(-1)).to(party.torch_device)
-                xs.append(x)
-                cts.append(ct)
-                ws.append(wscalar)
-                wvecs.append(wv)
+        sizes = [int(np.prod(sh)) if sh else 1 for sh in shapes]
+        if (nl > 1 and not as_torch and (weights is None or all(np.ndim(w) == 0 for w in weights))
+                and all(len({np.asarray(a).dtype for a in ll}) == 1 for ll in layer_lists)):
+            # host payloads of one dtype: pack on the host, one H2D copy per party
+            flat = [np.concatenate([np.asarray(a).reshape(-1) for a in ll]) for ll in layer_lists]
+            g = self._prepare_layer(data, flat, (sum(sizes),), weights)
+            return self._finish(data, [(list(range(nl)), sizes, g)], shapes, weights, average, as_torch,
+                                is_list, payloads, flags, masked_keep, digests_keep)
+        prepared = [self._prepare_layer(data, [ll[li] for ll in layer_lists], shapes[li], weights)
+                    for li in range(nl)]
+        # Consecutive layers draw consecutive stream positions, so when every
+        # layer of a party has the same element/arithmetic type and a scalar
+        # weight, the layers are packed into one contiguous vector per party
+        # (List[array] <-> one vector + offsets) and aggregated
+        # by ONE launch -- bit-identical to the per-layer launches.
+        packable = nl > 1 and all(
+            all(p["wvecs"][ci] is None and p["xs"][ci].dtype == prepared[0]["xs"][ci].dtype
+                and p["cts"][ci] == prepared[0]["cts"][ci] for p in prepared)
+            for ci in range(len(data)))
+        if packable:
+            groups = [(list(range(nl)), sizes, {
+                "n": sum(sizes), "cts": prepared[0]["cts"], "ws": prepared[0]["ws"],
+                "wvecs": [None] * len(data),
+                "xs": [torch.cat([p["xs"][ci] for p in prepared]) for ci in range(len(data))]})]
+        else:
+            groups = [([li], [prepared[li]["n"]], prepared[li]) for li in range(nl)]
 
-            s = self._masked_sum(data, xs, cts, ws, wvecs, n, flags, masked_keep, digests_keep)
+        return self._finish(data, groups, shapes, weights, average, as_torch, is_list, payloads, flags,
+                            masked_keep, digests_keep)
+
+    def _finish(self, data, groups, shapes, weights, average, as_torch, is_list, payloads, flags, masked_keep,
+                digests_keep):
+        """Masked sum + decode of every launch group, split back into layers."""
+        sdev = self._device.torch_device
+        server = self._device
+        nl = len(shapes)
+        out_layers = [None] * nl
+        for lis, sizes, g in groups:
+            n = g["n"]
+            keep_before = len(masked_keep)
+            s = self._masked_sum(data, g["xs"], g["cts"], g["ws"], g["wvecs"], n, flags, masked_keep,
+                                 digests_keep)
+            if self._keep_masked and len(lis) > 1:
+                packed = masked_keep.pop(keep_before)
+                bounds = np.cumsum([0] + sizes)
+                for k in range(len(lis)):
+                    masked_keep.append([m[bounds[k]:bounds[k + 1]] for m in packed])
 
             # decode on the server GPU: / 2^fxp, then / C or / sum(w)
             dec = torch.empty(n, dtype=torch.float64, device=sdev)
@@ -210,13 +228,15 @@ class SecureAggregator(Aggregator):
                 elif all(np.ndim(w) == 0 for w in weights):
                     divisor = float(sum(weights))
                 else:
+                    li = lis[0]
                     wb = [torch.from_numpy(np.ascontiguousarray(
                         np.broadcast_to(np.asarray(w), shapes[li]).astype(np.float64)).reshape(-1)).to(sdev)
                         for w in weights]
                     divisor_vec = K.sum_f64(wb, torch.empty(n, dtype=torch.float64, device=sdev))
             K.decode(s, dec, fxp_bits=self._fxp_bits, divisor=divisor, divisor_vec=divisor_vec)
-            dec = dec.reshape(shapes[li])
-            out_layers.append(dec if as_torch else dec.cpu().numpy())
+            parts = dec.split(sizes) if as_torch else np.split(dec.cpu().numpy(), np.cumsum(sizes)[:-1])
+            for li, part in zip(lis, parts):
+                out_layers[li] = part.reshape(shapes[li])
 
         if int(flags.item()) & L.SA_FLAG_PRG_REJECT:
             raise L.SALibraryError(
@@ -229,6 +249,35 @@ class SecureAggregator(Aggregator):
         if is_list and isinstance(payloads[0], tuple):
             result = tuple(result)
         return PYUObject(server, result)
+
+    def _prepare_layer(self, data, arrays, shape, weights) -> dict:
+        """Per-party device vector, arithmetic type and weight of one layer."""
+        n = int(np.prod(shape)) if shape else 1
+        xs, cts, ws, wvecs = [], [], [], []
+        for ci, d in enumerate(data):
+            party = d.device
+            a = arrays[ci]
+            w = None if weights is None else weights[ci]
+            ldt = _np_dtype(a)
+            ct = _compute_dtype(ldt, w, self._fxp_bits)
+            if ct not in (np.dtype(np.float32), np.dtype(np.float64), np.dtype(np.int64)):
+                raise NotImplementedError(f"arithmetic type {ct} (data {ldt}) is not supported")
+            xt = ldt if ldt in _NP2T else (np.dtype(np.int64) if ldt.kind in "biu" else np.dtype(np.float64))
+            if ldt.kind in "biu" and ldt != np.dtype(np.int64) and ct.kind == "i":
+                raise NotImplementedError(f"integer data of type {ldt} is not supported")
+            x = self._to_device(a, xt, party)
+            wv, wscalar = None, 1.0
+            if w is not None:
+                if np.ndim(w) == 0:
+                    wscalar = float(w) if ct.kind == "f" else int(w)
+                else:
+                    wb = np.broadcast_to(np.asarray(w), shape).astype(ct)
+                    wv = torch.from_numpy(np.ascontiguousarray(wb).reshape(-1)).to(party.torch_device)
+            xs.append(x)
+            cts.append(ct)
+            ws.append(wscalar)
+            wvecs.append(wv)
+        return {"n": n, "xs": xs, "cts": cts, "ws": ws, "wvecs": wvecs}
 
     @staticmethod
     def _to_device(a, xt: np.dtype, party: PYU) -> torch.Tensor:

@@ -1,0 +1,50 @@
+"""Loopback-socket party processes (BASELINE config 1 shape, SURVEY.md §8f
+row 2): one spawned process per client masks on the GPU and ships raw u64
+frames over 127.0.0.1; the server (this process) sums and decodes on the GPU.
+Checked against the oracle: the received wire images equal the oracle's
+masked vectors bit for bit, and the decoded results equal its float64."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+from oracle import secagg as o  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def test_loopback_rounds_bit_exact_vs_oracle():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.loopback import run_loopback, synthetic_gradient
+
+    names = ["alice", "bob", "carol"]
+    n, rounds = 20_011, 2
+    seeds = o.seeds_for(names)
+    w = [3, 5, 8]
+    res, timings, stats, masked = run_loopback(names, n, rounds, seeds=seeds, weights=w, average=True,
+                                               keep_masked=True, verify_digest=True, timeout=300)
+    for r in range(rounds):
+        xs = [synthetic_gradient(c, n, r) for c in range(len(names))]
+        exp, s, m = o.secure_average(xs, names, weights=w, seeds=seeds, offset=r * n)
+        assert np.array_equal(res[r], exp), r
+        for c in range(len(names)):
+            assert np.array_equal(masked[r][c], m[c]), (r, c)
+            assert stats[c][r]["result_xor"] == int(np.bitwise_xor.reduce(exp.view(np.uint64)))
+
+
+def test_loopback_dh_seeds_sum():
+    """Real DH agreement inside the party processes (seeds unknown to the
+    test): the masked sum is PRG-independent, so the decoded sum still equals
+    the oracle's."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.loopback import run_loopback, synthetic_gradient
+
+    names = [f"p{i}" for i in range(4)]
+    n = 4099
+    res, _, _, masked = run_loopback(names, n, 1, keep_masked=True, timeout=300)
+    xs = [synthetic_gradient(c, n, 0) for c in range(len(names))]
+    q = [o.quantize(x) for x in xs]
+    assert np.array_equal(res[0], o.decode(o.server_sum(q)))
+    for c in range(len(names)):
+        assert not np.array_equal(masked[0][c], q[c])  # masked on the wire
