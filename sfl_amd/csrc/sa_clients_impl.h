@@ -275,6 +275,89 @@ __device__ __forceinline__ uint64_t draw_signed(u128 s, uint32_t m, uint32_t& zm
   return big ? pack64(b, a) : pack64(a, b);
 }
 
+// One PCG64 step + signed XSL-RR draw + accumulation, hand-scheduled for
+// gfx950 (the whole inner loop of the kernel is this block, P times per element).
+//
+//   S' = S*A + C (mod 2^128) from 32-bit limbs: three 64-bit column chains
+//   (limbs 0-1: s0a0 + C01; limbs 1-2: s0a1 + s1a0; limbs 2-3: s0a2 + s1a1 +
+//   s2a0 + C23) on v_mad_u64_u32, the four limb-3 products on v_mul_lo_u32,
+//   joined by carry adds whose carry-ins are the mads' own carry-outs -- 6
+//   mads + 4 mul_lo + 8 adds, no register shuffling.  Then t = rotr(hi^lo^m,
+//   hi>>58) in 32-bit halves (v_bitop3 + v_alignbit + swap), the raw==0 test
+//   (hi == lo <=> xl == xh == m) folded into a running minimum, and
+//   acc_u += t (and acc_v -= t for an internal pair) on 32-bit halves.
+//
+// Carries live in three SGPR pairs, reused as they die (k1: kE then the acc_u
+// carry; k2: kO, c2, then the acc_v carry; k3: discarded carry-outs, c1, c3).
+// Every VALU-written SGPR (carries, VCC) is read >= 2 instructions later
+// (gfx950 VALU-SGPR-write -> VALU-read hazard).  v0-v9 are fixed scratch (low
+// registers, so the kernel's VGPR budget is not raised).
+#define SA_PCG_DRAW_ASM                                                                  \
+  "v_mad_u64_u32 v[0:1], %[k1], %[s0], %[a0], %[c01]\n\t"   /* E0 = s0a0 + C01, kE */   \
+  "v_mad_u64_u32 v[2:3], %[k3], %[s0], %[a1], 0\n\t"        /* O1 = s0a1 */             \
+  "v_mad_u64_u32 v[4:5], %[k3], %[s0], %[a2], %[c23]\n\t"   /* E2 = s0a2 + C23 */       \
+  "v_mul_lo_u32 v6, %[s0], %[a3]\n\t"                                                    \
+  "v_mad_u64_u32 v[2:3], %[k2], %[s1], %[a0], v[2:3]\n\t"   /* O1 += s1a0, kO */        \
+  "v_mad_u64_u32 v[4:5], %[k3], %[s1], %[a1], v[4:5]\n\t"                                \
+  "v_mul_lo_u32 v7, %[s1], %[a2]\n\t"                                                    \
+  "v_mad_u64_u32 v[4:5], %[k3], %[s2], %[a0], v[4:5]\n\t"                                \
+  "v_mul_lo_u32 v8, %[s2], %[a1]\n\t"                                                    \
+  "v_mul_lo_u32 v9, %[s3], %[a0]\n\t"                                                    \
+  "v_add_co_u32_e64 %[s1], %[k3], v1, v2\n\t"              /* r1 = e1 + o1, c1 */       \
+  "v_addc_co_u32_e64 %[s3], %[k2], v5, v6, %[k2]\n\t"      /* r3 = e3 + p03 + kO */     \
+  "v_add_u32_e32 %[s3], %[s3], v9\n\t"                      /* r3 += p30 */              \
+  "v_addc_co_u32_e64 %[s2], %[k2], v4, v3, %[k3]\n\t"      /* r2 = e2 + o2 + c1, c2 */  \
+  "v_addc_co_u32_e64 %[s2], %[k3], %[s2], 0, %[k1]\n\t"    /* r2 += kE, c3 */           \
+  "v_mov_b32_e32 %[s0], v0\n\t"                             /* r0 = e0 */                \
+  "v_addc_co_u32_e64 %[s3], %[k2], %[s3], v7, %[k2]\n\t"   /* r3 += p12 + c2 */         \
+  "v_addc_co_u32_e64 %[s3], %[k3], %[s3], v8, %[k3]\n\t"   /* r3 += p21 + c3 */         \
+  "v_bitop3_b32 v0, %[s0], %[s2], %[m] bitop3:0x96\n\t"    /* xl */                     \
+  "v_bitop3_b32 v1, %[s1], %[s3], %[m] bitop3:0x96\n\t"    /* xh */                     \
+  "v_cmp_gt_i32_e32 vcc, 0, %[s3]\n\t"                      /* rot >= 32: swap */        \
+  "v_lshrrev_b32_e32 v2, 26, %[s3]\n\t"                     /* rot (& 31 in alignbit) */ \
+  "v_bitop3_b32 v3, v0, v1, %[m] bitop3:0x7e\n\t"          /* 0 iff raw == 0 */         \
+  "v_alignbit_b32 v4, v1, v0, v2\n\t"                                                    \
+  "v_alignbit_b32 v5, v0, v1, v2\n\t"                                                    \
+  "v_min_u32_e32 %[zmin], %[zmin], v3\n\t"                                               \
+  "v_cndmask_b32_e32 v6, v4, v5, vcc\n\t"                   /* t lo */                   \
+  "v_add_co_u32_e64 %[ulo], %[k1], %[ulo], v6\n\t"
+
+#define SA_PCG_DRAW_OUTS                                                                 \
+  [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [zmin] "+v"(zmin),          \
+      [ulo] "+v"(ulo), [uhi] "+v"(uhi), [k1] "=&s"(k1), [k2] "=&s"(k2), [k3] "=&s"(k3)
+#define SA_PCG_DRAW_INS                                                                  \
+  [a0] "s"(a0), [a1] "s"(a1), [a2] "s"(a2), [a3] "s"(a3), [c01] "v"(c01), [c23] "v"(c23),  \
+      [m] "v"(m)
+#define SA_PCG_DRAW_CLOBBERS \
+  "vcc", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9"
+
+__device__ __forceinline__ void pcg_draw_pair(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
+                                              uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
+                                              uint32_t m, uint32_t& zmin, uint32_t& ulo, uint32_t& uhi,
+                                              uint32_t& vlo, uint32_t& vhi) {
+  uint64_t k1, k2, k3;
+  asm volatile(SA_PCG_DRAW_ASM
+               "v_sub_co_u32_e64 %[vlo], %[k2], %[vlo], v6\n\t"
+               "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"  // t hi
+               "v_addc_co_u32_e64 %[uhi], %[k1], %[uhi], v7, %[k1]\n\t"
+               "v_subb_co_u32_e64 %[vhi], %[k2], %[vhi], v7, %[k2]"
+               : SA_PCG_DRAW_OUTS, [vlo] "+v"(vlo), [vhi] "+v"(vhi)
+               : SA_PCG_DRAW_INS
+               : SA_PCG_DRAW_CLOBBERS);
+}
+__device__ __forceinline__ void pcg_draw_one(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
+                                             uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
+                                             uint32_t m, uint32_t& zmin, uint32_t& ulo, uint32_t& uhi) {
+  uint64_t k1, k2, k3;
+  asm volatile(SA_PCG_DRAW_ASM
+               "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"  // t hi
+               "s_nop 0\n\t"
+               "v_addc_co_u32_e64 %[uhi], %[k1], %[uhi], v7, %[k1]"
+               : SA_PCG_DRAW_OUTS
+               : SA_PCG_DRAW_INS
+               : SA_PCG_DRAW_CLOBBERS);
+}
+
 struct StreamLds {
   uint64_t inc_lo, inc_hi, cj_lo, cj_hi, smask, pad;
 };
@@ -334,7 +417,7 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
   }
 
   // ---- prologue: jump every stream from draw 0 to this lane's first element
-  u128 st[P > 0 ? P : 1];
+  uint32_t st[P > 0 ? P : 1][4];  // 128-bit states as 32-bit limbs
   if constexpr (P > 0) {
     Jump jl{1, 0};
     uint64_t pos = first;
@@ -344,7 +427,11 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
 #pragma unroll
     for (int j = 0; j < P; j++) {
       const StreamArg& s = a.s[j];
-      st[j] = apply(jl, ld128(s.s_lo, s.s_hi), ld128(s.inc_lo, s.inc_hi));
+      const u128 v = apply(jl, ld128(s.s_lo, s.s_hi), ld128(s.inc_lo, s.inc_hi));
+      st[j][0] = (uint32_t)lo64(v);
+      st[j][1] = (uint32_t)(lo64(v) >> 32);
+      st[j][2] = (uint32_t)hi64(v);
+      st[j][3] = (uint32_t)(hi64(v) >> 32);
     }
   }
   // The tile-to-tile jump is merged into the first draw of the next tile:
@@ -378,7 +465,9 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
   // wave-uniform trip count: every lane of a wave runs the wave's last tile
   // (out-of-range elements are masked at load/store) so the transpose has
   // all 64 lanes.
-  for (uint64_t i = first; i - 4 * (uint64_t)lane < n; i += stride, tile++) {
+  const uint64_t wave_off = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * 64 * kElemsPerLane);
+  for (uint64_t base = (uint64_t)blockIdx.x * kTileElems; base + wave_off < n; base += stride, tile++) {
+    const uint64_t i = base + (uint64_t)threadIdx.x * kElemsPerLane;
     const bool jstep = tile > 0;             // uniform: this tile's k=0 draws jump
     const u128 M0 = jstep ? AJ1 : kPcgMult;
     const int add0 = jstep ? 2 : 0;          // u64 offset of C_J1 vs inc in StreamLds
@@ -410,30 +499,38 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
     uint64_t fin[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      uint64_t acc[L];
+      uint32_t al[L], ah[L];  // per-client accumulators as 32-bit halves
 #pragma unroll
-      for (int c = 0; c < L; c++) acc[c] = a.c[c].bias;
+      for (int c = 0; c < L; c++) {
+        al[c] = (uint32_t)a.c[c].bias;
+        ah[c] = (uint32_t)(a.c[c].bias >> 32);
+      }
       if constexpr (P > 0) {
+        const u128 Mk = k == 0 ? M0 : kPcgMult;
+        const uint32_t m0 = (uint32_t)lo64(Mk), m1 = (uint32_t)(lo64(Mk) >> 32);
+        const uint32_t m2 = (uint32_t)hi64(Mk), m3 = (uint32_t)(hi64(Mk) >> 32);
 #pragma unroll
         for (int q = 0; q < P; q++) {
-          uint64_t slo = lo64(st[q]), shi = hi64(st[q]);
-          asm volatile("" : "+v"(slo), "+v"(shi), "+v"(slp));
+          asm volatile("" : "+v"(slp));  // constants re-read from LDS per draw, never hoisted
           typedef __attribute__((address_space(3))) const uint64_t* lds_u64;
           const lds_u64 cp = (lds_u64)(slp + q) + (k == 0 ? add0 : 0);
-          const u128 add = (SA_ABLATE & 16) ? mk128(q, 2 * q + 1) : mk128(cp[1], cp[0]);
-          const uint32_t m = (SA_ABLATE & 16) ? 0u : (uint32_t)slp[q].smask;
-          const u128 sv = mk128(shi, slo) * (k == 0 ? M0 : kPcgMult) + add;
-          const uint64_t t = draw_signed(sv, m, zmin);
-          slo = lo64(sv);
-          shi = hi64(sv);
+          const uint64_t c01 = (SA_ABLATE & 16) ? 2 * q + 1 : cp[0];
+          const uint64_t c23 = (SA_ABLATE & 16) ? q : cp[1];
+          const uint32_t sm = (SA_ABLATE & 16) ? 0u : (uint32_t)slp[q].smask;
           const int cu = q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1);
-          const int cv = q < PI ? Pairs<L>::v(q) : cu;
-          acc[cu] += t;
-          if (q < PI) acc[cv] -= t;
-          asm volatile("" : "+v"(slo), "+v"(shi), "+v"(acc[cu]), "+v"(acc[cv]), "+v"(zmin));
-          st[q] = mk128(shi, slo);
+          if (q < PI) {
+            const int cv = Pairs<L>::v(q);
+            pcg_draw_pair(st[q][0], st[q][1], st[q][2], st[q][3], m0, m1, m2, m3, c01, c23, sm, zmin, al[cu],
+                          ah[cu], al[cv], ah[cv]);
+          } else {
+            pcg_draw_one(st[q][0], st[q][1], st[q][2], st[q][3], m0, m1, m2, m3, c01, c23, sm, zmin, al[cu],
+                         ah[cu]);
+          }
         }
       }
+      uint64_t acc[L];
+#pragma unroll
+      for (int c = 0; c < L; c++) acc[c] = pack64(al[c], ah[c]);
       // ---- finish element k: add the quantized value (or the prior pass)
       uint64_t s_k = 0;
 #pragma unroll

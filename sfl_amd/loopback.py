@@ -123,8 +123,8 @@ class LoopbackServer:
         t2 = time.perf_counter()
         if keep_masked:
             self.last_masked = [h.numpy().view(np.uint64).copy() for h in host]
-        for c in self.conns:
-            W.send_frame(c, W.RESULT, out, rnd=rnd)
+        with ThreadPoolExecutor(len(self.conns)) as ex:  # concurrent sends (sendall drops the GIL)
+            list(ex.map(lambda c: W.send_frame(c, W.RESULT, out, rnd=rnd), self.conns))
         t3 = time.perf_counter()
         return out, {"recv_h2d_s": t_recv - t0, "sum_decode_d2h_s": t2 - t1, "broadcast_s": t3 - t2,
                      "round_s": t3 - t0}
@@ -232,11 +232,12 @@ def client_process(party: str, index: int, port: int, n: int, rounds: int, seeds
                    out_q) -> None:
     """Entry point of one spawned client party."""
     try:
+        xs = [synthetic_gradient(index, n, r) for r in range(rounds)]  # generated outside the rounds
         cl = LoopbackClient(party, index, port, gpu=gpu, fxp_bits=fxp_bits, seeds=seeds)
         cl.handshake()
         stats = []
         for r in range(rounds):
-            st = cl.submit(synthetic_gradient(index, n, r), r, weight)
+            st = cl.submit(xs[r], r, weight)
             res = cl.result()
             st["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))
             stats.append(st)

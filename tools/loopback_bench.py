@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Host-resident secure aggregation over loopback sockets (BASELINE north
+star: "this path starts and ends in host memory"; config 5's H2D/D2H-inclusive
+rate).  C client processes + this process as the server on one GPU; every
+round moves each client's fp32 gradient H2D, masks it, moves the masked u64
+vector D2H, sends it over 127.0.0.1, and the server receives, H2D, sums,
+decodes and broadcasts the float64 result.
+
+usage: python tools/loopback_bench.py [--clients 8] [--elems 100000000] [--rounds 3]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--elems", type=int, default=100_000_000)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+    import numpy as np
+
+    from sfl_amd.loopback import run_loopback
+
+    names = [f"client{c}" for c in range(args.clients)]
+    seeds = {a: {b: (0x5ECA66 << 32) | (min(i, j) << 16) | max(i, j) for j, b in enumerate(names) if b != a}
+             for i, a in enumerate(names)}
+    res, timings, stats, _ = run_loopback(names, args.elems, args.rounds, seeds=seeds, timeout=900)
+    steady = timings[1:] if len(timings) > 1 else timings
+    rs = float(np.median([t["round_s"] for t in steady]))
+    cl = [s for per in stats.values() for s in per[1:] or per]
+    out = {
+        "metric": "host-resident grad elems/s (loopback sockets, H2D/D2H inclusive)",
+        "clients": args.clients, "elems_per_client": args.elems, "rounds": args.rounds,
+        "round_s_median": rs, "grad_elems_per_s": args.clients * args.elems / rs,
+        "server": {k: float(np.median([t[k] for t in steady])) for k in steady[0]},
+        "client_h2d_mask_d2h_s_median": float(np.median([s["h2d_mask_d2h_s"] for s in cl])),
+        "client_send_s_median": float(np.median([s["send_s"] for s in cl])),
+        "wire_bytes_per_round": args.clients * args.elems * 8,
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
