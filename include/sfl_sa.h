@@ -164,6 +164,46 @@ int sa_decode(const uint64_t* s, uint64_t n, int fxp_bits, double divisor,
 int sa_sum_f64(const double* const* w, int k, uint64_t n, double* out, void* stream);
 
 /* ------------------------------------------------------------------ */
+/* GaussianModelDP pre-step (sfl/security/privacy/mechanism/            */
+/* mechanism_fl.py:62-130), applied by a client before masking:         */
+/*   x' = x * min(1, clip / ||x||) + N(0, sigma^2) / num_updates        */
+/* in float32, sigma = noise_multiplier * clip * clip as the reference  */
+/* computes it.  ||x|| is the global norm over all layers (or, with     */
+/* sumsq_layer, min(1, clip / sqrt(||layer|| * ||all||)) per layer,     */
+/* is_clip_each_layer).  The noise is Philox4x32-10 + Box-Muller keyed   */
+/* by (key, element index), not numpy's unseeded global MT19937 stream:  */
+/* parity for the noise is distributional, for the clip exact up to the  */
+/* float32 rounding of the norm.                                         */
+/* ------------------------------------------------------------------ */
+
+#define SA_DP_PARTIALS 1024 /* doubles of scratch for sa_sumsq_f32 */
+
+typedef struct sa_dp {
+  const double* sumsq;       /* device: sum of x^2 over the clipping group (sa_sumsq_f32) */
+  const double* sumsq_layer; /* device, optional: this layer's sum of squares */
+  float l2_norm_clip;
+  float noise_std;   /* sigma */
+  float num_updates; /* divisor of the noise (> 0) */
+  uint32_t reserved;
+  uint64_t key;      /* Philox key */
+  uint64_t counter0; /* noise index of element 0 (multiple of 4) */
+} sa_dp;
+
+/* *sumsq (+)= sum x[i]^2 in float64, deterministic fixed-order reduction;
+ * `partials` is caller scratch of SA_DP_PARTIALS doubles. */
+int sa_sumsq_f32(const float* x, uint64_t n, double* partials, double* sumsq, int accumulate, void* stream);
+
+/* out = clip-and-noise(x) (out may alias x). */
+int sa_dp_perturb_f32(const float* x, uint64_t n, const sa_dp* dp, float* out, void* stream);
+
+/* sa_mask of the DP-perturbed float32 x without materialising it: the
+ * clip+noise runs inside the masking kernel on the loaded tile.  Equal bit
+ * for bit to sa_dp_perturb_f32 followed by sa_mask. */
+int sa_mask_dp(const float* x, uint64_t n, double weight, int fxp_bits, const sa_mask_stream* streams,
+               int n_streams, const sa_dp* dp, uint64_t* out, uint64_t* sum_accum, uint64_t* digest,
+               uint32_t* flags, void* stream);
+
+/* ------------------------------------------------------------------ */
 /* multi-GPU exchange: the masked-sum reduce over RCCL (xGMI)           */
 /* Replaces the RayFed `.to(server)` transfer + server np.sum           */
 /* (sfl/distributed/op_strategy.py:131-141; sparse_plain_aggregator.py:86) */

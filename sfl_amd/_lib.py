@@ -23,13 +23,14 @@ SA_ERR_RCCL = -4
 SA_F32, SA_F64, SA_I64 = 0, 1, 2
 SA_FLAG_PRG_REJECT = 1
 SA_UNIQUE_ID_BYTES = 128
+SA_DP_PARTIALS = 1024
 
 # every symbol include/sfl_sa.h declares (checked by tests/test_boundary.py)
 EXPORTED = (
     "sa_abi_version", "sa_last_error", "sa_pcg64_from_seed", "sa_pcg64_advance",
     "sa_pcg64_raw_host", "sa_mask", "sa_fused_clients", "sa_sum_u64", "sa_decode",
     "sa_sum_f64", "sa_comm_unique_id", "sa_comm_init", "sa_comm_reduce_u64",
-    "sa_comm_allreduce_u64", "sa_comm_destroy",
+    "sa_comm_allreduce_u64", "sa_comm_destroy", "sa_sumsq_f32", "sa_dp_perturb_f32", "sa_mask_dp",
 )
 
 
@@ -65,6 +66,13 @@ class MaskStream(C.Structure):
 
 class LocalClient(C.Structure):
     _fields_ = [("x", C.c_void_p), ("weight", C.c_double), ("masked_out", C.c_void_p)]
+
+
+class DP(C.Structure):
+    """sa_dp: GaussianModelDP pre-step parameters."""
+    _fields_ = [("sumsq", C.c_void_p), ("sumsq_layer", C.c_void_p), ("l2_norm_clip", C.c_float),
+                ("noise_std", C.c_float), ("num_updates", C.c_float), ("reserved", C.c_uint32),
+                ("key", C.c_uint64), ("counter0", C.c_uint64)]
 
 
 _lock = threading.Lock()

@@ -137,6 +137,13 @@ extern "C" int sa_mask(const void* x, int x_type, int compute_type, uint64_t n, 
                        const void* weight_vec, int fxp_bits, const sa_mask_stream* streams,
                        int n_streams, uint64_t* out, uint64_t* sum_accum, uint64_t* digest,
                        uint32_t* flags, void* stream) {
+  return sa_mask_impl(x, x_type, compute_type, n, weight, weight_vec, fxp_bits, streams, n_streams, out,
+                      sum_accum, digest, flags, stream, nullptr);
+}
+
+int sa_mask_impl(const void* x, int x_type, int compute_type, uint64_t n, double weight, const void* weight_vec,
+                 int fxp_bits, const sa_mask_stream* streams, int n_streams, uint64_t* out, uint64_t* sum_accum,
+                 uint64_t* digest, uint32_t* flags, void* stream, const sa_dp* dp) {
   if (check_type(x_type, "sa_mask x_type") || check_type(compute_type, "sa_mask compute_type"))
     return SA_ERR_ARG;
   if (!out || n_streams < 0 || (n_streams > 0 && !streams) || fxp_bits < 0 || fxp_bits > 62) {
@@ -183,6 +190,16 @@ extern "C" int sa_mask(const void* x, int x_type, int compute_type, uint64_t n, 
     a.digests = last ? digest : nullptr;
     a.do_digest = (last && digest) ? 1 : 0;
     a.flags = flags;
+    if (dp) {
+      a.dp_on = 1;
+      a.dp_clip = dp->l2_norm_clip;
+      a.dp_sigma = dp->noise_std;
+      a.dp_updates = dp->num_updates;
+      a.dp_sumsq = dp->sumsq;
+      a.dp_sumsq_layer = dp->sumsq_layer;
+      a.dp_key = dp->key;
+      a.dp_block0 = dp->counter0 / 4;
+    }
     const int ct = compute_type;
     LaunchFn fn = find_clients_kernel(x_type, ct, 1, cnt);
     if (!fn) {

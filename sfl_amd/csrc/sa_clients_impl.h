@@ -35,6 +35,7 @@
 #include "../../include/sfl_sa.h"
 #include "pcg128.h"
 #include "sa_internal.h"
+#include "sa_philox.h"
 
 namespace sa {
 
@@ -220,6 +221,17 @@ __device__ __forceinline__ uint64_t quantize(XT x, CT w, const KArgs& a) {
   if constexpr (std::is_integral<CT>::value) {  // int64 arithmetic, wraps mod 2^64
     return (uint64_t)(long long)x * (uint64_t)w * ((uint64_t)1 << a.fxp_bits);
   } else if constexpr (sizeof(CT) == 4) {
+    // (x*w)*2^fxp == x*(w*2^fxp) exactly whenever w*2^fxp is finite: scaling
+    // by a power of two commutes with rounding, and where the product is
+    // subnormal it truncates to 0 either way.  Values of |p| < 2^31 (every
+    // gradient in practice) convert with one v_cvt_i32_f32; a wave with any
+    // larger / non-finite value takes the full int64 conversion.
+    const float ws = __fmul_rn((float)w, a.scale_f);  // wave-uniform
+    if (__builtin_isfinite(ws)) {
+      const float p = __fmul_rn((float)x, ws);
+      if (!__any(!(__builtin_fabsf(p) < 0x1p31f))) return (uint64_t)(int64_t)(int32_t)p;
+      return trunc_i64(p);
+    }
     const float p = __fmul_rn((float)x, (float)w);
     return trunc_i64(__fmul_rn(p, a.scale_f));
   } else {
@@ -460,6 +472,11 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
   const int lane = threadIdx.x & 63;
   uint64_t* const tw = tr_lds + (threadIdx.x & ~63) * kElemsPerLane;
 
+  float dp_s = 1.0f;
+  if constexpr (kGeneral && std::is_same<XT, float>::value && std::is_same<CT, float>::value) {
+    if (a.dp_on) dp_s = dp_scale(a.dp_sumsq, a.dp_sumsq_layer, a.dp_clip);
+  }
+
   lds_ptr slp = (lds_ptr)(sl);
   int tile = 0;
   // wave-uniform trip count: every lane of a wave runs the wave's last tile
@@ -488,6 +505,13 @@ __global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
           xv[c] = bload4<XT>(rx[c], i, n);
         }
         if (kGeneral && a.c[c].wvec) wv[c] = bload4<CT>(rw[kGeneral ? c : 0], i, n);
+      }
+    }
+    if constexpr (kGeneral && std::is_same<XT, float>::value && std::is_same<CT, float>::value) {
+      if (a.dp_on && !a.continue_mode) {  // fused DP pre-step (sa_mask_dp)
+        const Normal4 z = gauss4(a.dp_key, a.dp_block0 + (i >> 2));
+#pragma unroll
+        for (int k = 0; k < 4; k++) xv[0].v[k] = dp_apply(xv[0].v[k], dp_s, z.z[k], a.dp_sigma, a.dp_updates);
       }
     }
 
@@ -628,6 +652,7 @@ int launch_clients(const KArgs& in, void* stream) {
         if (a.c[c].masked_out) a.c[c].masked_out += off;
       }
       if (a.sum_out) a.sum_out += off;
+      a.dp_block0 += off / kElemsPerLane;
       const Jump jo = jump_of(off);
       for (int j = 0; j < P; j++) {
         const u128 s = apply(jo, mk128(a.s[j].s_hi, a.s[j].s_lo), mk128(a.s[j].inc_hi, a.s[j].inc_lo));

@@ -4,6 +4,13 @@
 
 void sa_set_error(const char* fmt, ...);
 
+struct sa_mask_stream;
+struct sa_dp;
+// sa_mask with an optional fused GaussianModelDP pre-step (sa_api.hip)
+int sa_mask_impl(const void* x, int x_type, int compute_type, uint64_t n, double weight, const void* weight_vec,
+                 int fxp_bits, const struct sa_mask_stream* streams, int n_streams, uint64_t* out,
+                 uint64_t* sum_accum, uint64_t* digest, uint32_t* flags, void* stream, const struct sa_dp* dp);
+
 #define SA_HIP_CHECK(expr)                                                              \
   do {                                                                                  \
     hipError_t e_ = (expr);                                                             \
@@ -50,6 +57,12 @@ struct KArgs {
   int32_t sum_mode;       // 0 none, 1 store, 2 accumulate
   int32_t continue_mode;  // acc starts from masked_out instead of quantize(x)
   int32_t do_digest;
+  // GaussianModelDP pre-step fused into quantize (single-client fp32 only)
+  int32_t dp_on;
+  float dp_clip, dp_sigma, dp_updates;
+  const double* dp_sumsq;
+  const double* dp_sumsq_layer;
+  uint64_t dp_key, dp_block0;  // Philox key; counter block of element 0
 };
 
 typedef int (*LaunchFn)(const KArgs& a, void* stream);

@@ -166,3 +166,54 @@ def sum_f64(ins: Sequence[torch.Tensor], out: torch.Tensor) -> torch.Tensor:
     L.check(L.lib().sa_sum_f64(ptrs, len(ins), out.numel(), _ptr(out), C.c_void_p(_stream(out))),
             "sa_sum_f64")
     return out
+
+
+# ---------------------------------------------------------------------------
+# GaussianModelDP pre-step (sa_sumsq_f32 / sa_dp_perturb_f32 / sa_mask_dp)
+# ---------------------------------------------------------------------------
+def make_dp(sumsq: torch.Tensor, *, l2_norm_clip: float, noise_std: float, num_updates: float, key: int,
+            counter0: int = 0, sumsq_layer: torch.Tensor | None = None) -> L.DP:
+    if counter0 % 4:
+        raise ValueError("counter0 must be a multiple of 4")
+    d = L.DP()
+    d.sumsq = sumsq.data_ptr()
+    d.sumsq_layer = sumsq_layer.data_ptr() if sumsq_layer is not None else None
+    d.l2_norm_clip = float(l2_norm_clip)
+    d.noise_std = float(noise_std)
+    d.num_updates = float(num_updates)
+    d.key = int(key) & ((1 << 64) - 1)
+    d.counter0 = int(counter0)
+    return d
+
+
+def sumsq_f32(x: torch.Tensor, out: torch.Tensor, partials: torch.Tensor, *, accumulate: bool = False) -> torch.Tensor:
+    """out[0] (+)= sum(x^2) in float64 (deterministic)."""
+    _require_gpu(x, out, partials)
+    if x.dtype != torch.float32 or out.dtype != torch.float64 or partials.numel() < L.SA_DP_PARTIALS:
+        raise ValueError("sumsq_f32: float32 x, float64 out, SA_DP_PARTIALS float64 partials")
+    L.check(L.lib().sa_sumsq_f32(_ptr(x), x.numel(), _ptr(partials), _ptr(out), int(bool(accumulate)),
+                                 C.c_void_p(_stream(out))), "sa_sumsq_f32")
+    return out
+
+
+def dp_perturb(x: torch.Tensor, out: torch.Tensor, dp: L.DP) -> torch.Tensor:
+    _require_gpu(x, out)
+    if x.dtype != torch.float32 or out.dtype != torch.float32 or out.numel() != x.numel():
+        raise ValueError("dp_perturb: float32 x and out of equal size")
+    L.check(L.lib().sa_dp_perturb_f32(_ptr(x), x.numel(), C.byref(dp), _ptr(out), C.c_void_p(_stream(out))),
+            "sa_dp_perturb_f32")
+    return out
+
+
+def mask_dp(x: torch.Tensor, out: torch.Tensor, streams: Sequence[tuple], dp: L.DP, *, weight: float = 1.0,
+            fxp_bits: int = 18, sum_accum: torch.Tensor | None = None, digest: torch.Tensor | None = None,
+            flags: torch.Tensor | None = None) -> torch.Tensor:
+    """sa_mask of the DP-perturbed float32 x, perturbation fused into the kernel."""
+    _require_gpu(x, out, sum_accum, digest, flags)
+    if x.dtype != torch.float32 or x.numel() != out.numel():
+        raise ValueError("mask_dp: float32 x with out of equal size")
+    sarr = make_streams(streams)
+    L.check(L.lib().sa_mask_dp(_ptr(x), x.numel(), float(weight), int(fxp_bits), sarr, len(streams), C.byref(dp),
+                               _ptr(out), _ptr(sum_accum), _ptr(digest), _ptr(flags), C.c_void_p(_stream(out))),
+            "sa_mask_dp")
+    return out

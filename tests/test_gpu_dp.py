@@ -1,0 +1,118 @@
+"""DP pre-step on the GPU vs the oracle (oracle/dp.py):
+norm reduction, clip (exact), Philox noise (within float tolerance of the
+numpy restatement), and the fused sa_mask_dp == perturb-then-mask bit for bit."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+from oracle import dp as D  # noqa: E402
+from oracle import secagg as o  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _K():
+    from sfl_amd import kernels as K
+
+    return K
+
+
+def _sumsq(x):
+    from sfl_amd import _lib as L
+
+    out = torch.zeros(1, dtype=torch.float64, device=DEV)
+    part = torch.empty(L.SA_DP_PARTIALS, dtype=torch.float64, device=DEV)
+    return _K().sumsq_f32(x, out, part)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 1027, 1_000_003])
+def test_sumsq_deterministic_and_accurate(n):
+    x = torch.randn(n, device=DEV)
+    a, b = _sumsq(x), _sumsq(x)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    ref = float(np.sum(x.cpu().numpy().astype(np.float64) ** 2))
+    assert abs(a.item() - ref) <= 1e-12 * ref
+
+
+@pytest.mark.parametrize("clip", [0.5, 1e6])
+def test_perturb_clip_exact_without_noise(clip):
+    K = _K()
+    n = 70_001
+    x = torch.randn(n, device=DEV) * 3
+    s = _sumsq(x)
+    dp = K.make_dp(s, l2_norm_clip=clip, noise_std=0.0, num_updates=4, key=1)
+    y = K.dp_perturb(x, torch.empty_like(x), dp)
+    torch.cuda.synchronize()
+    scale = D.clip_scale(s.item(), clip)
+    assert np.array_equal(y.cpu().numpy(), x.cpu().numpy() * scale)
+
+
+def test_perturb_noise_matches_oracle_stream():
+    K = _K()
+    n, key, ctr = 100_003, 0xDEADBEEF12345678, 4 * 1000
+    x = torch.zeros(n, device=DEV)
+    s = _sumsq(torch.ones(4, device=DEV))
+    dp = K.make_dp(s, l2_norm_clip=1.0, noise_std=1.5, num_updates=4, key=key, counter0=ctr)
+    y = K.dp_perturb(x, torch.empty_like(x), dp).cpu().numpy()
+    z = D.gauss(key, ctr, n)
+    exp = D.perturb(np.zeros(n, np.float32), 1.0, z, 1.5, 4)
+    assert np.allclose(y, exp, rtol=2e-5, atol=2e-6)
+    assert abs(y.mean()) < 0.01 and abs(y.std() - 1.5 / 4) < 0.01
+
+
+@pytest.mark.parametrize("nstreams", [0, 3, 17])
+def test_fused_mask_dp_equals_perturb_then_mask(nstreams):
+    K, L = _K(), None
+    from sfl_amd import _lib as L
+
+    n = 50_003
+    x = torch.randn(n, device=DEV) * 0.05
+    s = _sumsq(x)
+    seeds = [o.pair_seed(0, j + 1) for j in range(nstreams)]
+    streams = [(L.pcg64_from_seed(sd), 1 if j % 2 else -1, j) for j, sd in enumerate(seeds)]
+    mk = lambda: K.make_dp(s, l2_norm_clip=0.3, noise_std=0.01, num_updates=8, key=77, counter0=40)  # noqa: E731
+    xp = K.dp_perturb(x, torch.empty_like(x), mk())
+    m1 = torch.empty(n, dtype=torch.int64, device=DEV)
+    d1 = torch.zeros(1, dtype=torch.int64, device=DEV)
+    K.mask(xp, m1, streams, weight=3.0, digest=d1)
+    m2 = torch.empty(n, dtype=torch.int64, device=DEV)
+    d2 = torch.zeros(1, dtype=torch.int64, device=DEV)
+    K.mask_dp(x, m2, streams, mk(), weight=3.0, digest=d2)
+    torch.cuda.synchronize()
+    assert torch.equal(m1, m2) and torch.equal(d1, d2)
+    # and the masked vector is the oracle's for the perturbed input
+    exp = o.quantize(xp.cpu().numpy(), 3)
+    for sd, (_, sg, _) in zip(seeds, streams):
+        mm = o.mask_stream(sd, n)
+        exp = exp + mm if sg > 0 else exp - mm
+    assert np.array_equal(m2.cpu().numpy().view(np.uint64), exp)
+
+
+@pytest.mark.parametrize("each_layer", [False, True])
+def test_gaussian_model_dp_class_vs_oracle(each_layer):
+    from sfl_amd.security.privacy import GaussianModelDP
+
+    rng = np.random.default_rng(5)
+    layers = [rng.standard_normal((50, 4)).astype(np.float32), rng.standard_normal(50).astype(np.float32),
+              rng.standard_normal((3, 50)).astype(np.float32)]
+    dp = GaussianModelDP(noise_multiplier=0.7, num_clients=8, l2_norm_clip=2.0, is_clip_each_layer=each_layer,
+                         seed=99)
+    got = dp(layers)
+    exp = D.gaussian_model_dp(layers, 0.7, 8, 2.0, key=99, is_clip_each_layer=each_layer)
+    for g, e, a in zip(got, exp, layers):
+        assert isinstance(g, np.ndarray) and g.dtype == np.float32 and g.shape == a.shape
+        assert np.allclose(g, e, rtol=1e-5, atol=1e-6)
+    # noise-free: exact clip
+    dp0 = GaussianModelDP(noise_multiplier=0.0, num_clients=8, l2_norm_clip=2.0, seed=1)
+    got0 = dp0(layers)
+    exp0 = D.gaussian_model_dp(layers, 0.0, 8, 2.0)
+    for g, e in zip(got0, exp0):
+        assert np.array_equal(g, e)
