@@ -99,6 +99,9 @@ def _declare(lib):
     lib.sa_comm_reduce_u64.argtypes = [vp, vp, vp, u64, i32, vp]
     lib.sa_comm_allreduce_u64.argtypes = [vp, vp, vp, u64, vp]
     lib.sa_comm_destroy.argtypes = [vp]
+    lib.sa_sumsq_f32.argtypes = [vp, u64, vp, vp, i32, vp]
+    lib.sa_dp_perturb_f32.argtypes = [vp, u64, P(DP), vp, vp]
+    lib.sa_mask_dp.argtypes = [vp, u64, dbl, i32, P(MaskStream), i32, P(DP), vp, vp, vp, vp, vp]
     for name in EXPORTED:
         if name not in ("sa_last_error",):
             getattr(lib, name).restype = i32

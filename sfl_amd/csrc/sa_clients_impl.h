@@ -404,8 +404,13 @@ struct Pairs {
 // the kernel
 // ----------------------------------------------------------------------------
 
+// waves per SIMD the register allocation must allow: shapes with 17+ streams
+// (e.g. 4 local clients + 4 cross = 22) otherwise land a few VGPRs above the
+// 3-wave limit of 168
+constexpr int clients_waves(int streams) { return streams >= 17 ? 3 : (streams >= 13 && streams <= 15) ? 4 : 2; }
+
 template <typename XT, typename CT, int L, int X>
-__global__ void __launch_bounds__(kBlockThreads, 2) k_clients(const KArgs a) {
+__global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count + L * X)) k_clients(const KArgs a) {
   constexpr int PI = Pairs<L>::count;
   constexpr int P = PI + L * X;
   constexpr bool kGeneral = (L == 1);  // continue mode + per-element weights

@@ -178,8 +178,10 @@ class LoopbackClient:
                           torch.empty(n, dtype=torch.int64, device=dev))
         return self._bufs[1:]
 
-    def submit(self, x: np.ndarray, rnd: int, weight=None) -> dict:
-        """Mask ``x`` (host float32) for round ``rnd`` and send it."""
+    def submit(self, x: np.ndarray, rnd: int, weight=None, dp=None) -> dict:
+        """Mask ``x`` (host float32) for round ``rnd`` and send it.  With a
+        ``GaussianModelDP`` ``dp``, its clip + noise runs inside the masking
+        kernel (``sa_mask_dp``) on the device copy of ``x``."""
         import torch
 
         from . import _lib as L
@@ -194,8 +196,12 @@ class LoopbackClient:
         dig = torch.zeros(1, dtype=torch.int64, device=dev)
         flags = torch.zeros(1, dtype=torch.int32, device=dev)
         with torch.cuda.device(dev):
-            K.mask(dx, dm, self.masker.streams(), weight=1.0 if weight is None else weight,
-                   fxp_bits=self.fxp_bits, digest=dig, flags=flags)
+            w = 1.0 if weight is None else weight
+            if dp is None:
+                K.mask(dx, dm, self.masker.streams(), weight=w, fxp_bits=self.fxp_bits, digest=dig, flags=flags)
+            else:
+                K.mask_dp(dx, dm, self.masker.streams(), dp.params(dp.sumsq([dx]), n), weight=w,
+                          fxp_bits=self.fxp_bits, digest=dig, flags=flags)
         hm.copy_(dm, non_blocking=True)
         torch.cuda.synchronize(dev)
         if int(flags.item()) & L.SA_FLAG_PRG_REJECT:

@@ -111,7 +111,8 @@ class FedAvgW:
         self.model.load_state_dict(new)
 
     # ------------------------------------------------------- training
-    def train_step(self, weights, cur_steps: int, train_steps: int, refresh_data: bool = False, **kwargs):
+    def train_step(self, weights, cur_steps: int, train_steps: int, refresh_data: bool = False,
+                   dp_strategy=None, **kwargs):
         self.model.train()
         if refresh_data:
             self._reset_data_iter()
@@ -127,7 +128,10 @@ class FedAvgW:
             loss.backward()
             self.optimizer.step()
         self.last_loss = float(loss.item()) if loss is not None else float("nan")
-        return self.get_weights(return_numpy=True), num_sample
+        model_weights = self.get_weights(return_numpy=True)
+        if dp_strategy is not None and dp_strategy.model_gdp is not None:  # fed_avg_w.py:80-85
+            model_weights = dp_strategy.model_gdp(model_weights)
+        return model_weights, num_sample
 
     def apply_weights(self, weights, **kwargs):
         if weights is not None:
@@ -153,7 +157,7 @@ class FLModel:
 
     def __init__(self, server: Optional[PYU] = None, device_list: List[PYU] = (), model: TorchModel = None,
                  aggregator=None, strategy: str = "fed_avg_w", backend: str = "torch",
-                 random_seed: Optional[int] = None, train_device=None, **kwargs):
+                 random_seed: Optional[int] = None, train_device=None, dp_strategy=None, **kwargs):
         if (strategy, backend) not in _STRATEGIES:
             raise NotImplementedError(f"strategy {strategy!r} / backend {backend!r}")
         if aggregator is None:
@@ -162,6 +166,7 @@ class FLModel:
         self.device_list = list(device_list)
         self._aggregator = aggregator
         self.strategy = strategy
+        self.dp_strategy = dp_strategy
         self._workers: Dict[PYU, FedAvgW] = {
             d: _STRATEGIES[(strategy, backend)](model, d, random_seed, train_device) for d in self.device_list}
 
@@ -191,7 +196,8 @@ class FLModel:
                 for idx, (d, w) in enumerate(self._workers.items()):
                     cp = reveal(model_params_list[idx]) if model_params_list is not None else None
                     n_steps = aggregate_freq if step + aggregate_freq < steps else steps - step
-                    p, n = w.train_step(cp, epoch * steps + step, n_steps, refresh_data=(step == 0))
+                    p, n = w.train_step(cp, epoch * steps + step, n_steps, refresh_data=(step == 0),
+                                        dp_strategy=self.dp_strategy)
                     params.append(PYUObject(d, p))
                     nums.append(n)
                 t_agg = time.perf_counter()

@@ -109,3 +109,15 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
     finally:
         monkeypatch.delenv("SFL_SA_LIB")
         importlib.reload(L)
+
+
+def test_every_entry_point_has_ctypes_signature():
+    """ctypes converts Python floats only with declared argtypes: every
+    exported entry point that takes arguments must have them."""
+    from sfl_amd import _lib as L
+
+    lib = L.lib()
+    for name in L.EXPORTED:
+        if name in ("sa_abi_version", "sa_last_error"):
+            continue
+        assert getattr(lib, name).argtypes, name

@@ -184,3 +184,54 @@ def test_single_participant_and_errors():
     agg2 = SecureAggregator(a, [a, b])
     with pytest.raises(AssertionError):
         agg2.sum([a(lambda: x)()], axis=0)  # dropout is not supported
+
+
+def test_homo_binning_style_integer_sums():
+    """Secondary caller: HomoBinning sums per-party
+    int64 missing counts and [cols x split-points] rank tables with
+    aggregator.sum (sfl/preprocessing/binning/homo_binning.py:143-167,
+    homo_binning_base.py:133-144, 208-224).  Integer data stays int64 through
+    quantization, so the decoded sums are exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    parties = [PYU(n, 0) for n in ("alice", "bob", "carol")]
+    agg = SecureAggregator(PYU("server", 0), parties)
+    rng = np.random.default_rng(11)
+    for it in range(5):
+        missing = [rng.integers(0, 1000, 9) for _ in parties]
+        ranks = [rng.integers(0, 10**6, (9, 11)) for _ in parties]
+        got_m = rv(agg.sum([p(lambda a=a: a)() for p, a in zip(parties, missing)], axis=0))
+        got_r = rv(agg.sum([p(lambda a=a: a)() for p, a in zip(parties, ranks)], axis=0))
+        assert np.array_equal(got_m, np.sum(missing, axis=0).astype(np.float64))
+        assert np.array_equal(got_r, np.sum(ranks, axis=0).astype(np.float64))
+
+
+def test_subclass_with_reference_constructor_contract():
+    """StatefulFedGenAggregator subclasses SecureAggregator as
+    (device, participants, fxp_bits) and calls super().average(data, axis,
+    None) (sfl/security/aggregation/stateful_fedgen_aggregator.py:23-60)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    class StatefulFedGenLike(SecureAggregator):
+        def __init__(self, device, participants, server_actor, fxp_bits: int = 18):
+            super().__init__(device, participants, fxp_bits)
+            self.server_actor = server_actor
+
+        def average(self, data, axis=None, weights=None):
+            avg = super().average(data, axis, None)
+            if weights is not None:
+                return self._device(lambda x: x)({"generator_params": self.server_actor, "model_params": avg})
+            return avg
+
+    parties = [PYU("a", 0), PYU("b", 0)]
+    agg = StatefulFedGenLike(PYU("s", 0), parties, "gen-weights", 18)
+    xs = [np.arange(6, dtype=np.float32) * (i + 1) for i in range(2)]
+    out = rv(agg.average([p(lambda x=x: x)() for p, x in zip(parties, xs)], axis=0, weights=[1, 1]))
+    assert out["generator_params"] == "gen-weights"
+    assert np.allclose(rv(out["model_params"]), (xs[0] + xs[1]) / 2, atol=2 * 2.0**-18)
