@@ -23,6 +23,7 @@ The GPU kernels are the product path; nothing here falls back to the CPU.
 from __future__ import annotations
 
 import json
+import os
 import socket
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -31,6 +32,13 @@ import numpy as np
 
 from . import wire as W
 from .wire import META
+
+CHUNK_ELEMS = 8 << 20  # 64 MiB of u64 per pinned staging buffer
+
+
+def chunk_elems() -> int:
+    """Staging chunk (elements); SFL_LOOPBACK_CHUNK_ELEMS overrides (tests)."""
+    return int(os.environ.get("SFL_LOOPBACK_CHUNK_ELEMS", CHUNK_ELEMS))
 
 
 class LoopbackServer:
@@ -76,21 +84,26 @@ class LoopbackServer:
 
         if self._bufs is None or self._bufs[0] != n:
             dev = torch.device("cuda", self.gpu)
-            host = [torch.empty(n, dtype=torch.int64).pin_memory() for _ in self.conns]
+            ce = min(n, chunk_elems())
+            ring = [[torch.empty(ce, dtype=torch.int64).pin_memory() for _ in range(2)] for _ in self.conns]
             devb = [torch.empty(n, dtype=torch.int64, device=dev) for _ in self.conns]
             streams = [torch.cuda.Stream(dev) for _ in self.conns]
-            self._bufs = (n, host, devb, streams)
+            self._bufs = (n, ring, devb, streams)
         return self._bufs[1:]
 
     def round(self, n: int, rnd: int, *, average: bool = False, verify_digest: bool = False,
               keep_masked: bool = False):
-        """One aggregation round over n-element vectors -> (float64 result, timings)."""
+        """One aggregation round over n-element vectors -> (float64 result, timings).
+
+        Each connection's frame streams through a ring of two pinned chunk
+        buffers (chunk_elems() u64): chunk j is copied to the device while chunk
+        j+1 is received, so host memory stays O(chunk) per client."""
         import torch
 
         from . import kernels as K
 
         dev = torch.device("cuda", self.gpu)
-        host, devb, streams = self._buffers(n)
+        ring, devb, streams = self._buffers(n)
         t0 = time.perf_counter()
         weights = [None] * len(self.conns)
 
@@ -98,13 +111,26 @@ class LoopbackServer:
             conn = self.conns[i]
             _, mv = W.recv_frame(conn, expect_kind=META)
             weights[i] = json.loads(bytes(mv)).get("weight")
-            h, _ = W.recv_frame(conn, into=host[i], expect_kind=W.MASKED)
-            if h.count != n or h.round != rnd:
+            h = W.recv_header(conn, expect_kind=W.MASKED)
+            if h.count != n or h.round != rnd or h.dtype != W.U64:
                 raise W.WireError(f"client {i}: frame of {h.count} elems for round {h.round}, want {n} / {rnd}")
-            if verify_digest and h.digest != W.xor_digest(host[i].numpy()):
+            events = [None, None]
+            dig = [0]
+
+            def on_chunk(b, off, nbytes):
+                k, e0 = nbytes // 8, off // 8
+                if verify_digest:
+                    dig[0] ^= W.xor_digest(ring[i][b].numpy()[:k])
+                with torch.cuda.stream(streams[i]):
+                    devb[i][e0:e0 + k].copy_(ring[i][b][:k], non_blocking=True)
+                    events[b] = torch.cuda.Event()
+                    events[b].record(streams[i])
+                if events[1 - b] is not None:  # the other buffer is received into next
+                    events[1 - b].synchronize()
+
+            W.recv_payload_chunked(conn, h, ring[i], on_chunk)
+            if verify_digest and h.digest != dig[0]:
                 raise W.WireError(f"client {i}: payload digest mismatch")
-            with torch.cuda.stream(streams[i]):
-                devb[i].copy_(host[i], non_blocking=True)
             return time.perf_counter()
 
         with ThreadPoolExecutor(len(self.conns)) as ex:
@@ -122,7 +148,7 @@ class LoopbackServer:
         out = dec.cpu().numpy()
         t2 = time.perf_counter()
         if keep_masked:
-            self.last_masked = [h.numpy().view(np.uint64).copy() for h in host]
+            self.last_masked = [d.cpu().numpy().view(np.uint64) for d in devb]
         with ThreadPoolExecutor(len(self.conns)) as ex:  # concurrent sends (sendall drops the GIL)
             list(ex.map(lambda c: W.send_frame(c, W.RESULT, out, rnd=rnd), self.conns))
         t3 = time.perf_counter()
@@ -172,47 +198,74 @@ class LoopbackClient:
 
         if self._bufs is None or self._bufs[0] != n:
             dev = torch.device("cuda", self.gpu)
-            self._bufs = (n, torch.empty(n, dtype=torch.float32).pin_memory(),
-                          torch.empty(n, dtype=torch.int64).pin_memory(),
+            ce = min(n, chunk_elems())
+            self._bufs = (n, [torch.empty(ce, dtype=torch.float32).pin_memory() for _ in range(2)],
+                          [torch.empty(ce, dtype=torch.int64).pin_memory() for _ in range(2)],
                           torch.empty(n, dtype=torch.float32, device=dev),
-                          torch.empty(n, dtype=torch.int64, device=dev))
+                          torch.empty(n, dtype=torch.int64, device=dev), torch.cuda.Stream(dev))
         return self._bufs[1:]
 
     def submit(self, x: np.ndarray, rnd: int, weight=None, dp=None) -> dict:
         """Mask ``x`` (host float32) for round ``rnd`` and send it.  With a
         ``GaussianModelDP`` ``dp``, its clip + noise runs inside the masking
-        kernel (``sa_mask_dp``) on the device copy of ``x``."""
+        kernel (``sa_mask_dp``) on the device copy of ``x``.  Host <-> device
+        copies stream through two pinned chunk buffers each way."""
         import torch
 
         from . import _lib as L
         from . import kernels as K
 
         n = x.size
-        hx, hm, dx, dm = self._buffers(n)
+        hx, hm, dx, dm, cs = self._buffers(n)
         dev = dx.device
+        ce = hx[0].numel()
+        xf = np.asarray(x, dtype=np.float32).reshape(-1)
         t0 = time.perf_counter()
-        hx.numpy()[:] = np.asarray(x, dtype=np.float32).reshape(-1)
-        dx.copy_(hx, non_blocking=True)
-        dig = torch.zeros(1, dtype=torch.int64, device=dev)
-        flags = torch.zeros(1, dtype=torch.int32, device=dev)
-        with torch.cuda.device(dev):
+        ev = [None, None]
+        with torch.cuda.stream(cs):
+            for j, lo in enumerate(range(0, n, ce)):
+                b, k = j & 1, min(ce, n - lo)
+                if ev[b] is not None:
+                    ev[b].synchronize()
+                hx[b].numpy()[:k] = xf[lo:lo + k]
+                dx[lo:lo + k].copy_(hx[b][:k], non_blocking=True)
+                ev[b] = torch.cuda.Event()
+                ev[b].record(cs)
+            dig = torch.zeros(1, dtype=torch.int64, device=dev)
+            flags = torch.zeros(1, dtype=torch.int32, device=dev)
             w = 1.0 if weight is None else weight
             if dp is None:
                 K.mask(dx, dm, self.masker.streams(), weight=w, fxp_bits=self.fxp_bits, digest=dig, flags=flags)
             else:
                 K.mask_dp(dx, dm, self.masker.streams(), dp.params(dp.sumsq([dx]), n), weight=w,
                           fxp_bits=self.fxp_bits, digest=dig, flags=flags)
-        hm.copy_(dm, non_blocking=True)
-        torch.cuda.synchronize(dev)
+        cs.synchronize()
         if int(flags.item()) & L.SA_FLAG_PRG_REJECT:
             raise L.SALibraryError("a PCG64 raw draw was 0 (p=2^-64): re-position the streams")
         self.masker.consume(n)
         t1 = time.perf_counter()
         W.send_frame(self.sock, META, json.dumps({"weight": weight}).encode(), sender=self.index, rnd=rnd)
-        W.send_frame(self.sock, W.MASKED, hm, dtype=W.U64, sender=self.index, rnd=rnd,
-                     digest=int(dig.cpu().numpy().view(np.uint64)[0]))
+        self.sock.sendall(W.pack_header(W.MASKED, W.U64, self.index, rnd, n,
+                                        int(dig.cpu().numpy().view(np.uint64)[0])))
+        ev = [None, None]
+        pending = None
+        with torch.cuda.stream(cs):
+            for j, lo in enumerate(range(0, n, ce)):
+                b, k = j & 1, min(ce, n - lo)
+                hm[b][:k].copy_(dm[lo:lo + k], non_blocking=True)
+                ev[b] = torch.cuda.Event()
+                ev[b].record(cs)
+                if pending is not None:  # send the previous chunk while this one copies
+                    pb, pk = pending
+                    ev[pb].synchronize()
+                    self.sock.sendall(memoryview(hm[pb].numpy()[:pk]).cast("B"))
+                pending = (b, k)
+            if pending is not None:
+                pb, pk = pending
+                ev[pb].synchronize()
+                self.sock.sendall(memoryview(hm[pb].numpy()[:pk]).cast("B"))
         t2 = time.perf_counter()
-        return {"h2d_mask_d2h_s": t1 - t0, "send_s": t2 - t1}
+        return {"h2d_mask_s": t1 - t0, "d2h_send_s": t2 - t1}
 
     def result(self) -> np.ndarray:
         h, mv = W.recv_frame(self.sock, expect_kind=W.RESULT)
@@ -234,41 +287,55 @@ def synthetic_gradient(c: int, n: int, rnd: int = 0) -> np.ndarray:
     return (g.standard_normal(n, dtype=np.float32) * np.float32(1e-2)).astype(np.float32)
 
 
-def client_process(party: str, index: int, port: int, n: int, rounds: int, seeds, weight, gpu: int, fxp_bits: int,
-                   out_q) -> None:
-    """Entry point of one spawned client party."""
-    try:
-        xs = [synthetic_gradient(index, n, r) for r in range(rounds)]  # generated outside the rounds
-        cl = LoopbackClient(party, index, port, gpu=gpu, fxp_bits=fxp_bits, seeds=seeds)
-        cl.handshake()
-        stats = []
-        for r in range(rounds):
-            st = cl.submit(xs[r], r, weight)
-            res = cl.result()
-            st["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))
-            stats.append(st)
-        h, _ = W.recv_frame(cl.sock, expect_kind=W.BYE)
-        cl.close()
-        out_q.put((index, "ok", stats))
-    except Exception as e:  # reported to the parent, which fails loudly
-        out_q.put((index, "error", repr(e)))
+def client_process(parties: list, port: int, n: int, rounds: int, gpu: int, fxp_bits: int, out_q) -> None:
+    """Entry point of one spawned process hosting one or more client parties
+    (``parties``: (name, index, pair seeds or None, weight) tuples), each on
+    its own socket and thread."""
+    import threading
+
+    def run(party, index, seeds, weight):
+        try:
+            xs = [synthetic_gradient(index, n, r) for r in range(rounds)]  # generated outside the rounds
+            cl = LoopbackClient(party, index, port, gpu=gpu, fxp_bits=fxp_bits, seeds=seeds)
+            cl.handshake()
+            stats = []
+            for r in range(rounds):
+                st = cl.submit(xs[r], r, weight)
+                res = cl.result()
+                st["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))
+                stats.append(st)
+            W.recv_header(cl.sock, expect_kind=W.BYE)
+            cl.close()
+            out_q.put((index, "ok", stats))
+        except Exception as e:  # reported to the parent, which fails loudly
+            out_q.put((index, "error", repr(e)))
+
+    ts = [threading.Thread(target=run, args=p) for p in parties]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
 
 
 def run_loopback(names: list[str], n: int, rounds: int = 1, *, seeds: dict | None = None, weights=None,
                  average: bool = False, gpu: int = 0, fxp_bits: int = 18, keep_masked: bool = False,
-                 verify_digest: bool = False, timeout: float = 600.0):
-    """Spawn one process per client, run ``rounds`` rounds with this process
-    as the server.  Returns (results per round, server timings, client stats)."""
+                 verify_digest: bool = False, timeout: float = 600.0, parties_per_process: int = 1):
+    """Spawn the client parties (``parties_per_process`` per OS process), run
+    ``rounds`` rounds with this process as the server.  Returns (results per
+    round, server timings, client stats, received masked vectors)."""
     import multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     srv = LoopbackServer(len(names), gpu=gpu, fxp_bits=fxp_bits)
     q = ctx.Queue()
     procs = []
+    specs = []
     for i, p in enumerate(names):
         ps = None if seeds is None else {v: seeds[p][v] for v in names if v != p}
-        w = None if weights is None else weights[i]
-        pr = ctx.Process(target=client_process, args=(p, i, srv.port, n, rounds, ps, w, gpu, fxp_bits, q))
+        specs.append((p, i, ps, None if weights is None else weights[i]))
+    k = max(1, int(parties_per_process))
+    for g in range(0, len(specs), k):
+        pr = ctx.Process(target=client_process, args=(specs[g:g + k], srv.port, n, rounds, gpu, fxp_bits, q))
         pr.start()
         procs.append(pr)
     results, timings, masked = [], [], []
@@ -283,7 +350,7 @@ def run_loopback(names: list[str], n: int, rounds: int = 1, *, seeds: dict | Non
     finally:
         srv.close()
     stats = {}
-    for _ in procs:
+    for _ in names:
         idx, status, payload = q.get(timeout=timeout)
         if status != "ok":
             raise RuntimeError(f"client {idx} failed: {payload}")

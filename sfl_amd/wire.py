@@ -124,15 +124,37 @@ def send_frame(sock: socket.socket, kind: int, payload=None, *, dtype: int | Non
         sock.sendall(mv)
 
 
-def recv_frame(sock: socket.socket, into=None, *, expect_kind: int | None = None):
-    """Receive one frame -> (Header, memoryview of the payload).  With
-    ``into`` (a writable buffer: numpy array / pinned CPU tensor), the payload
-    lands there directly and must fit."""
+def recv_header(sock: socket.socket, *, expect_kind: int | None = None) -> Header:
     hb = bytearray(HEADER.size)
     _recv_exact(sock, memoryview(hb))
     h = unpack_header(bytes(hb))
     if expect_kind is not None and h.kind != expect_kind:
         raise WireError(f"expected frame kind {expect_kind}, got {h.kind}")
+    return h
+
+
+def recv_payload_chunked(sock: socket.socket, h: Header, buffers, on_chunk) -> None:
+    """Stream a frame's payload through a ring of host buffers (numpy arrays
+    or pinned CPU tensors): chunk j lands in buffers[j % len(buffers)], then
+    ``on_chunk(buf_index, byte_offset, nbytes)`` runs; the callback owns
+    waiting until a buffer is free again before returning."""
+    views = [memoryview(b.numpy() if hasattr(b, "numpy") and not isinstance(b, np.ndarray) else b).cast("B")
+             for b in buffers]
+    cap = min(len(v) for v in views)
+    off, j = 0, 0
+    while off < h.nbytes:
+        k = min(cap, h.nbytes - off)
+        _recv_exact(sock, views[j % len(views)][:k])
+        on_chunk(j % len(views), off, k)
+        off += k
+        j += 1
+
+
+def recv_frame(sock: socket.socket, into=None, *, expect_kind: int | None = None):
+    """Receive one frame -> (Header, memoryview of the payload).  With
+    ``into`` (a writable buffer: numpy array / pinned CPU tensor), the payload
+    lands there directly and must fit."""
+    h = recv_header(sock, expect_kind=expect_kind)
     if into is not None:
         a = into.numpy() if hasattr(into, "numpy") and not isinstance(into, np.ndarray) else into
         mv = memoryview(a).cast("B")

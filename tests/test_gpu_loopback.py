@@ -48,3 +48,24 @@ def test_loopback_dh_seeds_sum():
     assert np.array_equal(res[0], o.decode(o.server_sum(q)))
     for c in range(len(names)):
         assert not np.array_equal(masked[0][c], q[c])  # masked on the wire
+
+
+def test_loopback_chunked_streaming_multi_party_processes(monkeypatch):
+    """Transfers larger than the staging chunk stream through the pinned
+    rings on both sides; 4 parties hosted 2 per process (config 5 layout)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("SFL_LOOPBACK_CHUNK_ELEMS", "4096")
+    from sfl_amd.loopback import run_loopback, synthetic_gradient
+
+    names = [f"q{i}" for i in range(4)]
+    n = 50_001
+    seeds = o.seeds_for(names)
+    res, _, _, masked = run_loopback(names, n, 2, seeds=seeds, keep_masked=True, verify_digest=True,
+                                     parties_per_process=2, timeout=300)
+    for r in range(2):
+        xs = [synthetic_gradient(c, n, r) for c in range(len(names))]
+        masked_o = o.secure_masked(xs, names, seeds=seeds, offset=r * n)
+        assert np.array_equal(res[r], o.decode(o.server_sum(masked_o)))
+        for c in range(len(names)):
+            assert np.array_equal(masked[r][c], masked_o[c])

@@ -101,3 +101,23 @@ def test_loopback_handshake_agrees_pair_seeds():
     srv.close()
     for c in clients:
         c.close()
+
+
+def test_chunked_receive_through_buffer_ring():
+    a, b = _pair()
+    v = np.random.default_rng(1).integers(0, 2**64 - 1, 10_007, dtype=np.uint64)
+    t = threading.Thread(target=W.send_frame, args=(a, W.MASKED, v))
+    t.start()
+    h = W.recv_header(b, expect_kind=W.MASKED)
+    ring = [np.empty(1000, dtype=np.uint64) for _ in range(2)]
+    got = np.empty_like(v)
+    seen = []
+
+    def on_chunk(j, off, nbytes):
+        got[off // 8: (off + nbytes) // 8] = ring[j][: nbytes // 8]
+        seen.append((j, off, nbytes))
+
+    W.recv_payload_chunked(b, h, ring, on_chunk)
+    t.join()
+    assert np.array_equal(got, v)
+    assert [s[0] for s in seen] == [i % 2 for i in range(len(seen))] and len(seen) == 11

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--elems", type=int, default=100_000_000)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--parties-per-process", type=int, default=1,
+                    help="client parties hosted per OS process (config 5: 32 clients as 8 x 4)")
     args = ap.parse_args()
     import numpy as np
 
@@ -30,7 +32,8 @@ def main():
     names = [f"client{c}" for c in range(args.clients)]
     seeds = {a: {b: (0x5ECA66 << 32) | (min(i, j) << 16) | max(i, j) for j, b in enumerate(names) if b != a}
              for i, a in enumerate(names)}
-    res, timings, stats, _ = run_loopback(names, args.elems, args.rounds, seeds=seeds, timeout=900)
+    res, timings, stats, _ = run_loopback(names, args.elems, args.rounds, seeds=seeds, timeout=900,
+                                          parties_per_process=args.parties_per_process)
     steady = timings[1:] if len(timings) > 1 else timings
     rs = float(np.median([t["round_s"] for t in steady]))
     cl = [s for per in stats.values() for s in per[1:] or per]
@@ -39,8 +42,9 @@ def main():
         "clients": args.clients, "elems_per_client": args.elems, "rounds": args.rounds,
         "round_s_median": rs, "grad_elems_per_s": args.clients * args.elems / rs,
         "server": {k: float(np.median([t[k] for t in steady])) for k in steady[0]},
-        "client_h2d_mask_d2h_s_median": float(np.median([s["h2d_mask_d2h_s"] for s in cl])),
-        "client_send_s_median": float(np.median([s["send_s"] for s in cl])),
+        "client_h2d_mask_s_median": float(np.median([s["h2d_mask_s"] for s in cl])),
+        "client_d2h_send_s_median": float(np.median([s["d2h_send_s"] for s in cl])),
+        "parties_per_process": args.parties_per_process,
         "wire_bytes_per_round": args.clients * args.elems * 8,
     }
     print(json.dumps(out))
