@@ -185,8 +185,11 @@ def main():
     draws = (len(plan.pairs) + len(plan.cross)) * N
     bytes_alg = 4 * Lc * N + 8 * N  # fp32 reads of the local clients + one u64 sum write
     achieved = bytes_alg / (kern_ms / 1e3) / 1e9
+    # the launch's kernel: 5..8 co-located clients run the stream-split kernel
+    kname = (f"k_clients_split<{Lc}>" if 5 <= Lc <= 8 and plan.n_cross == 0
+             else f"k_clients<float, float, {Lc}, {plan.n_cross}>")
     # PMC bytes were collected on the default single-GPU workload only
-    pmc = pmc_traffic("void sa::k_clients<float, float, 8, 0>") if (world, C, N) == (1, 8, 100_000_000) else None
+    pmc = pmc_traffic(f"void sa::{kname}") if (world, C, N) == (1, 8, 100_000_000) else None
     out = {
         "metric": "grad elems/s device-resident: 100M-float quantize+mask+sum, 8 clients",
         "value": value,
@@ -207,7 +210,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": pmc["bytes"] if pmc else None, "traffic_detail": pmc,
-                     "kernel": "k_clients (sa_fused_clients)", "kernel_ms": kern_ms,
+                     "kernel": f"{kname} (sa_fused_clients)", "kernel_ms": kern_ms,
                      "launches_per_step": len(pipe.bounds),
                      "algorithmic_bytes_per_launch": bytes_alg,
                      "valu": {"pcg64_draws_per_launch": draws, "draws_per_s": draws / (kern_ms / 1e3),
