@@ -185,9 +185,7 @@ def main():
     draws = (len(plan.pairs) + len(plan.cross)) * N
     bytes_alg = 4 * Lc * N + 8 * N  # fp32 reads of the local clients + one u64 sum write
     achieved = bytes_alg / (kern_ms / 1e3) / 1e9
-    # the launch's kernel: 5..8 co-located clients run the stream-split kernel
-    kname = (f"k_clients_split<{Lc}>" if 5 <= Lc <= 8 and plan.n_cross == 0
-             else f"k_clients<float, float, {Lc}, {plan.n_cross}>")
+    kname = f"k_clients<float, float, {Lc}, {plan.n_cross}>"  # the launch's kernel
     # PMC bytes were collected on the default single-GPU workload only
     pmc = pmc_traffic(f"void sa::{kname}") if (world, C, N) == (1, 8, 100_000_000) else None
     out = {

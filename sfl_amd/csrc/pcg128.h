@@ -61,11 +61,15 @@ SA_HD constexpr uint64_t rotr64(uint64_t x, unsigned r) {
 }
 SA_HD constexpr uint64_t xslrr(u128 s) { return rotr64(hi64(s) ^ lo64(s), (unsigned)(hi64(s) >> 58)); }
 
-// Tables consumed by the kernels (built at compile time, see sa_tables.cpp):
-//   kPow[b]  = jump by 2^b draws, b = 0..63
-//   kLane[t] = jump by kElemsPerLane * t draws, t = 0..kBlockThreads-1
-constexpr int kBlockThreads = 256;
-constexpr int kElemsPerLane = 4;
-constexpr int kTileElems = kBlockThreads * kElemsPerLane;  // 1024
+// inverse of an odd value mod 2^128 (Newton: x <- x(2 - a x) doubles the
+// correct low bits; a*a == 1 mod 8 for odd a, so 6 steps reach 192 > 128)
+SA_HD constexpr u128 inv128(u128 a) {
+  u128 x = a;
+  for (int i = 0; i < 6; i++) x *= (u128)2 - a * x;
+  return x;
+}
+
+constexpr int kBlockThreads = 256;  // masking-kernel workgroup
+constexpr int kDpBlock = 4;         // elements per Philox counter block (DP noise)
 
 }  // namespace sa

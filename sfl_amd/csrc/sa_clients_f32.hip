@@ -1,11 +1,9 @@
 // sa_clients_f32.hip — fp32 instantiations of the masking kernel: the
 // single-client path (1 client, 0..16 streams per pass) and the fused
 // co-located-client shapes used by the benches (C clients over W GPUs:
-// L = C/W local clients, X = C - L cross streams each); 5..8 co-located
-// clients use the stream-split kernel.
+// L = C/W local clients, X = C - L cross streams each).
 #include "sa_clients_impl.h"
 #include "sa_registry.h"
-#include "sa_split_impl.h"
 
 namespace sa {
 
@@ -18,10 +16,7 @@ LaunchFn find_clients_kernel(int xt, int ct, int L, int X) {
     F32(1, 7),  F32(1, 8),  F32(1, 9),  F32(1, 10), F32(1, 11), F32(1, 12), F32(1, 13),
     F32(1, 14), F32(1, 15), F32(1, 16),
     // fused: C clients on one GPU
-    F32(2, 0), F32(3, 0), F32(4, 0),
-    // 5..8 clients: pair streams split over two waves (sa_split_impl.h)
-    {SA_F32, SA_F32, 5, 0, &launch_split<5>}, {SA_F32, SA_F32, 6, 0, &launch_split<6>},
-    {SA_F32, SA_F32, 7, 0, &launch_split<7>}, {SA_F32, SA_F32, 8, 0, &launch_split<8>},
+    F32(2, 0), F32(3, 0), F32(4, 0), F32(5, 0), F32(6, 0), F32(7, 0), F32(8, 0),
     // fused: C = 8 over W = 2 / 4 GPUs, C = 4 over 2 GPUs
     F32(4, 4), F32(2, 6), F32(2, 2),
   };

@@ -1,21 +1,26 @@
 // sa_clients_impl.h — the masking kernel: quantize + pairwise PCG64 mask
 // expansion + mod-2^64 accumulation for L co-located clients, gfx950.
 //
-// What one lane does.  A 256-lane workgroup owns a 1024-element tile; lane t
-// owns elements [tile + 4t, tile + 4t + 4).  For every mask stream the lane
-// keeps the 128-bit PCG64 state positioned at its own element (jumped there
-// once in the prologue with the affine-power table), steps it 4 times per
-// tile (one draw per element, numpy order) and then jumps it to its next
-// tile with one affine map (A^J, inc*G_J) — so every draw costs exactly one
-// 128-bit multiply-add and no lane ever waits on another.
+// What one lane does.  A 256-lane workgroup owns a 512-element tile; lane t
+// owns elements [tile + 2t, tile + 2t + 2) (8-B fp32 loads, 16-B u64 stores:
+// 512 B / 1 KiB contiguous per wave instruction).  For every mask stream the
+// lane keeps one 128-bit PCG64 state and advances it with exactly one affine
+// step per element: the first element of a tile is reached by the merged
+// tile jump S -> A^J S + inc*G_J (J = grid stride - 1), the second by the
+// plain step S -> A S + inc.  The prologue parks each state at the "virtual"
+// position one jump before the lane's first element (the affine jump is
+// invertible: A^J is odd), so every tile, the first included, runs the same
+// straight-line code.
 //
-// Data movement per tile (per lane): one 16-B load per client (4 fp32), two
-// 16-B stores for the 4 u64 sums, optional 2x16-B stores per client for the
-// wire image.  Consecutive lanes touch consecutive 16-B segments, so each
-// wave-instruction moves 1 KiB contiguous (dwordx4 coalescing).  Loads are
-// issued at the top of the tile and consumed at the bottom, so their HBM
-// latency hides under the tile's PRG work (the kernel is VALU-bound: ~30
-// VALU instructions, 10 of them 32x32->64 multiplies, per draw).
+// Loop order inside a tile is stream-outer: for stream q the lane draws both
+// of its elements back to back, so q's constants (inc, inc*G_J, sign mask)
+// are needed for two draws only.  They are scalar-loaded from the kernarg
+// segment into SGPRs, stream q+1's load issued after q's first draw (latency
+// hidden under one draw; SMEM returns out of order, so the wait is lgkmcnt(0)
+// right before q+1 starts).  No VGPRs or LDS traffic go to constants; the
+// multiplier limbs (A, A^J) sit in 8 wave-uniform VGPRs.  Measured on the
+// draw alone (tools/microbench/draw_issue.hip): LDS-resident constants issue
+// 10-15 % slower than SGPR ones.
 //
 // Sign handling without branches.  A client adds m = raw + K (K = 2^63-1,
 // numpy's Lemire offset) for a peer that sorts after it and subtracts it
@@ -28,6 +33,7 @@
 // same as an unsigned one.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include <type_traits>
@@ -41,10 +47,13 @@ namespace sa {
 
 // Tuning-only ablations (results are WRONG when nonzero; never shipped):
 // 1 = no zero-draw check, 2 = no quantize conversion, 8 = no global
-// loads/stores, 16 = stream constants as immediates (no LDS reads).
+// loads/stores.
 #ifndef SA_ABLATE
 #define SA_ABLATE 0
 #endif
+
+constexpr int kE = 2;                       // elements per lane per tile
+constexpr int kTile = kBlockThreads * kE;   // elements per workgroup tile (512)
 
 struct PowTable {
   Jump e[64];
@@ -64,144 +73,50 @@ static __constant__ PowTable kPowTable = make_pow_table();
 // ----------------------------------------------------------------------------
 // element loads / quantize
 // ----------------------------------------------------------------------------
-template <typename T>
-struct Vec4 {
-  T v[4];
-};
-
-template <typename T>
-__device__ __forceinline__ Vec4<T> load4(const T* __restrict__ p, uint64_t i, uint64_t n) {
-  Vec4<T> r;
-  if (i + 4 <= n) {
-    if constexpr (sizeof(T) == 4) {
-      const uint4 u = *reinterpret_cast<const uint4*>(p + i);
-      r.v[0] = __builtin_bit_cast(T, u.x);
-      r.v[1] = __builtin_bit_cast(T, u.y);
-      r.v[2] = __builtin_bit_cast(T, u.z);
-      r.v[3] = __builtin_bit_cast(T, u.w);
-    } else {
-      const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(p + i);
-      const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(p + i + 2);
-      r.v[0] = __builtin_bit_cast(T, a.x);
-      r.v[1] = __builtin_bit_cast(T, a.y);
-      r.v[2] = __builtin_bit_cast(T, b.x);
-      r.v[3] = __builtin_bit_cast(T, b.y);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; k++) r.v[k] = (i + k < n) ? p[i + k] : T(0);
-  }
-  return r;
-}
-
-__device__ __forceinline__ void store4_u64(uint64_t* __restrict__ p, uint64_t i, uint64_t n,
-                                           const uint64_t (&v)[4]) {
-  if (i + 4 <= n) {
-    reinterpret_cast<ulonglong2*>(p + i)[0] = ulonglong2{v[0], v[1]};
-    reinterpret_cast<ulonglong2*>(p + i)[1] = ulonglong2{v[2], v[3]};
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (i + k < n) p[i + k] = v[k];
-  }
-}
-
 // Raw buffer descriptors (SGPR, built from kernel arguments only, so hipcc
 // can prove them wave-uniform) + a 32-bit per-lane byte offset: one shared
 // offset VGPR serves every client instead of a 64-bit address per client.
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint64_t bytes) {
+  // launches are chunked so that every vector's bytes fit (kChunkElems)
   const int nrec = bytes > 0xFFFFFFF0ull ? (int)0xFFFFFFF0u : (int)bytes;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, nrec, 0x00020000);
 }
 
+// Tails without branches: gfx950 bounds-checks raw buffer accesses per
+// dword against the descriptor's num_records (tools/microbench/oob_test.hip:
+// a straddling dwordx4 load returns the in-range dwords and zeros, a
+// straddling store writes only the in-range dwords).  Descriptors carry the
+// exact byte length of their vector (0 for an absent one), so every tile
+// issues the same unconditional loads and stores — no per-lane tail paths,
+// whose merged control flow made the compiler wait (vmcnt(0)) for the
+// tile's loads before the mask expansion.
 template <typename T>
-__device__ __forceinline__ Vec4<T> bload4(rsrc_t r, uint64_t i, uint64_t n) {
-  Vec4<T> out;
+struct Vec2 {
+  T v[2];
+};
+// elements i, i+1 of a T vector (past the end: 0); i even, so the pair is one
+// 8-B (fp32) or 16-B (8-B types) aligned load
+template <typename T>
+__device__ __forceinline__ Vec2<T> bload2(rsrc_t r, uint64_t i) {
+  Vec2<T> out;
   const int off = (int)(i * sizeof(T));
-  if (i + 4 <= n) {
-    if constexpr (sizeof(T) == 4) {
-      const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-#pragma unroll
-      for (int k = 0; k < 4; k++) out.v[k] = __builtin_bit_cast(T, (uint32_t)u[k]);
-    } else {
-      const auto u0 = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-      const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0);
-      out.v[0] = __builtin_bit_cast(T, (uint64_t)u0[0] | ((uint64_t)u0[1] << 32));
-      out.v[1] = __builtin_bit_cast(T, (uint64_t)u0[2] | ((uint64_t)u0[3] << 32));
-      out.v[2] = __builtin_bit_cast(T, (uint64_t)u1[0] | ((uint64_t)u1[1] << 32));
-      out.v[3] = __builtin_bit_cast(T, (uint64_t)u1[2] | ((uint64_t)u1[3] << 32));
-    }
+  if constexpr (sizeof(T) == 4) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    out.v[0] = __builtin_bit_cast(T, (uint32_t)u[0]);
+    out.v[1] = __builtin_bit_cast(T, (uint32_t)u[1]);
   } else {
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      if (i + k < n) {
-        if constexpr (sizeof(T) == 4) {
-          out.v[k] = __builtin_bit_cast(T, (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * k, 0, 0));
-        } else {
-          const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off + 8 * k, 0, 0);
-          out.v[k] = __builtin_bit_cast(T, (uint64_t)u[0] | ((uint64_t)u[1] << 32));
-        }
-      } else {
-        out.v[k] = T(0);
-      }
-    }
+    const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    out.v[0] = __builtin_bit_cast(T, (uint64_t)u[0] | ((uint64_t)u[1] << 32));
+    out.v[1] = __builtin_bit_cast(T, (uint64_t)u[2] | ((uint64_t)u[3] << 32));
   }
   return out;
 }
-
-__device__ __forceinline__ uint64_t bload_u64(rsrc_t r, uint64_t i) {
-  const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8), 0, 0);
-  return (uint64_t)u[0] | ((uint64_t)u[1] << 32);
-}
-struct Vec2u64 {
-  uint64_t a, b;
-};
-// elements i, i+1 (either may lie past n: reads as 0)
-__device__ __forceinline__ Vec2u64 bload2_u64(rsrc_t r, uint64_t i, uint64_t n) {
-  Vec2u64 o{0, 0};
-  if (i + 2 <= n) {
-    const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 8), 0, 0);
-    o.a = (uint64_t)u[0] | ((uint64_t)u[1] << 32);
-    o.b = (uint64_t)u[2] | ((uint64_t)u[3] << 32);
-  } else if (i < n) {
-    const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 8), 0, 0);
-    o.a = (uint64_t)u[0] | ((uint64_t)u[1] << 32);
-  }
-  return o;
-}
-__device__ __forceinline__ void bstore2_u64(rsrc_t r, uint64_t i, uint64_t n, uint64_t v0, uint64_t v1) {
+// u64 elements i, i+1 (the part past the end is dropped by the bounds check)
+__device__ __forceinline__ void bstore2_u64(rsrc_t r, uint64_t i, uint64_t v0, uint64_t v1) {
   typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-  if (i + 2 <= n) {
-    const v4u d = {(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32)};
-    __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)(i * 8), 0, 0);
-  } else if (i < n) {
-    const v2u d = {(uint32_t)v0, (uint32_t)(v0 >> 32)};
-    __builtin_amdgcn_raw_buffer_store_b64(d, r, (int)(i * 8), 0, 0);
-  }
-}
-// Wave-level transpose through the wave's 256 LDS slots: lane l holds
-// elements 4l..4l+3 of the wave's chunk in `in`, gets 2l, 2l+1, 128+2l,
-// 129+2l in `out`.  LDS ops of one wave complete in order; the wave barriers
-// keep the compiler from moving them across the exchange.
-__device__ __forceinline__ void wave_transpose(uint64_t* tw, int lane, const uint64_t (&in)[4],
-                                               uint64_t (&out)[4]) {
-#pragma unroll
-  for (int k = 0; k < 4; k++) tw[4 * lane + k] = in[k];
-  __builtin_amdgcn_wave_barrier();
-  out[0] = tw[2 * lane];
-  out[1] = tw[2 * lane + 1];
-  out[2] = tw[128 + 2 * lane];
-  out[3] = tw[129 + 2 * lane];
-  __builtin_amdgcn_wave_barrier();
-}
-__device__ __forceinline__ void bstore_u64(rsrc_t r, uint64_t i, uint64_t v) {
-  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-  v2u d;
-  d[0] = (uint32_t)v;
-  d[1] = (uint32_t)(v >> 32);
-  __builtin_amdgcn_raw_buffer_store_b64(d, r, (int)(i * 8), 0, 0);
+  const v4u d = {(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)(i * 8), 0, 0);
 }
 
 // float -> int64 truncation with x86 "integer indefinite" semantics
@@ -216,75 +131,57 @@ __device__ __forceinline__ uint64_t trunc_i64(double v) {
 }
 
 // q = trunc(x * w * 2^fxp) in the compute type CT (numpy promotion result).
+struct QScale {
+  float f;     // 2^fxp
+  double d;    // 2^fxp
+  int32_t fxp;
+};
 template <typename XT, typename CT>
-__device__ __forceinline__ uint64_t quantize(XT x, CT w, const KArgs& a) {
+__device__ __forceinline__ uint64_t quantize(XT x, CT w, const QScale& q) {
   if constexpr (std::is_integral<CT>::value) {  // int64 arithmetic, wraps mod 2^64
-    return (uint64_t)(long long)x * (uint64_t)w * ((uint64_t)1 << a.fxp_bits);
+    return (uint64_t)(long long)x * (uint64_t)w * ((uint64_t)1 << q.fxp);
   } else if constexpr (sizeof(CT) == 4) {
     // (x*w)*2^fxp == x*(w*2^fxp) exactly whenever w*2^fxp is finite: scaling
     // by a power of two commutes with rounding, and where the product is
     // subnormal it truncates to 0 either way.  Values of |p| < 2^31 (every
     // gradient in practice) convert with one v_cvt_i32_f32; a wave with any
     // larger / non-finite value takes the full int64 conversion.
-    const float ws = __fmul_rn((float)w, a.scale_f);  // wave-uniform
+    const float ws = __fmul_rn((float)w, q.f);  // wave-uniform
     if (__builtin_isfinite(ws)) {
       const float p = __fmul_rn((float)x, ws);
       if (!__any(!(__builtin_fabsf(p) < 0x1p31f))) return (uint64_t)(int64_t)(int32_t)p;
       return trunc_i64(p);
     }
     const float p = __fmul_rn((float)x, (float)w);
-    return trunc_i64(__fmul_rn(p, a.scale_f));
+    return trunc_i64(__fmul_rn(p, q.f));
   } else {
     const double p = __dmul_rn((double)x, (double)w);
-    return trunc_i64(__dmul_rn(p, a.scale_d));
+    return trunc_i64(__dmul_rn(p, q.d));
   }
 }
 
 template <typename CT>
-__device__ __forceinline__ CT scalar_weight(const ClientArg& c) {
+__device__ __forceinline__ CT scalar_weight(double w) {
   if constexpr (std::is_integral<CT>::value)
-    return (CT)(long long)c.w;
+    return (CT)(long long)w;
   else
-    return (CT)c.w;
+    return (CT)w;
 }
 
 // ----------------------------------------------------------------------------
-// PCG64 draw helpers
+// PCG64 draw
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ u128 ld128(uint64_t lo, uint64_t hi) { return mk128(hi, lo); }
-
-// XSL-RR of the state with the stream's sign mask folded into the XOR.
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t d;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-  return d;
-}
 __device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) {
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   const u32x2 v = {lo, hi};
   return __builtin_bit_cast(uint64_t, v);
 }
-// XSL-RR output of state s with the sign mask m (0 / ~0) folded into the
-// XOR (it commutes with the rotation).  32-bit form: two 3-input XORs
-// (v_bitop3, gfx950) and a funnel-shift rotation (two v_alignbit + a swap
-// when r >= 32), all full-rate, where the 64-bit shifts of the generic form
-// issue at half rate.  Also folds the raw==0 test (raw == 0 <=> hi == lo <=>
-// xl == xh == m, a 3-input "all equal" LUT) into a running per-lane minimum.
-__device__ __forceinline__ uint64_t draw_signed(u128 s, uint32_t m, uint32_t& zmin) {
-  const uint64_t hi = hi64(s), lo = lo64(s);
-  const uint32_t s3 = (uint32_t)(hi >> 32);
-  const uint32_t xl = xor3((uint32_t)lo, (uint32_t)hi, m);
-  const uint32_t xh = xor3((uint32_t)(lo >> 32), s3, m);
-  if (!(SA_ABLATE & 1)) {
-    uint32_t z;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x7e" : "=v"(z) : "v"(xl), "v"(xh), "v"(m));
-    zmin = zmin < z ? zmin : z;
-  }
-  const uint32_t r = s3 >> 26;                       // alignbit uses r & 31
-  const uint32_t a = __builtin_amdgcn_alignbit(xh, xl, r);
-  const uint32_t b = __builtin_amdgcn_alignbit(xl, xh, r);
-  const bool big = (int32_t)s3 < 0;                  // r >= 32: halves swap
-  return big ? pack64(b, a) : pack64(a, b);
+// a wave-uniform value as an opaque VGPR (kept resident, never re-materialised)
+__device__ __forceinline__ uint32_t vreg(uint32_t x) {
+  uint32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+  return r;
 }
 
 // One PCG64 step + signed XSL-RR draw + accumulation, hand-scheduled for
@@ -337,9 +234,12 @@ __device__ __forceinline__ uint64_t draw_signed(u128 s, uint32_t m, uint32_t& zm
 #define SA_PCG_DRAW_OUTS                                                                 \
   [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [zmin] "+v"(zmin),          \
       [ulo] "+v"(ulo), [uhi] "+v"(uhi), [k1] "=&s"(k1), [k2] "=&s"(k2), [k3] "=&s"(k3)
+// Operand classes: the multiplier limbs are wave-uniform VGPRs (set once per
+// launch), the stream constants SGPRs (scalar-loaded per stream and tile), so
+// every VOP3 reads at most one SGPR (the gfx9 constant-bus limit).
 #define SA_PCG_DRAW_INS                                                                  \
-  [a0] "s"(a0), [a1] "s"(a1), [a2] "s"(a2), [a3] "s"(a3), [c01] "v"(c01), [c23] "v"(c23),  \
-      [m] "v"(m)
+  [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c01] "s"(c01), [c23] "s"(c23),  \
+      [m] "s"(m)
 #define SA_PCG_DRAW_CLOBBERS \
   "vcc", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9"
 
@@ -370,12 +270,6 @@ __device__ __forceinline__ void pcg_draw_one(uint32_t& s0, uint32_t& s1, uint32_
                : SA_PCG_DRAW_CLOBBERS);
 }
 
-struct StreamLds {
-  uint64_t inc_lo, inc_hi, cj_lo, cj_hi, smask, pad;
-};
-
-typedef __attribute__((address_space(3))) const StreamLds* lds_ptr;  // 32-bit LDS address
-
 // Compile-time enumeration of the internal pairs (u < v) of L clients.
 template <int L>
 struct Pairs {
@@ -404,57 +298,80 @@ struct Pairs {
 // the kernel
 // ----------------------------------------------------------------------------
 
-// waves per SIMD the register allocation must allow: shapes with 17+ streams
-// (e.g. 4 local clients + 4 cross = 22) otherwise land a few VGPRs above the
-// 3-wave limit of 168
-constexpr int clients_waves(int streams) { return streams >= 17 ? 3 : (streams >= 13 && streams <= 15) ? 4 : 2; }
+// Waves per SIMD the register allocation must allow (spill-free targets from
+// the compiler's census, tools/kregs.py): 4 VGPRs per stream state, 3 per
+// (client, element) (accumulator halves + input), plus the draw scratch,
+// multipliers and addressing; the single-client kernel also carries the
+// continue / per-element-weight / DP-noise paths.  L = 8 (28 pair streams):
+// 2 waves; 1 client + 7 cross streams: 5.
+constexpr int clients_waves(int P, int L) {
+  const int regs = 4 * P + 3 * L * kE + (L == 1 ? 60 : 48);
+  const int w = 512 / regs;
+  return w > 8 ? 8 : (w < 1 ? 1 : w);
+}
+
+typedef __attribute__((address_space(4))) const uint64_t* kptr_t;
+static_assert(offsetof(StreamArg, inc_lo) == 16 && offsetof(StreamArg, cj_lo) == 32 &&
+                  offsetof(StreamArg, smask) == 48,
+              "StreamArg layout (scalar loads below)");
+
+typedef __attribute__((address_space(4))) const KArgs kargs_t;
+
+// The kernarg image through an opaque SGPR pointer: loads through it are
+// scalar loads that cannot be hoisted above the fence, so per-client values
+// (buffer bases, bias, weight) are re-read where they are used instead of
+// pinning ~100 SGPRs (descriptors, biases, weights of 8 clients) across the
+// whole tile loop.
+__device__ __forceinline__ kargs_t* fenced_args() {
+  kargs_t* p = (kargs_t*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
 
 template <typename XT, typename CT, int L, int X>
-__global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count + L * X)) k_clients(const KArgs a) {
+__global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count + L * X, L))
+    k_clients(const KArgs a) {
   constexpr int PI = Pairs<L>::count;
   constexpr int P = PI + L * X;
-  constexpr bool kGeneral = (L == 1);  // continue mode + per-element weights
+  constexpr bool kGeneral = (L == 1);  // continue mode + per-element weights + DP
   static_assert(L >= 1 && L <= kMaxLocal, "L");
   static_assert(P <= kMaxStreams, "P");
 
   const uint64_t n = a.n;
-  // lane t of block b owns elements [b*1024 + 4t, +4) of each tile; tiles
-  // stride by the grid (16-B loads: 1 KiB contiguous per wave-instruction).
-  const uint64_t first = (uint64_t)blockIdx.x * kTileElems + (uint64_t)threadIdx.x * kElemsPerLane;
-  const uint64_t stride = (uint64_t)gridDim.x * kTileElems;
+  const uint64_t first = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kE;
+  const uint64_t stride = (uint64_t)gridDim.x * kTile;
 
-  // ---- per-stream constants go to LDS once (broadcast ds_read per use)
-  __shared__ StreamLds sl[P > 0 ? P : 1];
-  if constexpr (P > 0) {
-    for (int j = threadIdx.x; j < P; j += blockDim.x) {
-      const StreamArg& s = a.s[j];
-      sl[j] = StreamLds{s.inc_lo, s.inc_hi, s.cj_lo, s.cj_hi, s.smask, 0};
-    }
-    __syncthreads();
-  }
-
-  // ---- prologue: jump every stream from draw 0 to this lane's first element
+  // ---- prologue: park every stream one tile jump before S_{first+1}, the
+  // state element `first` is drawn from: V = A^-J (S_{first+1} - inc*G_J)
   uint32_t st[P > 0 ? P : 1][4];  // 128-bit states as 32-bit limbs
   if constexpr (P > 0) {
     Jump jl{1, 0};
-    uint64_t pos = first;
+    uint64_t pos = first + 1;
     for (int b = 0; pos != 0; b++, pos >>= 1) {
       if (pos & 1) jl = compose(jl, kPowTable.e[b]);
     }
+    const u128 aji = ld128(a.aji_lo, a.aji_hi);
 #pragma unroll
     for (int j = 0; j < P; j++) {
       const StreamArg& s = a.s[j];
-      const u128 v = apply(jl, ld128(s.s_lo, s.s_hi), ld128(s.inc_lo, s.inc_hi));
+      const u128 sf = apply(jl, ld128(s.s_lo, s.s_hi), ld128(s.inc_lo, s.inc_hi));
+      const u128 v = aji * (sf - ld128(s.cj_lo, s.cj_hi));
       st[j][0] = (uint32_t)lo64(v);
       st[j][1] = (uint32_t)(lo64(v) >> 32);
       st[j][2] = (uint32_t)hi64(v);
       st[j][3] = (uint32_t)(hi64(v) >> 32);
     }
   }
-  // The tile-to-tile jump is merged into the first draw of the next tile:
-  // S_{i+4} -> S_{i+stride+1} is ONE affine step (A^(stride-3), inc*G_(stride-3)),
-  // so moving to the next tile costs no multiply beyond the draw itself.
-  const u128 AJ1 = ld128(a.aj_lo, a.aj_hi);
+  // multiplier limbs: jump (first element of a tile) and plain step
+  uint32_t mj[4], mp[4];
+  if constexpr (P > 0) {
+    const u128 AJ = ld128(a.aj_lo, a.aj_hi);
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      mj[w] = vreg((uint32_t)(AJ >> (32 * w)));
+      mp[w] = vreg((uint32_t)(kPcgMult >> (32 * w)));
+    }
+  }
 
   uint32_t zmin = 0xFFFFFFFFu;  // 0 iff some raw PCG64 draw of this lane was 0
 
@@ -463,157 +380,131 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
 #pragma unroll
   for (int c = 0; c < L; c++) dig_lds[c][threadIdx.x] = 0;
 
-  rsrc_t rx[L], rw[kGeneral ? L : 1], rm[L];
-#pragma unroll
-  for (int c = 0; c < L; c++) {
-    rx[c] = make_rsrc(a.c[c].x, n * sizeof(XT));
-    rm[c] = make_rsrc(a.c[c].masked_out, n * 8);
-    if constexpr (kGeneral) rw[c] = make_rsrc(a.c[c].wvec, n * sizeof(CT));
-  }
-  const rsrc_t rs = make_rsrc(a.sum_out, n * 8);
-
-  // wave-private LDS slots for the output transpose (see below)
-  __shared__ uint64_t tr_lds[kBlockThreads * kElemsPerLane];
-  const int lane = threadIdx.x & 63;
-  uint64_t* const tw = tr_lds + (threadIdx.x & ~63) * kElemsPerLane;
-
   float dp_s = 1.0f;
   if constexpr (kGeneral && std::is_same<XT, float>::value && std::is_same<CT, float>::value) {
     if (a.dp_on) dp_s = dp_scale(a.dp_sumsq, a.dp_sumsq_layer, a.dp_clip);
   }
 
-  lds_ptr slp = (lds_ptr)(sl);
-  int tile = 0;
   // wave-uniform trip count: every lane of a wave runs the wave's last tile
-  // (out-of-range elements are masked at load/store) so the transpose has
-  // all 64 lanes.
-  const uint64_t wave_off = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * 64 * kElemsPerLane);
-  for (uint64_t base = (uint64_t)blockIdx.x * kTileElems; base + wave_off < n; base += stride, tile++) {
-    const uint64_t i = base + (uint64_t)threadIdx.x * kElemsPerLane;
-    const bool jstep = tile > 0;             // uniform: this tile's k=0 draws jump
-    const u128 M0 = jstep ? AJ1 : kPcgMult;
-    const int add0 = jstep ? 2 : 0;          // u64 offset of C_J1 vs inc in StreamLds
+  // (out-of-range elements are masked at load/store)
+  const uint64_t wave_off = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * 64 * kE);
+  for (uint64_t base = (uint64_t)blockIdx.x * kTile; base + wave_off < n; base += stride) {
+    const uint64_t i = base + (uint64_t)threadIdx.x * kE;
 
-    // ---- issue this tile's loads early; consumed as each element finishes
-    Vec4<XT> xv[L];
-    Vec4<CT> wv[kGeneral ? L : 1];
-    Vec4<uint64_t> pv[kGeneral ? L : 1];
-#pragma unroll
-    for (int c = 0; c < L; c++) {
-      if (kGeneral && a.continue_mode) {
-        pv[c] = bload4<uint64_t>(rm[c], i, n);
-      } else {
-        if (SA_ABLATE & 8) {
-#pragma unroll
-          for (int k = 0; k < 4; k++) xv[c].v[k] = (XT)(int)(i + k + c);
-        } else {
-          xv[c] = bload4<XT>(rx[c], i, n);
-        }
-        if (kGeneral && a.c[c].wvec) wv[c] = bload4<CT>(rw[kGeneral ? c : 0], i, n);
-      }
-    }
-    if constexpr (kGeneral && std::is_same<XT, float>::value && std::is_same<CT, float>::value) {
-      if (a.dp_on && !a.continue_mode) {  // fused DP pre-step (sa_mask_dp)
-        const Normal4 z = gauss4(a.dp_key, a.dp_block0 + (i >> 2));
-#pragma unroll
-        for (int k = 0; k < 4; k++) xv[0].v[k] = dp_apply(xv[0].v[k], dp_s, z.z[k], a.dp_sigma, a.dp_updates);
-      }
-    }
-
-    // ---- element-outer: one draw per stream per element.  Each stream's
-    // step is fenced (empty volatile asm on its state, the LDS pointer and
-    // the accumulators it touches), so only one stream's constants and
-    // temporaries are live at a time: P*4 state VGPRs + L accumulators.
-    uint64_t sum[4];
-    uint64_t fin[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      uint32_t al[L], ah[L];  // per-client accumulators as 32-bit halves
+    // ---- issue this tile's loads first; consumed after the mask expansion.
+    // Unconditional: an absent vector has a 0-byte descriptor (reads 0).
+    Vec2<XT> xv[L];
+    Vec2<CT> wv[kGeneral ? L : 1];
+    Vec2<uint64_t> pv[kGeneral ? L : 1];
+    uint32_t al[kE][L], ah[kE][L];  // per-client accumulators (32-bit halves)
+    {
+      kargs_t* ka = fenced_args();
+      const bool cont = kGeneral && ka->continue_mode;
 #pragma unroll
       for (int c = 0; c < L; c++) {
-        al[c] = (uint32_t)a.c[c].bias;
-        ah[c] = (uint32_t)(a.c[c].bias >> 32);
-      }
-      if constexpr (P > 0) {
-        const u128 Mk = k == 0 ? M0 : kPcgMult;
-        const uint32_t m0 = (uint32_t)lo64(Mk), m1 = (uint32_t)(lo64(Mk) >> 32);
-        const uint32_t m2 = (uint32_t)hi64(Mk), m3 = (uint32_t)(hi64(Mk) >> 32);
+        if (SA_ABLATE & 8) {
 #pragma unroll
-        for (int q = 0; q < P; q++) {
-          asm volatile("" : "+v"(slp));  // constants re-read from LDS per draw, never hoisted
-          typedef __attribute__((address_space(3))) const uint64_t* lds_u64;
-          const lds_u64 cp = (lds_u64)(slp + q) + (k == 0 ? add0 : 0);
-          const uint64_t c01 = (SA_ABLATE & 16) ? 2 * q + 1 : cp[0];
-          const uint64_t c23 = (SA_ABLATE & 16) ? q : cp[1];
-          const uint32_t sm = (SA_ABLATE & 16) ? 0u : (uint32_t)slp[q].smask;
-          const int cu = q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1);
+          for (int k = 0; k < kE; k++) xv[c].v[k] = (XT)(int)(i + k + c);
+        } else {
+          xv[c] = bload2<XT>(make_rsrc(ka->c[c].x, cont ? 0 : n * sizeof(XT)), i);
+        }
+        if constexpr (kGeneral) {
+          const void* wp = ka->c[c].wvec;
+          wv[c] = bload2<CT>(make_rsrc(wp, (wp && !cont) ? n * sizeof(CT) : 0), i);
+          pv[c] = bload2<uint64_t>(make_rsrc(ka->c[c].masked_out, cont ? n * 8 : 0), i);
+        }
+        // accumulators start at the client's folded bias constant
+        const uint64_t bias = ka->c[c].bias;
+#pragma unroll
+        for (int k = 0; k < kE; k++) {
+          al[k][c] = (uint32_t)bias;
+          ah[k][c] = (uint32_t)(bias >> 32);
+        }
+      }
+    }
+
+    // ---- mask expansion, stream-outer; stream q+1's constants are
+    // scalar-loaded during q's first draw
+    if constexpr (P > 0) {
+      const kptr_t ks = (const kptr_t)(&fenced_args()->s[0]);
+      uint64_t ni0 = ks[2], ni1 = ks[3], nj0 = ks[4], nj1 = ks[5];
+      uint32_t nm = (uint32_t)ks[6];
+#pragma unroll
+      for (int q = 0; q < P; q++) {
+        const uint64_t ci0 = ni0, ci1 = ni1, cj0 = nj0, cj1 = nj1;
+        const uint32_t m = nm;
+        const int cu = q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1);
+#pragma unroll
+        for (int k = 0; k < kE; k++) {
+          const uint32_t* mk = k == 0 ? mj : mp;
+          const uint64_t c01 = k == 0 ? cj0 : ci0, c23 = k == 0 ? cj1 : ci1;
           if (q < PI) {
             const int cv = Pairs<L>::v(q);
-            pcg_draw_pair(st[q][0], st[q][1], st[q][2], st[q][3], m0, m1, m2, m3, c01, c23, sm, zmin, al[cu],
-                          ah[cu], al[cv], ah[cv]);
+            pcg_draw_pair(st[q][0], st[q][1], st[q][2], st[q][3], mk[0], mk[1], mk[2], mk[3], c01, c23, m, zmin,
+                          al[k][cu], ah[k][cu], al[k][cv], ah[k][cv]);
           } else {
-            pcg_draw_one(st[q][0], st[q][1], st[q][2], st[q][3], m0, m1, m2, m3, c01, c23, sm, zmin, al[cu],
-                         ah[cu]);
+            pcg_draw_one(st[q][0], st[q][1], st[q][2], st[q][3], mk[0], mk[1], mk[2], mk[3], c01, c23, m, zmin,
+                         al[k][cu], ah[k][cu]);
+          }
+          if (k == 0 && q + 1 < P) {
+            kptr_t g = (const kptr_t)(&fenced_args()->s[q + 1]);
+            ni0 = g[2];
+            ni1 = g[3];
+            nj0 = g[4];
+            nj1 = g[5];
+            nm = (uint32_t)g[6];
           }
         }
       }
-      uint64_t acc[L];
-#pragma unroll
-      for (int c = 0; c < L; c++) acc[c] = pack64(al[c], ah[c]);
-      // ---- finish element k: add the quantized value (or the prior pass)
-      uint64_t s_k = 0;
-#pragma unroll
-      for (int c = 0; c < L; c++) {
-        if (kGeneral && a.continue_mode) {
-          acc[c] += pv[kGeneral ? c : 0].v[k];
-        } else {
-          const CT w = (kGeneral && a.c[c].wvec) ? wv[kGeneral ? c : 0].v[k] : scalar_weight<CT>(a.c[c]);
-          const XT xk = xv[c].v[k];
-          if (SA_ABLATE & 2)
-            acc[c] += __builtin_bit_cast(uint32_t, (float)xk);
-          else
-            acc[c] += quantize<XT, CT>(xk, w, a);
-        }
-        s_k += acc[c];
-        if (i + k < n)
-          __hip_atomic_fetch_xor(&dig_lds[c][threadIdx.x], acc[c], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        if constexpr (kGeneral) {
-          fin[k] = acc[c];
-        } else {
-          if (a.c[c].masked_out && i + k < n) bstore_u64(rm[c], i + k, acc[c]);
-        }
-      }
-      sum[k] = s_k;
     }
 
-    // ---- outputs.  A lane finishes 4 consecutive u64 (32 B); stored as is,
-    // each 16-B store instruction would leave every 128-B line half written.
-    // The wave's 256 results are transposed through LDS instead, so lane l
-    // stores elements (2l, 2l+1) and (128+2l, 129+2l): each store instruction
-    // writes 1 KiB contiguous.
-    const uint64_t e0 = i - 4 * (uint64_t)lane + 2 * (uint64_t)lane;  // wave base + 2l
-    const uint64_t e1 = e0 + 128;
-    if constexpr (kGeneral) {
-      if (a.c[0].masked_out) {
-        uint64_t v[4];
-        wave_transpose(tw, lane, fin, v);
-        bstore2_u64(rm[0], e0, n, v[0], v[1]);
-        bstore2_u64(rm[0], e1, n, v[2], v[3]);
+    // ---- finish: add the quantized value (or the prior pass), digest, sums
+    kargs_t* ka = fenced_args();
+    const bool cont = kGeneral && ka->continue_mode;
+    if constexpr (kGeneral && std::is_same<XT, float>::value && std::is_same<CT, float>::value) {
+      if (ka->dp_on && !cont) {  // fused DP pre-step (sa_mask_dp)
+        const Normal4 z = gauss4(ka->dp_key, ka->dp_block0 + (i >> 2));
+        const int h = (int)(i & 2);
+#pragma unroll
+        for (int k = 0; k < kE; k++)
+          xv[0].v[k] = dp_apply(xv[0].v[k], dp_s, h ? z.z[2 + k] : z.z[k], ka->dp_sigma, ka->dp_updates);
       }
     }
-    if (a.sum_mode != 0 && (!(SA_ABLATE & 8) || sum[0] == 0x123456789ull)) {
-      uint64_t v[4];
-      wave_transpose(tw, lane, sum, v);
-      if (a.sum_mode == 2) {
-        const Vec2u64 o0 = bload2_u64(rs, e0, n), o1 = bload2_u64(rs, e1, n);
-        v[0] += o0.a;
-        v[1] += o0.b;
-        v[2] += o1.a;
-        v[3] += o1.b;
+    const QScale qs{ka->scale_f, ka->scale_d, ka->fxp_bits};
+    uint64_t sum[kE] = {0, 0};
+#pragma unroll
+    for (int c = 0; c < L; c++) {
+      uint64_t acc[kE];
+#pragma unroll
+      for (int k = 0; k < kE; k++) {
+        uint64_t v = pack64(al[k][c], ah[k][c]);
+        if (cont) {
+          v += pv[kGeneral ? c : 0].v[k];
+        } else {
+          const CT w = (kGeneral && ka->c[c].wvec) ? wv[kGeneral ? c : 0].v[k] : scalar_weight<CT>(ka->c[c].w);
+          const XT xk = xv[c].v[k];
+          if (SA_ABLATE & 2)
+            v += __builtin_bit_cast(uint32_t, (float)xk);
+          else
+            v += quantize<XT, CT>(xk, w, qs);
+        }
+        acc[k] = v;
+        sum[k] += v;
       }
-      bstore2_u64(rs, e0, n, v[0], v[1]);
-      bstore2_u64(rs, e1, n, v[2], v[3]);
+      const uint64_t d = (i < n ? acc[0] : 0) ^ (i + 1 < n ? acc[1] : 0);
+      __hip_atomic_fetch_xor(&dig_lds[c][threadIdx.x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      uint64_t* mo = ka->c[c].masked_out;
+      if (mo) bstore2_u64(make_rsrc(mo, n * 8), i, acc[0], acc[1]);
+    }
+    const int sum_mode = ka->sum_mode;
+    if (sum_mode != 0 && (!(SA_ABLATE & 8) || sum[0] == 0x123456789ull)) {
+      const rsrc_t rs = make_rsrc(ka->sum_out, n * 8);
+      if (sum_mode == 2) {
+        const Vec2<uint64_t> o = bload2<uint64_t>(rs, i);
+        sum[0] += o.v[0];
+        sum[1] += o.v[1];
+      }
+      bstore2_u64(rs, i, sum[0], sum[1]);
     }
   }
 
@@ -639,7 +530,8 @@ int occupancy_blocks(const void* kernel);  // sa_api.hip
 // Buffer offsets are 32-bit byte offsets, so one launch covers at most
 // kChunkElems elements (4 GiB of u64); longer vectors are cut into chunks
 // whose streams start kChunkElems draws further on.
-constexpr uint64_t kChunkElems = (1ull << 29) - kTileElems;
+constexpr uint64_t kChunkElems = (1ull << 29) - kTile;
+static_assert(kChunkElems % kTile == 0, "chunk");
 
 template <typename XT, typename CT, int L, int X>
 int launch_clients(const KArgs& in, void* stream) {
@@ -657,7 +549,7 @@ int launch_clients(const KArgs& in, void* stream) {
         if (a.c[c].masked_out) a.c[c].masked_out += off;
       }
       if (a.sum_out) a.sum_out += off;
-      a.dp_block0 += off / kElemsPerLane;
+      a.dp_block0 += off / kDpBlock;
       const Jump jo = jump_of(off);
       for (int j = 0; j < P; j++) {
         const u128 s = apply(jo, mk128(a.s[j].s_hi, a.s[j].s_lo), mk128(a.s[j].inc_hi, a.s[j].inc_lo));
@@ -665,12 +557,15 @@ int launch_clients(const KArgs& in, void* stream) {
         a.s[j].s_hi = hi64(s);
       }
     }
-    const uint64_t tiles = (a.n + kTileElems - 1) / kTileElems;
+    const uint64_t tiles = (a.n + kTile - 1) / kTile;
     const int grid = (int)(tiles < (uint64_t)maxb ? tiles : (uint64_t)maxb);
-    // merged jump-step: S_{i+4} -> S_{i+stride+1}, i.e. stride - 3 draws
-    const Jump jj = jump_of((uint64_t)grid * kTileElems - (kElemsPerLane - 1));
+    // merged tile jump: S_{i+kE} -> S_{i+stride+1}, i.e. stride - kE + 1 draws
+    const Jump jj = jump_of((uint64_t)grid * kTile - (kE - 1));
     a.aj_lo = lo64(jj.mult);
     a.aj_hi = hi64(jj.mult);
+    const u128 aji = inv128(jj.mult);
+    a.aji_lo = lo64(aji);
+    a.aji_hi = hi64(aji);
     for (int j = 0; j < P; j++) {
       const u128 cj = jj.gsum * mk128(a.s[j].inc_hi, a.s[j].inc_lo);
       a.s[j].cj_lo = lo64(cj);

@@ -47,7 +47,8 @@ struct KArgs {
   ClientArg c[kMaxLocal];
   StreamArg s[kMaxStreams];
   uint64_t n;
-  uint64_t aj_lo, aj_hi;  // A^J, J = grid*1024 - 4
+  uint64_t aj_lo, aj_hi;    // A^J, J = grid stride - 1 (merged tile jump)
+  uint64_t aji_lo, aji_hi;  // (A^J)^-1 mod 2^128 (prologue: park states one jump back)
   uint64_t* sum_out;
   uint64_t* digests;
   uint32_t* flags;

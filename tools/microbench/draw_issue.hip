@@ -1,0 +1,265 @@
+// Microbenchmark: issue efficiency of the hand-scheduled PCG64 draw
+// (sa_clients_impl.h, SA_PCG_DRAW_ASM) outside the product kernel.
+// Question it answers: where do the ~40% between the tight-loop draw rate and
+// the k_clients draw rate go — occupancy, LDS-resident constants, or the
+// asm-volatile serialisation of one stream's chain?
+// Standalone tool; not part of the product.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 draw_issue.hip -o draw_issue
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../sfl_amd/csrc/sa_clients_impl.h"
+
+#define CHECK(x)                                                                                      \
+  do {                                                                                                \
+    hipError_t e_ = (x);                                                                              \
+    if (e_ != hipSuccess) {                                                                           \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);          \
+      return 1;                                                                                       \
+    }                                                                                                 \
+  } while (0)
+
+using namespace sa;
+
+// Same asm as pcg_draw_pair/one, but the stream constants are SGPR operands
+// (scalar-loaded) and the multiplier limbs VGPR operands (gfx9 constant bus: one
+// SGPR source per VOP3).
+constexpr uint32_t A0 = 0x9FCCF645u, A1 = 0x4385DF64u, A2 = 0x1FC65DA4u, A3 = 0x2360ED05u;
+#define SMEM_INS                                                                                         \
+  [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c01] "s"(c01), [c23] "s"(c23), [m] "s"(m)
+__device__ __forceinline__ void draw_pair_s(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
+                                            uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
+                                            uint32_t m, uint32_t& zmin, uint32_t& ulo, uint32_t& uhi,
+                                            uint32_t& vlo, uint32_t& vhi) {
+  uint64_t k1, k2, k3;
+  asm volatile(SA_PCG_DRAW_ASM
+               "v_sub_co_u32_e64 %[vlo], %[k2], %[vlo], v6\n\t"
+               "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"
+               "v_addc_co_u32_e64 %[uhi], %[k1], %[uhi], v7, %[k1]\n\t"
+               "v_subb_co_u32_e64 %[vhi], %[k2], %[vhi], v7, %[k2]"
+               : SA_PCG_DRAW_OUTS, [vlo] "+v"(vlo), [vhi] "+v"(vhi)
+               : SMEM_INS
+               : SA_PCG_DRAW_CLOBBERS);
+}
+__device__ __forceinline__ void draw_one_s(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
+                                           uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
+                                           uint32_t m, uint32_t& zmin, uint32_t& ulo, uint32_t& uhi) {
+  uint64_t k1, k2, k3;
+  asm volatile(SA_PCG_DRAW_ASM
+               "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"
+               "s_nop 0\n\t"
+               "v_addc_co_u32_e64 %[uhi], %[k1], %[uhi], v7, %[k1]"
+               : SA_PCG_DRAW_OUTS
+               : SMEM_INS
+               : SA_PCG_DRAW_CLOBBERS);
+}
+
+typedef __attribute__((address_space(4))) const uint64_t* cptr_t;
+
+// MODE 2: stream-outer tile (4 draws per stream per tile, 4 x L accumulators),
+// constants scalar-loaded once per stream per tile.  PREF: load stream q+1's
+// constants after stream q's first draw.
+template <int P, int L, bool PAIRS, bool PREF, int E = 4>
+__global__ void __launch_bounds__(256) k_smem(uint64_t* out, int iters, uint32_t seed, const uint64_t* gconst) {
+  extern __shared__ char dyn[];
+  if (dyn[0] == 123 && seed == 77) out[0] = 1;
+  uint32_t st[P][4];
+  const uint32_t tid = threadIdx.x + blockIdx.x * blockDim.x;
+#pragma unroll
+  for (int j = 0; j < P; j++) {
+    st[j][0] = tid * 0x9E3779B9u + j;
+    st[j][1] = seed ^ (j * 77u);
+    st[j][2] = tid + 13u * j;
+    st[j][3] = ~tid;
+  }
+  const uint32_t a0 = __builtin_amdgcn_readfirstlane(A0 + seed), a1 = A1, a2 = A2, a3 = A3;
+  uint32_t va0, va1, va2, va3;
+  asm volatile("v_mov_b32 %0, %4\n\tv_mov_b32 %1, %5\n\tv_mov_b32 %2, %6\n\tv_mov_b32 %3, %7"
+               : "=v"(va0), "=v"(va1), "=v"(va2), "=v"(va3) : "s"(a0), "s"(a1), "s"(a2), "s"(a3));
+  uint32_t al[E][L], ah[E][L];
+#pragma unroll
+  for (int k = 0; k < E; k++)
+#pragma unroll
+    for (int c = 0; c < L; c++) al[k][c] = ah[k][c] = c + k;
+  uint32_t zmin = 0xFFFFFFFFu;
+  cptr_t cp = (cptr_t)gconst;
+  for (int it = 0; it < iters; it++) {
+    cptr_t f = cp;
+    asm volatile("" : "+s"(f));
+    uint64_t n01 = f[0], n23 = f[1], nm = f[4];
+#pragma unroll
+    for (int q = 0; q < P; q++) {
+      uint64_t c01 = n01, c23 = n23;
+      uint32_t sm = (uint32_t)nm;
+      if constexpr (!PREF) {
+        cptr_t g = cp + 8 * q;
+        asm volatile("" : "+s"(g));
+        c01 = g[0];
+        c23 = g[1];
+        sm = (uint32_t)g[4];
+      }
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        if constexpr (PAIRS) {
+          constexpr int PI = Pairs<L>::count;
+          const int cu = Pairs<L>::u(q % PI), cv = Pairs<L>::v(q % PI);
+          draw_pair_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, c01, c23, sm, zmin, al[k][cu],
+                      ah[k][cu], al[k][cv], ah[k][cv]);
+        } else {
+          const int cu = q % L;
+          draw_one_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, c01, c23, sm, zmin, al[k][cu],
+                     ah[k][cu]);
+        }
+        if (PREF && k == 0 && q + 1 < P) {
+          cptr_t g = cp + 8 * (q + 1);
+          asm volatile("" : "+s"(g));
+          n01 = g[0];
+          n23 = g[1];
+          nm = g[4];
+        }
+      }
+    }
+  }
+  uint64_t acc = zmin;
+#pragma unroll
+  for (int k = 0; k < E; k++)
+#pragma unroll
+    for (int c = 0; c < L; c++) acc += pack64(al[k][c], ah[k][c]);
+#pragma unroll
+  for (int j = 0; j < P; j++) acc ^= st[j][0] ^ st[j][3];
+  out[tid] = acc;
+}
+
+// MODE 0: constants in VGPRs (loaded once);  MODE 1: constants from LDS per draw
+// (the product kernel's scheme).  PAIRS: internal pair draws into L accumulators.
+template <int P, int L, bool PAIRS, int MODE>
+__global__ void __launch_bounds__(256) k_draws(uint64_t* out, int iters, uint32_t seed) {
+  extern __shared__ char dyn[];  // occupancy limiter only
+  __shared__ StreamLds sl[P];
+  for (int j = threadIdx.x; j < P; j += blockDim.x)
+    sl[j] = StreamLds{2ull * j + 1 + seed, (uint64_t)j << 7, 3ull * j, 0, (j & 1) ? ~0ull : 0ull, 0};
+  __syncthreads();
+  if (dyn[0] == 123 && seed == 77) out[0] = 1;  // keep the dynamic LDS allocation
+
+  uint32_t st[P][4];
+  const uint32_t tid = threadIdx.x + blockIdx.x * blockDim.x;
+#pragma unroll
+  for (int j = 0; j < P; j++) {
+    st[j][0] = tid * 0x9E3779B9u + j;
+    st[j][1] = seed ^ (j * 77u);
+    st[j][2] = tid + 13u * j;
+    st[j][3] = ~tid;
+  }
+  uint64_t rc01[MODE == 0 ? P : 1], rc23[MODE == 0 ? P : 1];
+  uint32_t rm[MODE == 0 ? P : 1];
+  if constexpr (MODE == 0) {
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+      rc01[j] = sl[j].inc_lo;
+      rc23[j] = sl[j].inc_hi;
+      rm[j] = (uint32_t)sl[j].smask;
+    }
+  }
+  uint32_t al[L], ah[L];
+#pragma unroll
+  for (int c = 0; c < L; c++) al[c] = ah[c] = c;
+  uint32_t zmin = 0xFFFFFFFFu;
+  lds_ptr slp = (lds_ptr)(sl);
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int q = 0; q < P; q++) {
+      uint64_t c01, c23;
+      uint32_t sm;
+      if constexpr (MODE == 0) {
+        c01 = rc01[q];
+        c23 = rc23[q];
+        sm = rm[q];
+      } else {
+        asm volatile("" : "+v"(slp));
+        typedef __attribute__((address_space(3))) const uint64_t* lds_u64;
+        const lds_u64 cp = (lds_u64)(slp + q);
+        c01 = cp[0];
+        c23 = cp[1];
+        sm = (uint32_t)slp[q].smask;
+      }
+      if constexpr (PAIRS) {
+        constexpr int PI = Pairs<L>::count;
+        const int cu = Pairs<L>::u(q % PI), cv = Pairs<L>::v(q % PI);
+        pcg_draw_pair(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, c01, c23, sm, zmin, al[cu], ah[cu],
+                      al[cv], ah[cv]);
+      } else {
+        const int cu = q % L;
+        pcg_draw_one(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, c01, c23, sm, zmin, al[cu], ah[cu]);
+      }
+    }
+  }
+  uint64_t acc = zmin;
+#pragma unroll
+  for (int c = 0; c < L; c++) acc += pack64(al[c], ah[c]);
+#pragma unroll
+  for (int j = 0; j < P; j++) acc ^= st[j][0] ^ st[j][3];
+  out[tid] = acc;
+}
+
+int main() {
+  int ncu = 0;
+  CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  uint64_t* d_out;
+  CHECK(hipMalloc(&d_out, (size_t)ncu * 8 * 256 * sizeof(uint64_t)));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  uint64_t* gconst;
+  CHECK(hipMalloc(&gconst, 64 * 64));
+  {
+    uint64_t h[64 * 8];
+    for (int j = 0; j < 64; j++) {
+      h[8 * j + 0] = 2ull * j + 7;
+      h[8 * j + 1] = (uint64_t)j << 7;
+      h[8 * j + 2] = 3ull * j;
+      h[8 * j + 3] = 0;
+      h[8 * j + 4] = (j & 1) ? ~0ull : 0ull;
+      h[8 * j + 5] = h[8 * j + 6] = h[8 * j + 7] = 0;
+    }
+    CHECK(hipMemcpy(gconst, h, sizeof(h), hipMemcpyHostToDevice));
+  }
+  auto run = [&](auto kern, int P, const char* name, int iters, auto... extra) -> int {
+    for (int w : {1, 2, 3, 4, 5, 6, 8}) {
+      // w blocks of 4 waves per CU -> w waves per SIMD (if registers allow)
+      const size_t dyn = (160 * 1024) / w - 4096;
+      int nb = 0;
+      CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, dyn));
+      if (nb < w) {
+        printf("%-22s waves/SIMD=%d  not reachable (max %d)\n", name, w, nb);
+        continue;
+      }
+      const int blocks = ncu * w;
+      float ms = 0;
+      for (int rep = 0; rep < 2; rep++) {
+        CHECK(hipEventRecord(e0));
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), dyn, 0, d_out, iters, 5u, extra...);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+      }
+      const double draws = (double)blocks * 256 * iters * P;
+      printf("%-22s waves/SIMD=%d  %8.3f ms  %7.1f G draws/s\n", name, w, ms, draws / (ms * 1e-3) / 1e9);
+      fflush(stdout);
+    }
+    return 0;
+  };
+  if (run(k_draws<7, 1, false, 0>, 7, "one7 L1 reg", 4000)) return 1;
+  if (run(k_draws<7, 1, false, 1>, 7, "one7 L1 lds", 4000)) return 1;
+  if (run(k_draws<28, 8, true, 1>, 28, "pair28 L8 lds", 1000)) return 1;
+  if (run(k_draws<28, 8, true, 0>, 28, "pair28 L8 reg", 1000)) return 1;
+  const uint64_t* gc = gconst;
+  if (run(k_smem<7, 1, false, true, 4>, 28, "one7 L1 smem E4", 1000, gc)) return 1;
+  if (run(k_smem<7, 1, false, true, 1>, 7, "one7 L1 smem E1", 4000, gc)) return 1;
+  if (run(k_smem<7, 1, false, true, 2>, 14, "one7 L1 smem E2", 2000, gc)) return 1;
+  if (run(k_smem<28, 8, true, true, 4>, 112, "pair28 L8 smem E4", 250, gc)) return 1;
+  if (run(k_smem<28, 8, true, true, 2>, 56, "pair28 L8 smem E2", 500, gc)) return 1;
+  if (run(k_smem<28, 8, true, true, 1>, 28, "pair28 L8 smem E1", 1000, gc)) return 1;
+  CHECK(hipGetLastError());
+  return 0;
+}
