@@ -47,7 +47,7 @@ namespace sa {
 
 // Tuning-only ablations (results are WRONG when nonzero; never shipped):
 // 1 = no zero-draw check, 2 = no quantize conversion, 8 = no global
-// loads/stores.
+// loads/stores, 32 = no digest LDS atomics, 64 = no prologue jump.
 #ifndef SA_ABLATE
 #define SA_ABLATE 0
 #endif
@@ -69,6 +69,23 @@ constexpr PowTable make_pow_table() {
 }
 // jump by 2^b draws, b = 0..63 — identical in every translation unit
 static __constant__ PowTable kPowTable = make_pow_table();
+
+// kLaneJump[t] = jump by t*kE + 1 draws: from a block tile's base state to the
+// state lane t draws its first element from.  With the uniform block part
+// (bits of blockIdx * kTile, scalar-loaded from kPowTable) the prologue
+// costs one coalesced table load per lane instead of a divergent chain of
+// ~27 dependent table loads.
+struct LaneTable {
+  Jump e[kBlockThreads];
+};
+constexpr LaneTable make_lane_table() {
+  LaneTable t{};
+  for (int l = 0; l < kBlockThreads; l++) t.e[l] = jump_of((uint64_t)l * kE + 1);
+  return t;
+}
+static __constant__ LaneTable kLaneJump = make_lane_table();
+static_assert((kTile & (kTile - 1)) == 0, "kTile is a power of two");
+constexpr int kTileLog2 = __builtin_ctz(kTile);
 
 // ----------------------------------------------------------------------------
 // element loads / quantize
@@ -166,6 +183,44 @@ __device__ __forceinline__ CT scalar_weight(double w) {
     return (CT)(long long)w;
   else
     return (CT)w;
+}
+
+// The tile's products p = x * (w * 2^fxp) for the fp32 fast path, and
+// whether it applies: every product of the wave below 2^31 (one v_cmp each,
+// ANDed into one wave vote per tile), so each converts with one
+// v_cvt_i32_f32.  Otherwise the tile takes the exact x86-semantics int64
+// path (NaN / inf / huge values) of quantize().
+// (x*w)*2^fxp == x*(w*2^fxp) whenever w*2^fxp is finite (a power-of-two
+// scale commutes with rounding; subnormal products truncate to 0 either way);
+// a non-finite w*2^fxp yields a non-finite p, i.e. the exact path.
+template <typename XT, typename CT, int L, bool kGeneral>
+__device__ __forceinline__ bool fast_products(const Vec2<XT> (&xv)[L], const Vec2<CT> (&wv)[kGeneral ? L : 1],
+                                              const __attribute__((address_space(4))) KArgs* ka,
+                                              const QScale& qs, float (&p)[L][kE]) {
+  if constexpr (std::is_same<CT, float>::value) {
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < L; c++) {
+      const bool has_wv = kGeneral && ka->c[c].wvec;
+#pragma unroll
+      for (int k = 0; k < kE; k++) {
+        const float w = has_wv ? (float)wv[kGeneral ? c : 0].v[k] : scalar_weight<float>(ka->c[c].w);
+        p[c][k] = __fmul_rn((float)xv[c].v[k], __fmul_rn(w, qs.f));
+        ok = ok && (__builtin_fabsf(p[c][k]) < 0x1p31f);
+      }
+    }
+    return !__any(!ok) || (SA_ABLATE & 2);
+  } else {
+    return false;
+  }
+}
+template <typename XT, typename CT, int L, bool kGeneral>
+__device__ __forceinline__ uint64_t exact_q(const Vec2<XT> (&xv)[L], const Vec2<CT> (&wv)[kGeneral ? L : 1],
+                                            const __attribute__((address_space(4))) KArgs* ka, const QScale& qs,
+                                            int c, int k) {
+  const bool has_wv = kGeneral && ka->c[c].wvec;
+  const CT w = has_wv ? wv[kGeneral ? c : 0].v[k] : scalar_weight<CT>(ka->c[c].w);
+  return quantize<XT, CT>(xv[c].v[k], w, qs);
 }
 
 // ----------------------------------------------------------------------------
@@ -299,13 +354,14 @@ struct Pairs {
 // ----------------------------------------------------------------------------
 
 // Waves per SIMD the register allocation must allow (spill-free targets from
-// the compiler's census, tools/kregs.py): 4 VGPRs per stream state, 3 per
-// (client, element) (accumulator halves + input), plus the draw scratch,
-// multipliers and addressing; the single-client kernel also carries the
-// continue / per-element-weight / DP-noise paths.  L = 8 (28 pair streams):
-// 2 waves; 1 client + 7 cross streams: 5.
+// the compiler's census, tools/kregs.py): 4 VGPRs per stream state, 4 per
+// (client, element) (accumulator halves, input, product), 2 per client
+// (digest), plus the draw scratch, multipliers and addressing; the
+// single-client kernel also carries the continue / per-element-weight /
+// DP-noise paths.  L = 8 (28 pair streams): 2 waves; 1 client + 7 cross
+// streams: 5.
 constexpr int clients_waves(int P, int L) {
-  const int regs = 4 * P + 3 * L * kE + (L == 1 ? 60 : 48);
+  const int regs = 4 * P + 4 * L * kE + 2 * L + (L == 1 ? 64 : 56);
   const int w = 512 / regs;
   return w > 8 ? 8 : (w < 1 ? 1 : w);
 }
@@ -338,18 +394,19 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
   static_assert(P <= kMaxStreams, "P");
 
   const uint64_t n = a.n;
-  const uint64_t first = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kE;
   const uint64_t stride = (uint64_t)gridDim.x * kTile;
 
   // ---- prologue: park every stream one tile jump before S_{first+1}, the
   // state element `first` is drawn from: V = A^-J (S_{first+1} - inc*G_J)
   uint32_t st[P > 0 ? P : 1][4];  // 128-bit states as 32-bit limbs
   if constexpr (P > 0) {
-    Jump jl{1, 0};
-    uint64_t pos = first + 1;
-    for (int b = 0; pos != 0; b++, pos >>= 1) {
-      if (pos & 1) jl = compose(jl, kPowTable.e[b]);
+    // J(first + 1) = J(blockIdx * kTile) o J(lane * kE + 1)
+    Jump jb{1, 0};
+    const uint32_t bid = (SA_ABLATE & 64) ? 0u : blockIdx.x;
+    for (int b = 0; (bid >> b) != 0; b++) {  // wave-uniform
+      if ((bid >> b) & 1) jb = compose(jb, kPowTable.e[kTileLog2 + b]);
     }
+    const Jump jl = compose(kLaneJump.e[threadIdx.x], jb);
     const u128 aji = ld128(a.aji_lo, a.aji_hi);
 #pragma unroll
     for (int j = 0; j < P; j++) {
@@ -375,10 +432,9 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
 
   uint32_t zmin = 0xFFFFFFFFu;  // 0 iff some raw PCG64 draw of this lane was 0
 
-  // per-lane XOR digests live in LDS (one lane-private slot per client)
-  __shared__ uint64_t dig_lds[L][kBlockThreads];
+  uint64_t dig[L];  // per-lane XOR digests of the clients' masked values
 #pragma unroll
-  for (int c = 0; c < L; c++) dig_lds[c][threadIdx.x] = 0;
+  for (int c = 0; c < L; c++) dig[c] = 0;
 
   float dp_s = 1.0f;
   if constexpr (kGeneral && std::is_same<XT, float>::value && std::is_same<CT, float>::value) {
@@ -471,30 +527,35 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
       }
     }
     const QScale qs{ka->scale_f, ka->scale_d, ka->fxp_bits};
+    // elements past n only occur in the wave's last tile (uniform test)
+    const bool wave_full = base + wave_off + 64 * kE <= n;
     uint64_t sum[kE] = {0, 0};
-#pragma unroll
-    for (int c = 0; c < L; c++) {
-      uint64_t acc[kE];
-#pragma unroll
-      for (int k = 0; k < kE; k++) {
-        uint64_t v = pack64(al[k][c], ah[k][c]);
-        if (cont) {
-          v += pv[kGeneral ? c : 0].v[k];
-        } else {
-          const CT w = (kGeneral && ka->c[c].wvec) ? wv[kGeneral ? c : 0].v[k] : scalar_weight<CT>(ka->c[c].w);
-          const XT xk = xv[c].v[k];
-          if (SA_ABLATE & 2)
-            v += __builtin_bit_cast(uint32_t, (float)xk);
-          else
-            v += quantize<XT, CT>(xk, w, qs);
-        }
-        acc[k] = v;
-        sum[k] += v;
+    auto finish = [&](int c, uint64_t q0, uint64_t q1) {
+      const uint64_t a0 = pack64(al[0][c], ah[0][c]) + q0, a1 = pack64(al[1][c], ah[1][c]) + q1;
+      sum[0] += a0;
+      sum[1] += a1;
+      if (!(SA_ABLATE & 32)) {
+        if (wave_full)
+          dig[c] ^= a0 ^ a1;
+        else
+          dig[c] ^= (i < n ? a0 : 0) ^ (i + 1 < n ? a1 : 0);
       }
-      const uint64_t d = (i < n ? acc[0] : 0) ^ (i + 1 < n ? acc[1] : 0);
-      __hip_atomic_fetch_xor(&dig_lds[c][threadIdx.x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       uint64_t* mo = ka->c[c].masked_out;
-      if (mo) bstore2_u64(make_rsrc(mo, n * 8), i, acc[0], acc[1]);
+      if (mo) bstore2_u64(make_rsrc(mo, n * 8), i, a0, a1);
+    };
+    static_assert(kE == 2, "finish() takes the lane's two elements");
+    float p[L][kE];
+    if (cont) {  // a further pass: add the prior pass's masked vector
+#pragma unroll
+      for (int c = 0; c < L; c++) finish(c, pv[kGeneral ? c : 0].v[0], pv[kGeneral ? c : 0].v[1]);
+    } else if (__builtin_expect(fast_products<XT, CT, L, kGeneral>(xv, wv, ka, qs, p), 1)) {
+#pragma unroll
+      for (int c = 0; c < L; c++)
+        finish(c, (uint64_t)(int64_t)(int32_t)p[c][0], (uint64_t)(int64_t)(int32_t)p[c][1]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < L; c++)
+        finish(c, exact_q<XT, CT, L, kGeneral>(xv, wv, ka, qs, c, 0), exact_q<XT, CT, L, kGeneral>(xv, wv, ka, qs, c, 1));
     }
     const int sum_mode = ka->sum_mode;
     if (sum_mode != 0 && (!(SA_ABLATE & 8) || sum[0] == 0x123456789ull)) {
@@ -512,7 +573,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
   if (a.do_digest) {
 #pragma unroll
     for (int c = 0; c < L; c++) {
-      uint64_t d = dig_lds[c][threadIdx.x];
+      uint64_t d = dig[c];
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) d ^= __shfl_xor(d, off, 64);
       if ((threadIdx.x & 63) == 0 && d) atomicXor((unsigned long long*)&a.digests[c], d);

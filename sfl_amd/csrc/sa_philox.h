@@ -37,8 +37,13 @@ SA_PHX_HD inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 }
 
 #if defined(__HIPCC__)
-// 4 standard normals of counter block `blk` under `key`.
-__device__ __forceinline__ Normal4 gauss4(uint64_t key, uint64_t blk) {
+// 4 standard normals of counter block `blk` under `key`.  Never inlined: the
+// libm calls inside (logf, sincospif) are otherwise optimised together with
+// the caller, and contraction / scheduling decisions that differ between the
+// fused masking kernel and the standalone perturb kernel changed the last
+// bit of some normals.  As a called function every kernel runs the same
+// instruction sequence.
+__device__ __noinline__ Normal4 gauss4(uint64_t key, uint64_t blk) {
   uint32_t c[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u};
   philox4x32_10(c, (uint32_t)key, (uint32_t)(key >> 32));
   Normal4 o;
