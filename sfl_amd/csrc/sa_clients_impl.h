@@ -40,6 +40,7 @@
 
 #include "../../include/sfl_sa.h"
 #include "pcg128.h"
+#include "sa_draw2.h"
 #include "sa_internal.h"
 #include "sa_philox.h"
 
@@ -47,7 +48,8 @@ namespace sa {
 
 // Tuning-only ablations (results are WRONG when nonzero; never shipped):
 // 1 = no zero-draw check, 2 = no quantize conversion, 8 = no global
-// loads/stores, 32 = no digest LDS atomics, 64 = no prologue jump.
+// loads/stores, 32 = no digests, 64 = no prologue jump, 128 = stream 0's
+// constants for every stream (no per-stream scalar loads).
 #ifndef SA_ABLATE
 #define SA_ABLATE 0
 #endif
@@ -349,6 +351,43 @@ struct Pairs {
   }
 };
 
+
+// Draw schedule of a launch: the P streams grouped into interleaved pairs
+// (sa_draw2.h) wherever two streams touch disjoint accumulators (or, for
+// two cross streams of the same client, one shared accumulator), singles
+// otherwise.  Internal pairs of L clients are matched greedily
+// (for L = 8: 14 disjoint pairs of pairs), cross streams by client.
+struct Group {
+  int qa, qb;          // streams (qb < 0: single draw)
+  int ua, va, ub, vb;  // accumulators (clients); v < 0: a cross stream (no partner)
+};
+template <int L, int X>
+struct Sched {
+  static constexpr int PI = Pairs<L>::count;
+  static constexpr int P = PI + L * X;
+  int n = 0;
+  Group g[P > 0 ? P : 1] = {};
+  constexpr Sched() {
+    bool used[P > 0 ? P : 1] = {};
+    auto cl_u = [](int q) { return q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1); };
+    auto cl_v = [](int q) { return q < PI ? Pairs<L>::v(q) : -1; };
+    for (int q = 0; q < P; q++) {
+      if (used[q]) continue;
+      used[q] = true;
+      int mate = -1;
+      for (int r = q + 1; r < P && mate < 0; r++) {
+        if (used[r] || (q < PI) != (r < PI)) continue;
+        const int a = cl_u(q), b = cl_v(q), c = cl_u(r), d = cl_v(r);
+        const bool disjoint = a != c && a != d && (b < 0 || (b != c && b != d));
+        const bool same_one = q >= PI && a == c;  // two cross streams of one client
+        if (disjoint || same_one) mate = r;
+      }
+      if (mate >= 0) used[mate] = true;
+      g[n++] = Group{q, mate, cl_u(q), cl_v(q), mate >= 0 ? cl_u(mate) : -1, mate >= 0 ? cl_v(mate) : -1};
+    }
+  }
+};
+
 // ----------------------------------------------------------------------------
 // the kernel
 // ----------------------------------------------------------------------------
@@ -432,9 +471,19 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
 
   uint32_t zmin = 0xFFFFFFFFu;  // 0 iff some raw PCG64 draw of this lane was 0
 
-  uint64_t dig[L];  // per-lane XOR digests of the clients' masked values
+  // per-lane XOR digests of the clients' masked values: VGPRs, or for the
+  // register-bound shapes (5+ co-located clients) lane-private LDS slots
+  // updated with one ds_xor_b64 per client and tile
+  constexpr bool kDigLds = L >= 5;
+  uint64_t dig[kDigLds ? 1 : L];
+  __shared__ uint64_t dig_lds[kDigLds ? L : 1][kBlockThreads];
 #pragma unroll
-  for (int c = 0; c < L; c++) dig[c] = 0;
+  for (int c = 0; c < L; c++) {
+    if constexpr (kDigLds)
+      dig_lds[c][threadIdx.x] = 0;
+    else
+      dig[c] = 0;
+  }
 
   float dp_s = 1.0f;
   if constexpr (kGeneral && std::is_same<XT, float>::value && std::is_same<CT, float>::value) {
@@ -479,37 +528,67 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
       }
     }
 
-    // ---- mask expansion, stream-outer; stream q+1's constants are
-    // scalar-loaded during q's first draw
+    // ---- mask expansion, stream-outer, two streams per asm block where the
+    // schedule pairs them; group g+1's constants are scalar-loaded during
+    // group g's first draw
     if constexpr (P > 0) {
-      const kptr_t ks = (const kptr_t)(&fenced_args()->s[0]);
-      uint64_t ni0 = ks[2], ni1 = ks[3], nj0 = ks[4], nj1 = ks[5];
-      uint32_t nm = (uint32_t)ks[6];
+      constexpr Sched<L, X> S{};
+      uint64_t ni0[2], ni1[2], nj0[2], nj1[2];
+      uint32_t nm[2];
+      auto fetch = [&](int g) {
 #pragma unroll
-      for (int q = 0; q < P; q++) {
-        const uint64_t ci0 = ni0, ci1 = ni1, cj0 = nj0, cj1 = nj1;
-        const uint32_t m = nm;
-        const int cu = q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1);
+        for (int h = 0; h < 2; h++) {
+          const int q = h == 0 ? S.g[g].qa : S.g[g].qb;
+          if (q < 0) continue;
+          kptr_t c = (const kptr_t)(&fenced_args()->s[q]);
+          ni0[h] = c[2];
+          ni1[h] = c[3];
+          nj0[h] = c[4];
+          nj1[h] = c[5];
+          nm[h] = (uint32_t)c[6];
+        }
+      };
+      fetch(0);
+#pragma unroll
+      for (int g = 0; g < S.n; g++) {
+        const Group G = S.g[g];
+        uint64_t ci0[2], ci1[2], cj0[2], cj1[2];
+        uint32_t m[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          ci0[h] = ni0[h];
+          ci1[h] = ni1[h];
+          cj0[h] = nj0[h];
+          cj1[h] = nj1[h];
+          m[h] = nm[h];
+        }
 #pragma unroll
         for (int k = 0; k < kE; k++) {
           const uint32_t* mk = k == 0 ? mj : mp;
-          const uint64_t c01 = k == 0 ? cj0 : ci0, c23 = k == 0 ? cj1 : ci1;
-          if (q < PI) {
-            const int cv = Pairs<L>::v(q);
-            pcg_draw_pair(st[q][0], st[q][1], st[q][2], st[q][3], mk[0], mk[1], mk[2], mk[3], c01, c23, m, zmin,
-                          al[k][cu], ah[k][cu], al[k][cv], ah[k][cv]);
+          const uint64_t ca = k == 0 ? cj0[0] : ci0[0], da = k == 0 ? cj1[0] : ci1[0];
+          const uint64_t cb = k == 0 ? cj0[1] : ci0[1], db = k == 0 ? cj1[1] : ci1[1];
+          uint32_t* sa = st[G.qa];
+          if (G.qb < 0) {
+            if (G.va >= 0)
+              pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], zmin,
+                            al[k][G.ua], ah[k][G.ua], al[k][G.va], ah[k][G.va]);
+            else
+              pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], zmin,
+                           al[k][G.ua], ah[k][G.ua]);
           } else {
-            pcg_draw_one(st[q][0], st[q][1], st[q][2], st[q][3], mk[0], mk[1], mk[2], mk[3], c01, c23, m, zmin,
-                         al[k][cu], ah[k][cu]);
+            uint32_t* sb = st[G.qb];
+            if (G.va >= 0)
+              pcg_draw2_pair(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca,
+                             da, m[0], cb, db, m[1], zmin, al[k][G.ua], ah[k][G.ua], al[k][G.va], ah[k][G.va],
+                             al[k][G.ub], ah[k][G.ub], al[k][G.vb], ah[k][G.vb]);
+            else if (G.ua == G.ub)
+              pcg_draw2_one_same(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3],
+                                 ca, da, m[0], cb, db, m[1], zmin, al[k][G.ua], ah[k][G.ua]);
+            else
+              pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca,
+                            da, m[0], cb, db, m[1], zmin, al[k][G.ua], ah[k][G.ua], al[k][G.ub], ah[k][G.ub]);
           }
-          if (k == 0 && q + 1 < P) {
-            kptr_t g = (const kptr_t)(&fenced_args()->s[q + 1]);
-            ni0 = g[2];
-            ni1 = g[3];
-            nj0 = g[4];
-            nj1 = g[5];
-            nm = (uint32_t)g[6];
-          }
+          if (k == 0 && g + 1 < S.n && !(SA_ABLATE & 128)) fetch(g + 1);
         }
       }
     }
@@ -535,10 +614,11 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
       sum[0] += a0;
       sum[1] += a1;
       if (!(SA_ABLATE & 32)) {
-        if (wave_full)
-          dig[c] ^= a0 ^ a1;
+        const uint64_t d = wave_full ? a0 ^ a1 : (i < n ? a0 : 0) ^ (i + 1 < n ? a1 : 0);
+        if constexpr (kDigLds)
+          __hip_atomic_fetch_xor(&dig_lds[c][threadIdx.x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         else
-          dig[c] ^= (i < n ? a0 : 0) ^ (i + 1 < n ? a1 : 0);
+          dig[kDigLds ? 0 : c] ^= d;
       }
       uint64_t* mo = ka->c[c].masked_out;
       if (mo) bstore2_u64(make_rsrc(mo, n * 8), i, a0, a1);
@@ -573,7 +653,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
   if (a.do_digest) {
 #pragma unroll
     for (int c = 0; c < L; c++) {
-      uint64_t d = dig[c];
+      uint64_t d = kDigLds ? dig_lds[c][threadIdx.x] : dig[kDigLds ? 0 : c];
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) d ^= __shfl_xor(d, off, 64);
       if ((threadIdx.x & 63) == 0 && d) atomicXor((unsigned long long*)&a.digests[c], d);

@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""Generates sfl_amd/csrc/sa_draw2.h: two PCG64 draws (two independent mask
+streams, same multiplier) as ONE hand-scheduled inline-asm block, their
+instruction streams interleaved so every dependent pair of one stream sits at
+least two issue slots apart (the other stream's instruction fills the gap).
+
+The single-draw schedule is SA_PCG_DRAW_ASM in sa_clients_impl.h; this script
+keeps its instructions, renames stream B onto its own scratch VGPRs
+(v10-v19), carry SGPR pairs and a swap mask in an SGPR pair instead of VCC,
+merges the two raw==0 running minimums into one v_min3, and checks the gfx950
+rule the single draw already follows: a VALU-written SGPR (carry, VCC) is
+read no earlier than the third instruction after the write (s_nop padding is
+inserted where the interleave alone does not give that).
+
+usage: python tools/gen_draw2.py > sfl_amd/csrc/sa_draw2.h
+"""
+
+# one draw: (asm, sgpr_writes, sgpr_reads); {..} fields are renamed per stream
+DRAW = [
+    ("v_mad_u64_u32 v[{v0}:{v1}], %[{k1}], %[{s0}], %[a0], %[{c01}]", {"k1"}, set()),
+    ("v_mad_u64_u32 v[{v2}:{v3}], %[{k3}], %[{s0}], %[a1], 0", {"k3"}, set()),
+    ("v_mad_u64_u32 v[{v4}:{v5}], %[{k3}], %[{s0}], %[a2], %[{c23}]", {"k3"}, set()),
+    ("v_mul_lo_u32 v{v6}, %[{s0}], %[a3]", set(), set()),
+    ("v_mad_u64_u32 v[{v2}:{v3}], %[{k2}], %[{s1}], %[a0], v[{v2}:{v3}]", {"k2"}, set()),
+    ("v_mad_u64_u32 v[{v4}:{v5}], %[{k3}], %[{s1}], %[a1], v[{v4}:{v5}]", {"k3"}, set()),
+    ("v_mul_lo_u32 v{v7}, %[{s1}], %[a2]", set(), set()),
+    ("v_mad_u64_u32 v[{v4}:{v5}], %[{k3}], %[{s2}], %[a0], v[{v4}:{v5}]", {"k3"}, set()),
+    ("v_mul_lo_u32 v{v8}, %[{s2}], %[a1]", set(), set()),
+    ("v_mul_lo_u32 v{v9}, %[{s3}], %[a0]", set(), set()),
+    ("v_add_co_u32_e64 %[{s1}], %[{k3}], v{v1}, v{v2}", {"k3"}, set()),
+    ("v_addc_co_u32_e64 %[{s3}], %[{k2}], v{v5}, v{v6}, %[{k2}]", {"k2"}, {"k2"}),
+    ("v_add_u32_e32 %[{s3}], %[{s3}], v{v9}", set(), set()),
+    ("v_addc_co_u32_e64 %[{s2}], %[{k2}], v{v4}, v{v3}, %[{k3}]", {"k2"}, {"k3"}),
+    ("v_addc_co_u32_e64 %[{s2}], %[{k3}], %[{s2}], 0, %[{k1}]", {"k3"}, {"k1"}),
+    ("v_mov_b32_e32 %[{s0}], v{v0}", set(), set()),
+    ("v_addc_co_u32_e64 %[{s3}], %[{k2}], %[{s3}], v{v7}, %[{k2}]", {"k2"}, {"k2"}),
+    ("v_addc_co_u32_e64 %[{s3}], %[{k3}], %[{s3}], v{v8}, %[{k3}]", {"k3"}, {"k3"}),
+    ("v_bitop3_b32 v{v0}, %[{s0}], %[{s2}], %[{m}] bitop3:0x96", set(), set()),
+    ("v_bitop3_b32 v{v1}, %[{s1}], %[{s3}], %[{m}] bitop3:0x96", set(), set()),
+    ("{cmp}", {"sw"}, set()),
+    ("v_lshrrev_b32_e32 v{v2}, 26, %[{s3}]", set(), set()),
+    ("v_bitop3_b32 v{v3}, v{v0}, v{v1}, %[{m}] bitop3:0x7e", set(), set()),
+    ("v_alignbit_b32 v{v4}, v{v1}, v{v0}, v{v2}", set(), set()),
+    ("v_alignbit_b32 v{v5}, v{v0}, v{v1}, v{v2}", set(), set()),
+    ("ZMIN", set(), set()),
+    ("{cnd_lo}", set(), {"sw"}),
+    ("v_add_co_u32_e64 %[{ulo}], %[{k1}], %[{ulo}], v{v6}", {"k1"}, set()),
+    ("SUBLO", {"k2"}, set()),
+    ("{cnd_hi}", set(), {"sw"}),
+    ("v_addc_co_u32_e64 %[{uhi}], %[{k1}], %[{uhi}], v{v7}, %[{k1}]", {"k1"}, {"k1"}),
+    ("SUBHI", {"k2"}, {"k2"}),
+]
+
+
+def stream(tag, base, pair, acc_u, acc_v):
+    f = {"s0": f"s0{tag}", "s1": f"s1{tag}", "s2": f"s2{tag}", "s3": f"s3{tag}",
+         "k1": f"k1{tag}", "k2": f"k2{tag}", "k3": f"k3{tag}",
+         "c01": f"c01{tag}", "c23": f"c23{tag}", "m": f"m{tag}", "ulo": f"{acc_u}lo", "uhi": f"{acc_u}hi"}
+    for i in range(10):
+        f[f"v{i}"] = str(base + i)
+    if tag == "a":
+        f["cmp"] = f"v_cmp_gt_i32_e32 vcc, 0, %[s3a]"
+        f["cnd_lo"] = f"v_cndmask_b32_e32 v{base + 6}, v{base + 4}, v{base + 5}, vcc"
+        f["cnd_hi"] = f"v_cndmask_b32_e32 v{base + 7}, v{base + 5}, v{base + 4}, vcc"
+    else:
+        f["cmp"] = f"v_cmp_gt_i32_e64 %[swb], 0, %[s3b]"
+        f["cnd_lo"] = f"v_cndmask_b32_e64 v{base + 6}, v{base + 4}, v{base + 5}, %[swb]"
+        f["cnd_hi"] = f"v_cndmask_b32_e64 v{base + 7}, v{base + 5}, v{base + 4}, %[swb]"
+    out = []
+    for asm, w, r in DRAW:
+        if asm == "SUBLO":
+            if not pair:
+                continue
+            asm = f"v_sub_co_u32_e64 %[{acc_v}lo], %[k2{tag}], %[{acc_v}lo], v{base + 6}"
+        elif asm == "SUBHI":
+            if not pair:
+                continue
+            asm = f"v_subb_co_u32_e64 %[{acc_v}hi], %[k2{tag}], %[{acc_v}hi], v{base + 7}, %[k2{tag}]"
+        elif asm == "ZMIN":
+            asm = "ZMIN"
+        else:
+            asm = asm.format(**f)
+        out.append((asm, {f"{x}{tag}" for x in w}, {f"{x}{tag}" for x in r}))
+    return out
+
+
+def interleave(a, b):
+    seq = []
+    for i in range(max(len(a), len(b))):
+        if i < len(a):
+            seq.append(a[i])
+        if i < len(b):
+            seq.append(b[i])
+    # the two raw==0 minimums become one v_min3 at B's ZMIN slot
+    zs = [i for i, s in enumerate(seq) if s[0] == "ZMIN"]
+    seq[zs[1]] = ("v_min3_u32 %[zmin], %[zmin], v3, v13", set(), set())
+    del seq[zs[0]]
+    # hazard check: reader index - last writer index >= 3, else pad with s_nop
+    out = []
+    last_w = {}
+    for asm, w, r in seq:
+        need = max([last_w[x] + 3 for x in r if x in last_w] or [0])
+        while len(out) < need:
+            out.append(("s_nop 0", set(), set()))
+            need = max([last_w[x] + 3 for x in r if x in last_w] or [0])
+        for x in w:
+            last_w[x] = len(out)
+        out.append((asm, w, r))
+    return out
+
+
+def emit(name, pair, same_acc):
+    acc_ua, acc_va = "ua", "va"
+    acc_ub, acc_vb = ("ua", None) if same_acc else ("ub", "vb")
+    a = stream("a", 0, pair, acc_ua, acc_va)
+    b = stream("b", 10, pair, acc_ub, acc_vb)
+    seq = interleave(a, b)
+    n_valu = sum(1 for s in seq if s[0].startswith("v_"))
+    n_nop = sum(1 for s in seq if s[0].startswith("s_nop"))
+    accs = ["ua"] + (["va"] if pair else []) + ([] if same_acc else ["ub"] + (["vb"] if pair else []))
+    lines = []
+    lines.append(f"// {name}: {n_valu} VALU + {n_nop} s_nop for two draws")
+    params = ["uint32_t& s0a", "uint32_t& s1a", "uint32_t& s2a", "uint32_t& s3a",
+              "uint32_t& s0b", "uint32_t& s1b", "uint32_t& s2b", "uint32_t& s3b",
+              "uint32_t a0", "uint32_t a1", "uint32_t a2", "uint32_t a3",
+              "uint64_t c01a", "uint64_t c23a", "uint32_t ma", "uint64_t c01b", "uint64_t c23b", "uint32_t mb",
+              "uint32_t& zmin"] + [f"uint32_t& {x}{h}" for x in accs for h in ("lo", "hi")]
+    lines.append(f"__device__ __forceinline__ void {name}(" + ", ".join(params) + ") {")
+    lines.append("  uint64_t k1a, k2a, k3a, k1b, k2b, k3b, swb;")
+    lines.append("  asm volatile(")
+    for asm, _, _ in seq:
+        lines.append(f'      "{asm}\\n\\t"')
+    outs = ['[s0a] "+v"(s0a)', '[s1a] "+v"(s1a)', '[s2a] "+v"(s2a)', '[s3a] "+v"(s3a)',
+            '[s0b] "+v"(s0b)', '[s1b] "+v"(s1b)', '[s2b] "+v"(s2b)', '[s3b] "+v"(s3b)', '[zmin] "+v"(zmin)']
+    outs += [f'[{x}{h}] "+v"({x}{h})' for x in accs for h in ("lo", "hi")]
+    outs += [f'[{k}] "=&s"({k})' for k in ("k1a", "k2a", "k3a", "k1b", "k2b", "k3b", "swb")]
+    ins = ['[a0] "v"(a0)', '[a1] "v"(a1)', '[a2] "v"(a2)', '[a3] "v"(a3)',
+           '[c01a] "s"(c01a)', '[c23a] "s"(c23a)', '[ma] "s"(ma)',
+           '[c01b] "s"(c01b)', '[c23b] "s"(c23b)', '[mb] "s"(mb)']
+    clob = ['"vcc"'] + [f'"v{i}"' for i in range(20)]
+    lines.append("      : " + ", ".join(outs))
+    lines.append("      : " + ", ".join(ins))
+    lines.append("      : " + ", ".join(clob) + ");")
+    lines.append("}")
+    return "\n".join(lines)
+
+
+def main():
+    print("// sa_draw2.h -- GENERATED by tools/gen_draw2.py; do not edit.")
+    print("// Two interleaved PCG64 draws per asm block (see the generator's docstring);")
+    print("// operand conventions as pcg_draw_pair / pcg_draw_one in sa_clients_impl.h.")
+    print("#pragma once")
+    print("#include <stdint.h>")
+    print()
+    print("namespace sa {")
+    print()
+    print(emit("pcg_draw2_pair", pair=True, same_acc=False))
+    print()
+    print(emit("pcg_draw2_one", pair=False, same_acc=False))
+    print()
+    print(emit("pcg_draw2_one_same", pair=False, same_acc=True))
+    print()
+    print("}  // namespace sa")
+
+
+if __name__ == "__main__":
+    main()
