@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round profile of the headline path (run on the GPU box from the repo root):
+#   1. bench.py (default workload) -> gpurun_out/bench.jsonl
+#   2. rocprofv3 --kernel-trace --stats of the same bench command
+#   3. PMC passes (one counter group per run): FETCH_SIZE, WRITE_SIZE, SQ census
+#      on tools/kernel_bench.py (8 clients x 100M on one GPU + the k_sum_u64
+#      calibration launch whose bytes are known)
+# Copy what should be judged into profiles/<round>/ afterwards.
+set -e
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python bench.py > gpurun_out/bench.jsonl 2> gpurun_out/bench.err
+tail -1 gpurun_out/bench.jsonl
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- \
+  python3 bench.py --steps 10 --warmup 2 --cpu-baseline-seconds 0 > gpurun_out/bench_prof.jsonl 2> gpurun_out/bench_prof.err
+tail -1 gpurun_out/bench_prof.jsonl
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
+  python3 tools/kernel_bench.py --shapes 8:1 --rounds 1 --reps 2 --calib 8 > gpurun_out/pmc_fetch.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- \
+  python3 tools/kernel_bench.py --shapes 8:1 --rounds 1 --reps 2 --calib 8 > gpurun_out/pmc_write.log 2>&1
+tools/pmc_sq.sh 8:1,8:8 > /dev/null
+echo PROFILE_OK

@@ -22,6 +22,11 @@
 
 using namespace sa;
 
+struct StreamLds {
+  uint64_t inc_lo, inc_hi, cj_lo, cj_hi, smask, pad;
+};
+typedef __attribute__((address_space(3))) const StreamLds* lds_ptr;
+
 // Same asm as pcg_draw_pair/one, but the stream constants are SGPR operands
 // (scalar-loaded) and the multiplier limbs VGPR operands (gfx9 constant bus: one
 // SGPR source per VOP3).
@@ -124,6 +129,86 @@ __global__ void __launch_bounds__(256) k_smem(uint64_t* out, int iters, uint32_t
   uint64_t acc = zmin;
 #pragma unroll
   for (int k = 0; k < E; k++)
+#pragma unroll
+    for (int c = 0; c < L; c++) acc += pack64(al[k][c], ah[k][c]);
+#pragma unroll
+  for (int j = 0; j < P; j++) acc ^= st[j][0] ^ st[j][3];
+  out[tid] = acc;
+}
+
+// dual-draw variant of k_smem (E = 2): the kernel's Sched grouping
+template <int L, int X>
+__global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t seed, const uint64_t* gconst) {
+  constexpr Sched<L, X> S{};
+  constexpr int P = Sched<L, X>::P;
+  extern __shared__ char dyn[];
+  if (dyn[0] == 123 && seed == 77) out[0] = 1;
+  uint32_t st[P][4];
+  const uint32_t tid = threadIdx.x + blockIdx.x * blockDim.x;
+#pragma unroll
+  for (int j = 0; j < P; j++) {
+    st[j][0] = tid * 0x9E3779B9u + j;
+    st[j][1] = seed ^ (j * 77u);
+    st[j][2] = tid + 13u * j;
+    st[j][3] = ~tid;
+  }
+  const uint32_t mk[4] = {vreg(A0 + seed), vreg(A1), vreg(A2), vreg(A3)};
+  uint32_t al[2][L], ah[2][L];
+#pragma unroll
+  for (int k = 0; k < 2; k++)
+#pragma unroll
+    for (int c = 0; c < L; c++) al[k][c] = ah[k][c] = c + k;
+  uint32_t zmin = 0xFFFFFFFFu;
+  cptr_t cp = (cptr_t)gconst;
+  for (int it = 0; it < iters; it++) {
+    uint64_t n01[2], n23[2], nm[2];
+    auto fetch = [&](int g) {
+      for (int h = 0; h < 2; h++) {
+        const int q = h == 0 ? S.g[g].qa : S.g[g].qb;
+        if (q < 0) continue;
+        cptr_t c = cp + 8 * q;
+        asm volatile("" : "+s"(c));
+        n01[h] = c[0];
+        n23[h] = c[1];
+        nm[h] = c[4];
+      }
+    };
+    fetch(0);
+#pragma unroll
+    for (int g = 0; g < S.n; g++) {
+      const Group G = S.g[g];
+      const uint64_t ca = n01[0], da = n23[0], cb = n01[1], db = n23[1];
+      const uint32_t ma = (uint32_t)nm[0], mb = (uint32_t)nm[1];
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        uint32_t* sa = st[G.qa];
+        if (G.qb < 0) {
+          if (G.va >= 0)
+            pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, ma, zmin, al[k][G.ua],
+                          ah[k][G.ua], al[k][G.va], ah[k][G.va]);
+          else
+            pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, ma, zmin, al[k][G.ua],
+                         ah[k][G.ua]);
+        } else {
+          uint32_t* sb = st[G.qb];
+          if (G.va >= 0)
+            pcg_draw2_pair(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca, da,
+                           ma, cb, db, mb, zmin, al[k][G.ua], ah[k][G.ua], al[k][G.va], ah[k][G.va], al[k][G.ub],
+                           ah[k][G.ub], al[k][G.vb], ah[k][G.vb]);
+          else if (G.ua == G.ub)
+            pcg_draw2_one_same(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca,
+                               da, ma, cb, db, mb, zmin, al[k][G.ua], ah[k][G.ua]);
+          else
+            pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca, da,
+                          ma, cb, db, mb, zmin, al[k][G.ua], ah[k][G.ua], al[k][G.ub], ah[k][G.ub]);
+        }
+        if (k == 0 && g + 1 < S.n) fetch(g + 1);
+      }
+    }
+  }
+  uint64_t acc = zmin;
+#pragma unroll
+  for (int k = 0; k < 2; k++)
 #pragma unroll
     for (int c = 0; c < L; c++) acc += pack64(al[k][c], ah[k][c]);
 #pragma unroll
@@ -254,6 +339,9 @@ int main() {
   if (run(k_draws<28, 8, true, 1>, 28, "pair28 L8 lds", 1000)) return 1;
   if (run(k_draws<28, 8, true, 0>, 28, "pair28 L8 reg", 1000)) return 1;
   const uint64_t* gc = gconst;
+  if (run(k_dual<1, 7>, 14, "dual one7 E2", 1000, gc)) return 1;
+  if (run(k_dual<8, 0>, 56, "dual pair28 E2", 250, gc)) return 1;
+  if (run(k_dual<4, 4>, 44, "dual 4+4x4 E2", 300, gc)) return 1;
   if (run(k_smem<7, 1, false, true, 4>, 28, "one7 L1 smem E4", 1000, gc)) return 1;
   if (run(k_smem<7, 1, false, true, 1>, 7, "one7 L1 smem E1", 4000, gc)) return 1;
   if (run(k_smem<7, 1, false, true, 2>, 14, "one7 L1 smem E2", 2000, gc)) return 1;
