@@ -193,6 +193,31 @@ def test_fused_clients_bit_exact(C, n):
     assert np.abs(ref - np.sum(np.stack(xs).astype(np.float64), axis=0)).max() < C * 2.0**-18
 
 
+@pytest.mark.parametrize("C", [4, 8])
+def test_fused_mixed_fast_and_exact_tiles(C):
+    """A few scattered values that leave the int32 conversion (|x*w*2^fxp| >=
+    2^31, +-inf, NaN) send their tiles down the exact int64 path while every
+    other tile of the launch takes the one-v_cvt fast path: both bit-exact."""
+    K = _K()
+    n = 300_007
+    names, xs, seeds, pg, ps = _fused_setup(C, n, 0, seed=C)
+    rng = np.random.default_rng(100 + C)
+    idx = rng.choice(n, 48, replace=False)
+    bad = np.array([3e9, -3e9, np.inf, -np.inf, np.nan, 8192.0, -8192.0, 8191.999], np.float32)
+    xs[1][idx] = bad[np.arange(idx.size) % bad.size]
+    masked = o.secure_masked(xs, names, seeds=seeds)
+    s = torch.empty(n, dtype=torch.int64, device=DEV)
+    dig = torch.zeros(C, dtype=torch.int64, device=DEV)
+    mo = [torch.empty(n, dtype=torch.int64, device=DEV) for _ in range(C)]
+    K.fused_clients([torch.from_numpy(x).to(DEV) for x in xs], [1.0] * C, pg, ps, [], 0, s, digests=dig,
+                    masked_outs=mo)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(s), o.server_sum(masked))
+    for c in range(C):
+        assert np.array_equal(_u64(mo[c]), masked[c]), c
+    assert [int(v) for v in _u64(dig)] == [o.digest(m) for m in masked]
+
+
 def test_fused_accumulate_and_weights():
     K = _K()
     C, n = 4, 3001
