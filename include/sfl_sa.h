@@ -139,6 +139,9 @@ int sa_mask(const void* x, int x_type, int compute_type, uint64_t n, double weig
  *   cross           n_clients * n_cross streams, client-major
  *   sum_out         n u64; accumulate != 0 means sum_out[i] += local sum
  *   digests         n_clients u64 (XOR-accumulated; zero them first)
+ * Shapes without a fused kernel (more than 8 clients, more than 32 streams,
+ * or an uninstantiated (C, n_cross)) return SA_ERR_UNSUPPORTED: the caller
+ * then masks client by client with sa_mask(..., sum_accum), same result.
  * Replaces: the client-side `mask` calls plus server `_sum`'s
  * np.sum(..., axis=0) for co-located parties. */
 int sa_fused_clients(const sa_local_client* clients, int n_clients, int x_type, uint64_t n,

@@ -220,10 +220,14 @@ extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, i
   if (check_type(x_type, "sa_fused_clients x_type")) return SA_ERR_ARG;
   const int L = n_clients;
   const int PI = L * (L - 1) / 2;
-  if (!clients || L < 1 || L > kMaxLocal || n_cross < 0 || !sum_out || fxp_bits < 0 ||
+  if (!clients || L < 1 || n_cross < 0 || !sum_out || fxp_bits < 0 ||
       fxp_bits > 62 || (PI > 0 && (!pair_gens || !pair_sign)) || (n_cross > 0 && !cross)) {
     sa_set_error("sa_fused_clients: bad arguments (n_clients=%d n_cross=%d)", L, n_cross);
     return SA_ERR_ARG;
+  }
+  if (L > kMaxLocal) {  // valid, but one launch holds at most kMaxLocal clients' accumulators
+    sa_set_error("sa_fused_clients: %d co-located clients exceed the %d per launch", L, kMaxLocal);
+    return SA_ERR_UNSUPPORTED;
   }
   if (PI + L * n_cross > kMaxStreams) {
     sa_set_error("sa_fused_clients: %d streams exceed the %d per launch", PI + L * n_cross,

@@ -399,6 +399,22 @@ def test_fused_fallback_for_uninstantiated_shape():
     assert [int(v) for v in _u64(dig)] == [o.digest(masked[c]) for c in plan.clients]
 
 
+def test_fused_more_than_8_clients_falls_back():
+    """12 clients on one GPU (config 5 run on one GPU is 32): more co-located
+    clients than one launch holds -> SA_ERR_UNSUPPORTED -> per-client masking
+    with accumulation, bit-identical to the oracle."""
+    K = _K()
+    C, n = 12, 4099
+    names, xs, seeds, pg, ps = _fused_setup(C, n, 9)
+    masked = o.secure_masked(xs, names, seeds=seeds, offset=9)
+    s = torch.empty(n, dtype=torch.int64, device=DEV)
+    dig = torch.zeros(C, dtype=torch.int64, device=DEV)
+    K.fused_clients([torch.from_numpy(x).to(DEV) for x in xs], [1.0] * C, pg, ps, [], 0, s, digests=dig)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(s), o.server_sum(masked))
+    assert [int(v) for v in _u64(dig)] == [o.digest(m) for m in masked]
+
+
 def test_chunked_launch_past_4gib():
     """Vectors longer than one launch's 32-bit buffer offsets (2^29 - 1024
     u64) are cut into chunks whose streams resume at the chunk offset: the
