@@ -24,14 +24,16 @@ Reference interfaces followed:
 Parties are ``PYU``s (``sfl_amd.device``); local training runs on
 ``train_device`` (the party's GPU by default, or the CPU).  Out of scope:
 the reference's dataset builders, callbacks, DP accountant hooks,
-compression strategies and the other strategies (fed_prox, scaffold, ...).
+compression strategies and the other strategies (fed_prox, scaffold, ...);
+``moon`` is mirrored because its reference test is the FL end-to-end the
+survey names for the aggregator swap.
 """
 
 from __future__ import annotations
 
+import copy
 import math
 import time
-from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
 
 import numpy as np
@@ -49,26 +51,30 @@ def optim_wrapper(func, *args, **kwargs):
     return make
 
 
-@dataclass
 class TorchModel:
-    """Model builder record (reference module.py:247)."""
+    """Model builder record (reference module.py:247): extra keyword
+    arguments go to ``model_fn`` (e.g. MOON's ``cosine_similarity_fn``,
+    tests/ml/nn/fl/strategy/test_moon_torch.py:76-91)."""
 
-    model_fn: Callable[[], torch.nn.Module]
-    loss_fn: Callable[[], torch.nn.Module]
-    optim_fn: Callable
-    metrics: list = field(default_factory=list)
+    def __init__(self, model_fn: Callable[..., torch.nn.Module] = None, loss_fn: Callable = None,
+                 optim_fn: Callable = None, metrics: Optional[list] = None, **kwargs):
+        self.model_fn = model_fn
+        self.loss_fn = loss_fn
+        self.optim_fn = optim_fn
+        self.metrics = list(metrics or [])
+        self.kwargs = kwargs
 
 
 class FedAvgW:
     """One party's worker for the ``fed_avg_w`` strategy."""
 
     def __init__(self, builder: TorchModel, device: PYU, random_seed: Optional[int] = None,
-                 train_device: Optional[torch.device] = None):
+                 train_device: Optional[torch.device] = None, **kwargs):
         if random_seed is not None:
             torch.manual_seed(random_seed)
         self.device = device
         self.exe_device = torch.device(train_device) if train_device is not None else device.torch_device
-        self.model = builder.model_fn().to(self.exe_device)
+        self.model = builder.model_fn(**builder.kwargs).to(self.exe_device)
         self.optimizer = builder.optim_fn(self.model.parameters())
         self.loss_fn = builder.loss_fn()
         self._x = self._y = None
@@ -101,14 +107,15 @@ class FedAvgW:
             return {k: v.cpu() for k, v in self.model.state_dict().items()}
         return [v.detach().cpu().numpy().copy() for v in self.model.state_dict().values()]
 
-    def set_weights(self, weights):
-        sd = self.model.state_dict()
+    def set_weights(self, weights, model: Optional[torch.nn.Module] = None):
+        model = self.model if model is None else model
+        sd = model.state_dict()
         new = {}
         for (k, v), w in zip(sd.items(), weights):
             w = w.detach().cpu().numpy() if isinstance(w, torch.Tensor) else np.asarray(w)
             # reference: torch.Tensor(np.copy(v)) -> float32 for float params
             new[k] = torch.from_numpy(np.array(w, copy=True)).to(dtype=v.dtype)
-        self.model.load_state_dict(new)
+        model.load_state_dict(new)
 
     # ------------------------------------------------------- training
     def train_step(self, weights, cur_steps: int, train_steps: int, refresh_data: bool = False,
@@ -147,8 +154,76 @@ class FedAvgW:
         acc = float((out.argmax(1) == yt).float().mean().item())
         return loss, acc
 
+    @torch.no_grad()
+    def predict(self, x, batch_size: int = 32):
+        self.model.eval()
+        xt = torch.as_tensor(np.asarray(x, dtype=np.float32))
+        outs = [self.model(xt[i:i + batch_size].to(self.exe_device)).cpu() for i in range(0, len(xt), batch_size)]
+        return torch.cat(outs).numpy() if outs else np.zeros((0,), np.float32)
 
-_STRATEGIES = {("fed_avg_w", "torch"): FedAvgW}
+
+class MOON(FedAvgW):
+    """One party's worker for the ``moon`` strategy (model-contrastive FL,
+    sfl/ml/nn/fl/backend/torch/strategy/moon.py:27-139): local loss = task
+    loss + mu * CE(cos(z, z_global) / T against cos(z, z_prev) / T) with the
+    model's projection ``z`` (``model(x, return_all=True)`` -> (h, z, y)),
+    the aggregated global model and the last ``model_buffer_size`` local
+    models.  The aggregation itself is fed_avg_w's: ``average(weights,
+    weights=num_samples)`` -- the secure aggregator's caller is unchanged."""
+
+    def __init__(self, builder: TorchModel, device: PYU, random_seed: Optional[int] = None,
+                 train_device: Optional[torch.device] = None, model_buffer_size: int = 1, **kwargs):
+        super().__init__(builder, device, random_seed, train_device)
+        self.model_buffer_size = int(model_buffer_size)
+        self.prev_model_list: List[torch.nn.Module] = []
+        self.global_model = copy.deepcopy(self.model)
+
+    def train_step(self, weights, cur_steps: int, train_steps: int, refresh_data: bool = False,
+                   dp_strategy=None, **kwargs):
+        self.model.train()
+        if refresh_data:
+            self._reset_data_iter()
+        if weights is not None:  # moon.py:64-72: global model <- aggregated weights, frozen
+            self.set_weights(weights, model=self.global_model)
+            self.global_model.eval()
+            for prm in self.global_model.parameters():
+                prm.requires_grad = False
+            self.set_weights(weights)
+        num_sample = 0
+        loss = None
+        for _ in range(train_steps):  # moon.py:76-97
+            x, y = self.next_batch()
+            num_sample += x.shape[0]
+            self.optimizer.zero_grad()
+            _, pro1, y_pred = self.model(x, return_all=True)
+            loss = self.loss_fn(y_pred, y)
+            _, pro2, _ = self.global_model(x, return_all=True)
+            logits = self.model.cosine_similarity_fn(pro1, pro2).reshape(-1, 1)
+            for pre in self.prev_model_list:
+                _, pro3, _ = pre(x, return_all=True)
+                nega = self.model.cosine_similarity_fn(pro1, pro3)
+                logits = torch.cat((logits, nega.reshape(-1, 1)), dim=1)
+            logits = logits / self.model.temperature
+            labels = torch.zeros(x.size(0), dtype=torch.long, device=x.device)
+            loss = loss + self.model.mu * self.loss_fn(logits, labels)
+            loss.backward()
+            self.optimizer.step()
+        self.last_loss = float(loss.item()) if loss is not None else float("nan")
+        model_weights = self.get_weights(return_numpy=True)
+        if dp_strategy is not None and dp_strategy.model_gdp is not None:
+            model_weights = dp_strategy.model_gdp(model_weights)
+        # moon.py:115-130: keep the last model_buffer_size local models, frozen
+        if len(self.prev_model_list) >= self.model_buffer_size:
+            self.prev_model_list.pop(0)
+        hist = copy.deepcopy(self.model)
+        hist.eval()
+        for prm in hist.parameters():
+            prm.requires_grad = False
+        self.prev_model_list.append(hist)
+        return model_weights, num_sample
+
+
+_STRATEGIES = {("fed_avg_w", "torch"): FedAvgW, ("moon", "torch"): MOON}
 
 
 class FLModel:
@@ -168,7 +243,8 @@ class FLModel:
         self.strategy = strategy
         self.dp_strategy = dp_strategy
         self._workers: Dict[PYU, FedAvgW] = {
-            d: _STRATEGIES[(strategy, backend)](model, d, random_seed, train_device) for d in self.device_list}
+            d: _STRATEGIES[(strategy, backend)](model, d, random_seed, train_device, **kwargs)
+            for d in self.device_list}
 
     def initialize_weights(self):
         """Average the clients' initial weights and install them everywhere
@@ -225,6 +301,11 @@ class FLModel:
         aggregated weights, so the first worker evaluates."""
         w = next(iter(self._workers.values()))
         return w.evaluate(x, y)
+
+    def predict(self, x: Dict[PYU, np.ndarray], batch_size: int = 32) -> Dict[PYU, PYUObject]:
+        """Every party's predictions on its own data (reference fl_model.py
+        ``predict``: a dict device -> PYUObject)."""
+        return {d: PYUObject(d, self._workers[d].predict(x[d], batch_size)) for d in self.device_list}
 
     def get_weights(self, device: Optional[PYU] = None):
         d = device or self.device_list[0]
