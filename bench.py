@@ -111,7 +111,7 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0, help="0 disables")
     ap.add_argument("--extra", action="store_true", help="also time the wire chain and H2D/D2H-inclusive rate")
     ap.add_argument("--chunks", type=int, default=None,
-                    help="N>1: masking/reduce pipeline depth (default 4; 1 = reduce after the whole launch)")
+                    help="N>1: masking/reduce pipeline depth (default 8; 1 = reduce after the whole launch)")
     args = ap.parse_args()
 
     import torch
@@ -143,7 +143,7 @@ def main():
         g = torch.Generator(device=dev).manual_seed(20260116 + c)
         xs.append(torch.randn(N, generator=g, device=dev, dtype=torch.float32) * 1e-2)
     total_steps = args.warmup + args.steps
-    chunks = args.chunks if args.chunks is not None else (4 if world > 1 else 1)
+    chunks = args.chunks if args.chunks is not None else (8 if world > 1 else 1)
     pipe = PipelinedMaskedSum(comm, dev, N, chunks)
     # every step is a new round: streams start i*N draws in, chunk j at +lo_j
     gens = [[plan_generators(plan, pair_seed, offset=i * N + lo) for lo, _ in pipe.bounds]
