@@ -216,6 +216,69 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
   out[tid] = acc;
 }
 
+// Throughput of the draw's instruction MIX with no dependencies between
+// instructions of one iteration: 6 v_mad_u64_u32 + 4 v_mul_lo_u32 + 22 simple
+// ops (adds / bitop3 / alignbit / cndmask-like) per "draw" -- the issue
+// ceiling the real dependency chains are measured against.
+__global__ void __launch_bounds__(256) k_mix(uint64_t* out, int iters, uint32_t seed) {
+  extern __shared__ char dyn[];
+  if (dyn[0] == 123 && seed == 77) out[0] = 1;
+  const uint32_t t = threadIdx.x + blockIdx.x * blockDim.x;
+  uint64_t m[6];
+  uint32_t l[4], r[22];
+  uint32_t b = t * 3 + seed, c = t ^ 0x55;
+  for (int j = 0; j < 6; j++) m[j] = t + j;
+  for (int j = 0; j < 4; j++) l[j] = t * 7 + j;
+  for (int j = 0; j < 22; j++) r[j] = t + 11 * j;
+  for (int it = 0; it < iters; it++) {
+    asm volatile(
+        "v_mad_u64_u32 %0, s[40:41], %10, %11, %0\n\t"
+        "v_add_u32 %12, %12, %11\n\t"
+        "v_mad_u64_u32 %1, s[42:43], %10, %11, %1\n\t"
+        "v_bitop3_b32 %13, %13, %10, %11 bitop3:0x96\n\t"
+        "v_mad_u64_u32 %2, s[44:45], %10, %11, %2\n\t"
+        "v_add_u32 %14, %14, %11\n\t"
+        "v_mul_lo_u32 %6, %6, %11\n\t"
+        "v_alignbit_b32 %15, %15, %10, %11\n\t"
+        "v_mad_u64_u32 %3, s[46:47], %10, %11, %3\n\t"
+        "v_add_u32 %16, %16, %11\n\t"
+        "v_mul_lo_u32 %7, %7, %11\n\t"
+        "v_bitop3_b32 %17, %17, %10, %11 bitop3:0x96\n\t"
+        "v_mad_u64_u32 %4, s[48:49], %10, %11, %4\n\t"
+        "v_add_u32 %18, %18, %11\n\t"
+        "v_mul_lo_u32 %8, %8, %11\n\t"
+        "v_alignbit_b32 %19, %19, %10, %11\n\t"
+        "v_mad_u64_u32 %5, s[50:51], %10, %11, %5\n\t"
+        "v_add_u32 %20, %20, %11\n\t"
+        "v_mul_lo_u32 %9, %9, %11\n\t"
+        "v_bitop3_b32 %21, %21, %10, %11 bitop3:0x96\n\t"
+        "v_add_u32 %22, %22, %11\n\t"
+        "v_add_u32 %23, %23, %11\n\t"
+        "v_bitop3_b32 %24, %24, %10, %11 bitop3:0x96\n\t"
+        "v_add_u32 %25, %25, %11\n\t"
+        "v_alignbit_b32 %26, %26, %10, %11\n\t"
+        "v_add_u32 %27, %27, %11\n\t"
+        "v_add_u32 %28, %28, %11\n\t"
+        "v_bitop3_b32 %29, %29, %10, %11 bitop3:0x96\n\t"
+        "v_add_u32 %30, %30, %11\n\t"
+        "v_add_u32 %31, %31, %11\n\t"
+        "v_add_u32 %32, %32, %11\n\t"
+        "v_add_u32 %33, %33, %11"
+        : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]), "+v"(m[3]), "+v"(m[4]), "+v"(m[5]), "+v"(l[0]), "+v"(l[1]),
+          "+v"(l[2]), "+v"(l[3]), "+v"(b), "+v"(c), "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]),
+          "+v"(r[5]), "+v"(r[6]), "+v"(r[7]), "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), "+v"(r[12]),
+          "+v"(r[13]), "+v"(r[14]), "+v"(r[15]), "+v"(r[16]), "+v"(r[17]), "+v"(r[18]), "+v"(r[19]),
+          "+v"(r[20]), "+v"(r[21])
+        :
+        : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51");
+  }
+  uint64_t acc = 0;
+  for (int j = 0; j < 6; j++) acc += m[j];
+  for (int j = 0; j < 4; j++) acc += l[j];
+  for (int j = 0; j < 22; j++) acc ^= r[j];
+  out[t] = acc;
+}
+
 // MODE 0: constants in VGPRs (loaded once);  MODE 1: constants from LDS per draw
 // (the product kernel's scheme).  PAIRS: internal pair draws into L accumulators.
 template <int P, int L, bool PAIRS, int MODE>
@@ -339,6 +402,7 @@ int main() {
   if (run(k_draws<28, 8, true, 1>, 28, "pair28 L8 lds", 1000)) return 1;
   if (run(k_draws<28, 8, true, 0>, 28, "pair28 L8 reg", 1000)) return 1;
   const uint64_t* gc = gconst;
+  if (run(k_mix, 1, "mix 10mul+22simple", 20000)) return 1;
   if (run(k_dual<1, 7>, 14, "dual one7 E2", 1000, gc)) return 1;
   if (run(k_dual<8, 0>, 56, "dual pair28 E2", 250, gc)) return 1;
   if (run(k_dual<4, 4>, 44, "dual 4+4x4 E2", 300, gc)) return 1;
