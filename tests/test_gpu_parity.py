@@ -317,7 +317,7 @@ def test_prg_zero_draw_is_flagged():
 # full-size properties (BASELINE configs): too big for the oracle, so check
 # mask cancellation, fused == per-client (wire) path, and oracle spot checks
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("C,n", [(4, 10_000_000), (8, 20_000_000)])
+@pytest.mark.parametrize("C,n", [(4, 10_000_000), (8, 20_000_000), (8, 100_000_000)])
 def test_full_size_properties(C, n):
     K, L = _K(), _L()
     names = [f"client{c}" for c in range(C)]
