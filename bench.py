@@ -110,6 +110,9 @@ def main():
     ap.add_argument("--fxp-bits", type=int, default=18)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0, help="0 disables")
     ap.add_argument("--extra", action="store_true", help="also time the wire chain and H2D/D2H-inclusive rate")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the multi-GPU code path (RCCL communicator, pipelined reduce) even at N=1 "
+                         "(rehearsal of the N>1 path on one GPU under torchrun)")
     ap.add_argument("--chunks", type=int, default=None,
                     help="N>1: masking/reduce pipeline depth (default 8; 1 = reduce after the whole launch)")
     args = ap.parse_args()
@@ -130,7 +133,8 @@ def main():
     dev = torch.device("cuda", local_rank)
     _lib.lib()
     comm = None
-    if world > 1:
+    multi = world > 1 or args.dist
+    if multi:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         comm = RcclComm(rank, world, local_rank)
 
@@ -143,13 +147,13 @@ def main():
         g = torch.Generator(device=dev).manual_seed(20260116 + c)
         xs.append(torch.randn(N, generator=g, device=dev, dtype=torch.float32) * 1e-2)
     total_steps = args.warmup + args.steps
-    chunks = args.chunks if args.chunks is not None else (8 if world > 1 else 1)
+    chunks = args.chunks if args.chunks is not None else (8 if multi else 1)
     pipe = PipelinedMaskedSum(comm, dev, N, chunks)
     # every step is a new round: streams start i*N draws in, chunk j at +lo_j
     gens = [[plan_generators(plan, pair_seed, offset=i * N + lo) for lo, _ in pipe.bounds]
             for i in range(total_steps)]
     sum_buf = torch.empty(N, dtype=torch.int64, device=dev)
-    recv = torch.empty(N, dtype=torch.int64, device=dev) if (rank == 0 and world > 1) else None
+    recv = torch.empty(N, dtype=torch.int64, device=dev) if (rank == 0 and multi) else None
     digests = torch.zeros(Lc, dtype=torch.int64, device=dev)
     flags = torch.zeros(1, dtype=torch.int32, device=dev)
     kev = []  # (start, end) events around every masking launch of the timed steps (compute stream)
@@ -161,19 +165,19 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, i)
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in kev) / args.steps  # masking kernel time per step
-    if world > 1:
+    if multi:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
