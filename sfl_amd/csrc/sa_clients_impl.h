@@ -12,15 +12,17 @@
 // invertible: A^J is odd), so every tile, the first included, runs the same
 // straight-line code.
 //
-// Loop order inside a tile is stream-outer: for stream q the lane draws both
-// of its elements back to back, so q's constants (inc, inc*G_J, sign mask)
-// are needed for two draws only.  They are scalar-loaded from the kernarg
-// segment into SGPRs, stream q+1's load issued after q's first draw (latency
-// hidden under one draw; SMEM returns out of order, so the wait is lgkmcnt(0)
-// right before q+1 starts).  No VGPRs or LDS traffic go to constants; the
-// multiplier limbs (A, A^J) sit in 8 wave-uniform VGPRs.  Measured on the
-// draw alone (tools/microbench/draw_issue.hip): LDS-resident constants issue
-// 10-15 % slower than SGPR ones.
+// Loop order inside a tile is stream-outer: streams are taken in groups of
+// two (Sched: two streams whose accumulators are disjoint, drawn by one
+// interleaved asm block from sa_draw2.h) and the lane draws both of its
+// elements for a group back to back, so a group's constants (inc, inc*G_J,
+// sign mask) serve two draws per stream.  They are scalar-loaded from the
+// kernarg segment into SGPRs, group g+1's loads issued after group g's first
+// draw (latency hidden under one draw; SMEM returns out of order, so the
+// wait is lgkmcnt(0) right before g+1 starts).  No VGPRs or LDS traffic go
+// to constants; the multiplier limbs (A, A^J) sit in 8 wave-uniform VGPRs.
+// Measured on the draw alone (tools/microbench/draw_issue.hip): LDS-resident
+// constants issue 10-15 % slower than SGPR ones.
 //
 // Sign handling without branches.  A client adds m = raw + K (K = 2^63-1,
 // numpy's Lemire offset) for a peer that sorts after it and subtracts it
