@@ -90,6 +90,7 @@ constexpr LaneTable make_lane_table() {
 static __constant__ LaneTable kLaneJump = make_lane_table();
 static_assert((kTile & (kTile - 1)) == 0, "kTile is a power of two");
 constexpr int kTileLog2 = __builtin_ctz(kTile);
+constexpr int kGridBits = 12;  // grids are < 2^12 blocks (launch_clients checks)
 
 // ----------------------------------------------------------------------------
 // element loads / quantize
@@ -442,10 +443,17 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
   uint32_t st[P > 0 ? P : 1][4];  // 128-bit states as 32-bit limbs
   if constexpr (P > 0) {
     // J(first + 1) = J(blockIdx * kTile) o J(lane * kE + 1)
+    // Block part: a fixed, fully unrolled bit loop (grids stay below 2^12
+    // blocks: 8 waves/SIMD x 256 CUs / 4 waves per block = 512... 2048), so
+    // the table loads are issued together instead of one dependent scalar
+    // load per set bit.
+    static_assert(kTileLog2 + kGridBits <= 64, "power table");
     Jump jb{1, 0};
     const uint32_t bid = (SA_ABLATE & 64) ? 0u : blockIdx.x;
-    for (int b = 0; (bid >> b) != 0; b++) {  // wave-uniform
-      if ((bid >> b) & 1) jb = compose(jb, kPowTable.e[kTileLog2 + b]);
+#pragma unroll
+    for (int b = 0; b < kGridBits; b++) {  // wave-uniform
+      const Jump e = kPowTable.e[kTileLog2 + b];
+      if ((bid >> b) & 1) jb = compose(jb, e);
     }
     const Jump jl = compose(kLaneJump.e[threadIdx.x], jb);
     const u128 aji = ld128(a.aji_lo, a.aji_hi);
@@ -713,6 +721,10 @@ int launch_clients(const KArgs& in, void* stream) {
     }
     const uint64_t tiles = (a.n + kTile - 1) / kTile;
     const int grid = (int)(tiles < (uint64_t)maxb ? tiles : (uint64_t)maxb);
+    if (grid >= (1 << kGridBits)) {
+      sa_set_error("masking kernel: grid of %d blocks exceeds the prologue's %d-bit block jump", grid, kGridBits);
+      return SA_ERR_UNSUPPORTED;
+    }
     // merged tile jump: S_{i+kE} -> S_{i+stride+1}, i.e. stride - kE + 1 draws
     const Jump jj = jump_of((uint64_t)grid * kTile - (kE - 1));
     a.aj_lo = lo64(jj.mult);
