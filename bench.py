@@ -79,7 +79,7 @@ PMC_DIR = os.path.join(ROOT, "profiles", "r01")
 
 def pmc_traffic(kernel: str) -> dict | None:
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (tools/gpu_r01_profile.sh: separate FETCH_SIZE / WRITE_SIZE runs of
+    (tools/gpu_profile.sh: separate FETCH_SIZE / WRITE_SIZE runs of
     tools/kernel_bench.py on this workload).  Units are KiB; gfx950 reports
     FETCH_SIZE at half the bytes of 16-B/lane streaming reads, so it is
     doubled (MI355X_MICROARCH.md, HBM); both corrections were checked on the
