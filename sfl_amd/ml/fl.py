@@ -26,7 +26,9 @@ Parties are ``PYU``s (``sfl_amd.device``); local training runs on
 the reference's dataset builders, callbacks, DP accountant hooks,
 compression strategies and the other strategies (fed_prox, scaffold, ...);
 ``moon`` is mirrored because its reference test is the FL end-to-end the
-survey names for the aggregator swap.
+survey names for the aggregator swap, ``fed_avg_u``
+and ``fed_avg_g`` because they are the other payload producers of §8(a8)
+(model updates and gradients instead of weights).
 """
 
 from __future__ import annotations
@@ -223,7 +225,88 @@ class MOON(FedAvgW):
         return model_weights, num_sample
 
 
-_STRATEGIES = {("fed_avg_w", "torch"): FedAvgW, ("moon", "torch"): MOON}
+class FedAvgU(FedAvgW):
+    """``fed_avg_u`` worker (sfl/ml/nn/fl/backend/torch/strategy/fed_avg_u.py:
+    30-96): clients upload their model UPDATES (new - old weights) and apply
+    the aggregated update.  The aggregator sees small signed deltas."""
+
+    def train_step(self, updates, cur_steps: int, train_steps: int, refresh_data: bool = False,
+                   dp_strategy=None, **kwargs):
+        self.model.train()
+        if refresh_data:
+            self._reset_data_iter()
+        if updates is not None:  # fed_avg_u.py:55-57
+            self.set_weights([np.add(w, u) for w, u in zip(self.get_weights(), updates)])
+        old = self.get_weights()
+        num_sample = 0
+        loss = None
+        for _ in range(train_steps):
+            x, y = self.next_batch()
+            num_sample += x.shape[0]
+            self.optimizer.zero_grad()
+            loss = self.loss_fn(self.model(x), y)
+            loss.backward()
+            self.optimizer.step()
+        self.last_loss = float(loss.item()) if loss is not None else float("nan")
+        client_updates = [np.subtract(n, o) for n, o in zip(self.get_weights(), old)]  # :77-80
+        if dp_strategy is not None and dp_strategy.model_gdp is not None:
+            client_updates = dp_strategy.model_gdp(client_updates)
+        return client_updates, num_sample
+
+    def apply_weights(self, updates, **kwargs):
+        if updates is not None:
+            self.set_weights([np.add(w, u) for w, u in zip(self.get_weights(), updates)])
+
+
+class FedAvgG(FedAvgW):
+    """``fed_avg_g`` worker (sfl/ml/nn/fl/backend/torch/strategy/fed_avg_g.py:
+    28-112): clients upload the gradients accumulated over the round and step
+    their optimizer with the aggregated gradients.  Two deviations, both
+    about the reference's plumbing rather than the aggregation: the
+    reference's ``local_gradients_sum += local_gradients`` (:91) concatenates
+    the Python lists, so here the per-step gradients are summed element-wise
+    (identical for ``train_steps == 1``, i.e. ``aggregate_freq=1``); and the
+    aggregate (float64 out of the secure decode) is cast to each parameter's
+    dtype before it becomes ``p.grad`` (mixins.py:99-111 assigns it as is)."""
+
+    def _set_gradients(self, gradients):
+        for g, prm in zip(gradients, self.model.parameters()):
+            if g is not None:
+                prm.grad = torch.from_numpy(np.array(g, copy=True)).to(device=prm.device, dtype=prm.dtype)
+
+    def train_step(self, gradients, cur_steps: int, train_steps: int, refresh_data: bool = False,
+                   dp_strategy=None, **kwargs):
+        self.model.train()
+        if refresh_data:
+            self._reset_data_iter()
+        if gradients is not None:  # fed_avg_g.py:67-71
+            self._set_gradients(gradients)
+            self.optimizer.step()
+        num_sample = 0
+        loss = None
+        grad_sum = None
+        for _ in range(train_steps):
+            self.optimizer.zero_grad()
+            x, y = self.next_batch()
+            num_sample += x.shape[0]
+            loss = self.loss_fn(self.model(x), y)
+            loss.backward()
+            grads = [None if prm.grad is None else prm.grad.detach().cpu().numpy().copy()
+                     for prm in self.model.parameters()]  # mixins.py:91-97
+            grad_sum = grads if grad_sum is None else [a + b for a, b in zip(grad_sum, grads)]
+        self.last_loss = float(loss.item()) if loss is not None else float("nan")
+        if dp_strategy is not None and dp_strategy.model_gdp is not None:
+            grad_sum = dp_strategy.model_gdp(grad_sum)
+        return grad_sum, num_sample
+
+    def apply_weights(self, gradients, **kwargs):
+        if gradients is not None:  # fed_avg_g.py:103-112
+            self._set_gradients(gradients)
+            self.optimizer.step()
+
+
+_STRATEGIES = {("fed_avg_w", "torch"): FedAvgW, ("fed_avg_u", "torch"): FedAvgU, ("fed_avg_g", "torch"): FedAvgG,
+               ("moon", "torch"): MOON}
 
 
 class FLModel:
