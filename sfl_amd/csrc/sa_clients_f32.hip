@@ -27,3 +27,17 @@ LaunchFn find_clients_kernel(int xt, int ct, int L, int X) {
 #undef F32
 
 }  // namespace sa
+
+#ifdef SA_TIMING
+// Tuning-only: the wave timeline of the last fp32 masking launch (this TU's
+// kernels), kTsWaves x kTsWords u64, zeroed by reset.
+extern "C" int sa_debug_timeline(uint64_t* host_out, int reset) {
+  using sa::g_sa_ts;
+  const size_t bytes = sizeof(g_sa_ts);
+  if (reset) {
+    static uint64_t zeros[sa::kTsWaves][sa::kTsWords];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_sa_ts), zeros, bytes) == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_sa_ts), bytes) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -56,6 +56,25 @@ namespace sa {
 #define SA_ABLATE 0
 #endif
 
+// Tuning-only wave timeline (make VARIANT=_ts EXTRA=-DSA_TIMING; results stay
+// correct): lane 0 of every wave records s_memrealtime (100 MHz) at entry,
+// after the prologue, after its first tile and after its last tile, the end,
+// its tile count and HW_ID / XCC_ID, read back by sa_debug_timeline
+// (sa_clients_f32.hip, tools/wave_timeline.py).
+// Issue-priority rotation (see the tile loop): windows of 2^SA_PRIO ticks of
+// the 100 MHz clock (14: 164 us); 0 = off.
+#ifndef SA_PRIO
+#define SA_PRIO 14
+#endif
+
+#ifdef SA_TIMING
+constexpr int kTsWaves = 16384, kTsWords = 8;
+static __device__ uint64_t g_sa_ts[kTsWaves][kTsWords];
+#define SA_TS(v) (v) = __builtin_amdgcn_s_memrealtime()
+#else
+#define SA_TS(v) (void)0
+#endif
+
 constexpr int kE = 2;                       // elements per lane per tile
 constexpr int kTile = kBlockThreads * kE;   // elements per workgroup tile (512)
 
@@ -437,6 +456,11 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
 
   const uint64_t n = a.n;
   const uint64_t stride = (uint64_t)gridDim.x * kTile;
+#ifdef SA_TIMING
+  uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0;
+  uint32_t tiles = 0;
+#endif
+  SA_TS(ts0);
 
   // ---- prologue: park every stream one tile jump before S_{first+1}, the
   // state element `first` is drawn from: V = A^-J (S_{first+1} - inc*G_J)
@@ -480,6 +504,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
   }
 
   uint32_t zmin = 0xFFFFFFFFu;  // 0 iff some raw PCG64 draw of this lane was 0
+  SA_TS(ts1);
 
   // per-lane XOR digests of the clients' masked values: VGPRs, or for the
   // register-bound shapes (5+ co-located clients) lane-private LDS slots
@@ -503,8 +528,25 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
   // wave-uniform trip count: every lane of a wave runs the wave's last tile
   // (out-of-range elements are masked at load/store)
   const uint64_t wave_off = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * 64 * kE);
+  // Two waves share a SIMD and its VALU issue is arbitrated by priority, then
+  // age: at equal priority the older wave runs ~1.6x faster, ends ~40% early
+  // and the younger then runs the rest alone, which issues fewer VALU per
+  // cycle than two waves do (tools/wave_timeline.py: per-wave tile time
+  // 5.2 vs 8.7 us, the last waves end at 1.7x the first).  Rotating priority
+  // 1 between the wave slots in fixed clock windows makes the pair progress
+  // equally and end together: 8 clients x 100M, 2.77 -> 2.49 ms.
+#if SA_PRIO
+  uint32_t slot;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID, 0, 1)" : "=s"(slot));
+#endif
   for (uint64_t base = (uint64_t)blockIdx.x * kTile; base + wave_off < n; base += stride) {
     const uint64_t i = base + (uint64_t)threadIdx.x * kE;
+#if SA_PRIO
+    if ((((uint32_t)__builtin_amdgcn_s_memrealtime() >> SA_PRIO) ^ slot) & 1)
+      __builtin_amdgcn_s_setprio(1);
+    else
+      __builtin_amdgcn_s_setprio(0);
+#endif
 
     // ---- issue this tile's loads first; consumed after the mask expansion.
     // Unconditional: an absent vector has a 0-byte descriptor (reads 0).
@@ -657,7 +699,11 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
       }
       bstore2_u64(rs, i, sum[0], sum[1]);
     }
+#ifdef SA_TIMING
+    if (tiles++ == 0) SA_TS(ts2);
+#endif
   }
+  SA_TS(ts3);
 
   // ---- digests: wave XOR reduction (shuffles), then the block's 4 waves
   // through LDS, one 64-bit atomic per client per BLOCK.  Every wave ends at
@@ -682,6 +728,18 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
   }
   if (a.flags && !(SA_ABLATE & 1) && __any(zmin == 0) && (threadIdx.x & 63) == 0)
     atomicOr(a.flags, SA_FLAG_PRG_REJECT);
+#ifdef SA_TIMING
+  SA_TS(ts4);
+  const uint32_t wid = blockIdx.x * (kBlockThreads / 64) + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && wid < kTsWaves) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint64_t* o = g_sa_ts[wid];
+    o[0] = ts0; o[1] = ts1; o[2] = ts2; o[3] = ts3; o[4] = ts4;
+    o[5] = tiles; o[6] = hw; o[7] = xcc;
+  }
+#endif
 }
 
 // ----------------------------------------------------------------------------

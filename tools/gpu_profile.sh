@@ -12,7 +12,7 @@ mkdir -p gpurun_out
 timeout -k 10 300 python bench.py > gpurun_out/bench.jsonl 2> gpurun_out/bench.err
 tail -1 gpurun_out/bench.jsonl
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- \
-  python3 bench.py --steps 10 --warmup 2 --cpu-baseline-seconds 0 > gpurun_out/bench_prof.jsonl 2> gpurun_out/bench_prof.err
+  python3 bench.py --cpu-baseline-seconds 0 > gpurun_out/bench_prof.jsonl 2> gpurun_out/bench_prof.err
 tail -1 gpurun_out/bench_prof.jsonl
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
   python3 tools/kernel_bench.py --shapes 8:1 --rounds 1 --reps 2 --calib 8 > gpurun_out/pmc_fetch.log 2>&1
