@@ -272,11 +272,11 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
 //   joined by carry adds whose carry-ins are the mads' own carry-outs -- 6
 //   mads + 4 mul_lo + 8 adds, no register shuffling.  Then t = rotr(hi^lo^m,
 //   hi>>58) in 32-bit halves (v_bitop3 + v_alignbit + swap), the raw==0 test
-//   (hi == lo <=> xl == xh == m) folded into a running minimum, and
-//   acc_u += t (and acc_v -= t for an internal pair) on 32-bit halves.
+//   (hi == lo <=> xl == xh == m) folded into a running minimum, and the
+//   accumulation (below).
 //
-// Carries live in three SGPR pairs, reused as they die (k1: kE then the acc_u
-// carry; k2: kO, c2, then the acc_v carry; k3: discarded carry-outs, c1, c3).
+// Carries live in three SGPR pairs, reused as they die (k1: kE; k2: kO, c2,
+// then the acc_v borrow; k3: discarded carry-outs, c1, c3).
 // Every VALU-written SGPR (carries, VCC) is read >= 2 instructions later
 // (gfx950 VALU-SGPR-write -> VALU-read hazard).  v0-v9 are fixed scratch (low
 // registers, so the kernel's VGPR budget is not raised).
@@ -307,12 +307,11 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
   "v_alignbit_b32 v4, v1, v0, v2\n\t"                                                    \
   "v_alignbit_b32 v5, v0, v1, v2\n\t"                                                    \
   "v_min_u32_e32 %[zmin], %[zmin], v3\n\t"                                               \
-  "v_cndmask_b32_e32 v6, v4, v5, vcc\n\t"                   /* t lo */                   \
-  "v_add_co_u32_e64 %[ulo], %[k1], %[ulo], v6\n\t"
+  "v_cndmask_b32_e32 v6, v4, v5, vcc\n\t"                   /* t lo */
 
 #define SA_PCG_DRAW_OUTS                                                                 \
   [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [zmin] "+v"(zmin),          \
-      [ulo] "+v"(ulo), [uhi] "+v"(uhi), [k1] "=&s"(k1), [k2] "=&s"(k2), [k3] "=&s"(k3)
+      [u] "+v"(u), [k1] "=&s"(k1), [k2] "=&s"(k2), [k3] "=&s"(k3)
 // Operand classes: the multiplier limbs are wave-uniform VGPRs (set once per
 // launch), the stream constants SGPRs (scalar-loaded per stream and tile), so
 // every VOP3 reads at most one SGPR (the gfx9 constant-bus limit).
@@ -322,28 +321,44 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
 #define SA_PCG_DRAW_CLOBBERS \
   "vcc", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9"
 
+// acc_u += t with one v_lshl_add_u64 on the 64-bit accumulator (the issue cost
+// of one v_add_co, tools/microbench/op_rate.hip); the internal pair's second
+// client subtracts on 32-bit halves (pcg_draw_pair) or, when the kernel keeps
+// that client negated, also adds (pcg_draw_pair_a).
 __device__ __forceinline__ void pcg_draw_pair(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
                                               uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
-                                              uint32_t m, uint32_t& zmin, uint32_t& ulo, uint32_t& uhi,
-                                              uint32_t& vlo, uint32_t& vhi) {
+                                              uint32_t m, uint32_t& zmin, uint64_t& u, uint64_t& v) {
   uint64_t k1, k2, k3;
+  uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
   asm volatile(SA_PCG_DRAW_ASM
                "v_sub_co_u32_e64 %[vlo], %[k2], %[vlo], v6\n\t"
                "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"  // t hi
-               "v_addc_co_u32_e64 %[uhi], %[k1], %[uhi], v7, %[k1]\n\t"
+               "v_lshl_add_u64 %[u], v[6:7], 0, %[u]\n\t"
                "v_subb_co_u32_e64 %[vhi], %[k2], %[vhi], v7, %[k2]"
                : SA_PCG_DRAW_OUTS, [vlo] "+v"(vlo), [vhi] "+v"(vhi)
+               : SA_PCG_DRAW_INS
+               : SA_PCG_DRAW_CLOBBERS);
+  v = ((uint64_t)vhi << 32) | vlo;
+}
+__device__ __forceinline__ void pcg_draw_pair_a(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
+                                                uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
+                                                uint32_t m, uint32_t& zmin, uint64_t& u, uint64_t& v) {
+  uint64_t k1, k2, k3;
+  asm volatile(SA_PCG_DRAW_ASM
+               "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"  // t hi
+               "v_lshl_add_u64 %[u], v[6:7], 0, %[u]\n\t"
+               "v_lshl_add_u64 %[v], v[6:7], 0, %[v]"
+               : SA_PCG_DRAW_OUTS, [v] "+v"(v)
                : SA_PCG_DRAW_INS
                : SA_PCG_DRAW_CLOBBERS);
 }
 __device__ __forceinline__ void pcg_draw_one(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
                                              uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
-                                             uint32_t m, uint32_t& zmin, uint32_t& ulo, uint32_t& uhi) {
+                                             uint32_t m, uint32_t& zmin, uint64_t& u) {
   uint64_t k1, k2, k3;
   asm volatile(SA_PCG_DRAW_ASM
                "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"  // t hi
-               "s_nop 0\n\t"
-               "v_addc_co_u32_e64 %[uhi], %[k1], %[uhi], v7, %[k1]"
+               "v_lshl_add_u64 %[u], v[6:7], 0, %[u]"
                : SA_PCG_DRAW_OUTS
                : SA_PCG_DRAW_INS
                : SA_PCG_DRAW_CLOBBERS);
@@ -374,6 +389,18 @@ struct Pairs {
 };
 
 
+// Clients whose accumulator holds the NEGATED running value (st = -acc): the
+// upper half.  An internal pair (u, v) adds t to u and subtracts it from v;
+// with u in the lower and v in the upper half both become adds (one
+// v_lshl_add_u64 each instead of an add and a two-instruction subtract) --
+// 16 of the 28 pairs of 8 clients.  A negated client's cross streams draw
+// ~t = -t - 1 (sign mask inverted) and add; its accumulator starts at
+// X - bias; the finish forms q - st.
+template <int L>
+constexpr bool negated(int c) {
+  return L >= 2 && c >= L / 2;
+}
+
 // Draw schedule of a launch: the P streams grouped into interleaved pairs
 // (sa_draw2.h) wherever two streams touch disjoint accumulators (or, for
 // two cross streams of the same client, one shared accumulator), singles
@@ -381,7 +408,9 @@ struct Pairs {
 // (for L = 8: 14 disjoint pairs of pairs), cross streams by client.
 struct Group {
   int qa, qb;          // streams (qb < 0: single draw)
-  int ua, va, ub, vb;  // accumulators (clients); v < 0: a cross stream (no partner)
+  int ua, va, ub, vb;  // accumulators: u adds t; v < 0: a cross stream (no partner)
+  bool va_add, vb_add;  // the partner adds t (it is stored negated) instead of subtracting
+  bool fa, fb;          // cross stream of a negated client: inverted sign mask
 };
 template <int L, int X>
 struct Sched {
@@ -389,23 +418,37 @@ struct Sched {
   static constexpr int P = PI + L * X;
   int n = 0;
   Group g[P > 0 ? P : 1] = {};
+  struct Role {
+    int u, v;  // add target, partner (-1: none)
+    bool v_add, flip;
+  };
+  static constexpr Role role(int q) {
+    if (q >= PI) {
+      const int c = (q - PI) / (X > 0 ? X : 1);
+      return Role{c, -1, false, negated<L>(c)};
+    }
+    const int u = Pairs<L>::u(q), v = Pairs<L>::v(q);
+    if (!negated<L>(v)) return Role{u, v, false, false};  // both plain: u += t, v -= t
+    if (!negated<L>(u)) return Role{u, v, true, false};   // v negated: both add
+    return Role{v, u, false, false};                      // both negated: -u -= t, -v += t
+  }
   constexpr Sched() {
     bool used[P > 0 ? P : 1] = {};
-    auto cl_u = [](int q) { return q < PI ? Pairs<L>::u(q) : (q - PI) / (X > 0 ? X : 1); };
-    auto cl_v = [](int q) { return q < PI ? Pairs<L>::v(q) : -1; };
     for (int q = 0; q < P; q++) {
       if (used[q]) continue;
       used[q] = true;
+      const Role a = role(q);
       int mate = -1;
       for (int r = q + 1; r < P && mate < 0; r++) {
         if (used[r] || (q < PI) != (r < PI)) continue;
-        const int a = cl_u(q), b = cl_v(q), c = cl_u(r), d = cl_v(r);
-        const bool disjoint = a != c && a != d && (b < 0 || (b != c && b != d));
-        const bool same_one = q >= PI && a == c;  // two cross streams of one client
+        const Role b = role(r);
+        const bool disjoint = a.u != b.u && a.u != b.v && (a.v < 0 || (a.v != b.u && a.v != b.v));
+        const bool same_one = q >= PI && a.u == b.u;  // two cross streams of one client
         if (disjoint || same_one) mate = r;
       }
       if (mate >= 0) used[mate] = true;
-      g[n++] = Group{q, mate, cl_u(q), cl_v(q), mate >= 0 ? cl_u(mate) : -1, mate >= 0 ? cl_v(mate) : -1};
+      const Role b = mate >= 0 ? role(mate) : Role{-1, -1, false, false};
+      g[n++] = Group{q, mate, a.u, a.v, b.u, b.v, a.v_add, b.v_add, a.flip, b.flip};
     }
   }
 };
@@ -553,7 +596,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
     Vec2<XT> xv[L];
     Vec2<CT> wv[kGeneral ? L : 1];
     Vec2<uint64_t> pv[kGeneral ? L : 1];
-    uint32_t al[kE][L], ah[kE][L];  // per-client accumulators (32-bit halves)
+    uint64_t acc[kE][L];  // per-client accumulators (negated<L> clients: -acc)
     {
       kargs_t* ka = fenced_args();
       const bool cont = kGeneral && ka->continue_mode;
@@ -570,13 +613,11 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
           wv[c] = bload2<CT>(make_rsrc(wp, (wp && !cont) ? n * sizeof(CT) : 0), i);
           pv[c] = bload2<uint64_t>(make_rsrc(ka->c[c].masked_out, cont ? n * 8 : 0), i);
         }
-        // accumulators start at the client's folded bias constant
-        const uint64_t bias = ka->c[c].bias;
+        // accumulators start at the client's folded bias constant (negated
+        // clients: X - bias, see negated<L>)
+        const uint64_t bias = negated<L>(c) ? (uint64_t)X - ka->c[c].bias : ka->c[c].bias;
 #pragma unroll
-        for (int k = 0; k < kE; k++) {
-          al[k][c] = (uint32_t)bias;
-          ah[k][c] = (uint32_t)(bias >> 32);
-        }
+        for (int k = 0; k < kE; k++) acc[k][c] = bias;
       }
     }
 
@@ -597,7 +638,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
           ni1[h] = c[3];
           nj0[h] = c[4];
           nj1[h] = c[5];
-          nm[h] = (uint32_t)c[6];
+          nm[h] = (uint32_t)c[6] ^ ((h == 0 ? S.g[g].fa : S.g[g].fb) ? 0xFFFFFFFFu : 0u);
         }
       };
       fetch(0);
@@ -620,25 +661,36 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
           const uint64_t ca = k == 0 ? cj0[0] : ci0[0], da = k == 0 ? cj1[0] : ci1[0];
           const uint64_t cb = k == 0 ? cj0[1] : ci0[1], db = k == 0 ? cj1[1] : ci1[1];
           uint32_t* sa = st[G.qa];
+          uint64_t* ak = acc[k];
           if (G.qb < 0) {
-            if (G.va >= 0)
-              pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], zmin,
-                            al[k][G.ua], ah[k][G.ua], al[k][G.va], ah[k][G.va]);
+            if (G.va >= 0 && G.va_add)
+              pcg_draw_pair_a(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], zmin, ak[G.ua],
+                              ak[G.va]);
+            else if (G.va >= 0)
+              pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], zmin, ak[G.ua],
+                            ak[G.va]);
             else
-              pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], zmin,
-                           al[k][G.ua], ah[k][G.ua]);
+              pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], zmin, ak[G.ua]);
           } else {
             uint32_t* sb = st[G.qb];
-            if (G.va >= 0)
-              pcg_draw2_pair(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca,
-                             da, m[0], cb, db, m[1], zmin, al[k][G.ua], ah[k][G.ua], al[k][G.va], ah[k][G.va],
-                             al[k][G.ub], ah[k][G.ub], al[k][G.vb], ah[k][G.vb]);
+#define SA_DRAW2_PAIR(fn)                                                                                   \
+  fn(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], cb, db, \
+     m[1], zmin, ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb])
+            if (G.va >= 0 && G.va_add && G.vb_add)
+              SA_DRAW2_PAIR(pcg_draw2_pair_aa);
+            else if (G.va >= 0 && G.va_add)
+              SA_DRAW2_PAIR(pcg_draw2_pair_as);
+            else if (G.va >= 0 && G.vb_add)
+              SA_DRAW2_PAIR(pcg_draw2_pair_sa);
+            else if (G.va >= 0)
+              SA_DRAW2_PAIR(pcg_draw2_pair_ss);
+#undef SA_DRAW2_PAIR
             else if (G.ua == G.ub)
               pcg_draw2_one_same(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3],
-                                 ca, da, m[0], cb, db, m[1], zmin, al[k][G.ua], ah[k][G.ua]);
+                                 ca, da, m[0], cb, db, m[1], zmin, ak[G.ua]);
             else
               pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca,
-                            da, m[0], cb, db, m[1], zmin, al[k][G.ua], ah[k][G.ua], al[k][G.ub], ah[k][G.ub]);
+                            da, m[0], cb, db, m[1], zmin, ak[G.ua], ak[G.ub]);
           }
           if (k == 0 && g + 1 < S.n && !(SA_ABLATE & 128)) fetch(g + 1);
         }
@@ -662,7 +714,8 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
     const bool wave_full = base + wave_off + 64 * kE <= n;
     uint64_t sum[kE] = {0, 0};
     auto finish = [&](int c, uint64_t q0, uint64_t q1) {
-      const uint64_t a0 = pack64(al[0][c], ah[0][c]) + q0, a1 = pack64(al[1][c], ah[1][c]) + q1;
+      const uint64_t a0 = negated<L>(c) ? q0 - acc[0][c] : acc[0][c] + q0;
+      const uint64_t a1 = negated<L>(c) ? q1 - acc[1][c] : acc[1][c] + q1;
       sum[0] += a0;
       sum[1] += a1;
       if (!(SA_ABLATE & 32)) {

@@ -12,6 +12,14 @@ rule the single draw already follows: a VALU-written SGPR (carry, VCC) is
 read no earlier than the third instruction after the write (s_nop padding is
 inserted where the interleave alone does not give that).
 
+Accumulation: the client accumulators are 64-bit VGPR pairs.  The draw is
+added with ONE v_lshl_add_u64 (measured at the issue cost of one v_add_co,
+tools/microbench/op_rate.hip: the v_add_co + v_addc pair costs two); the
+second client of an internal pair either also adds (kernel stores it
+negated) or subtracts with v_sub_co + v_subb on the pair's 32-bit halves.
+Functions are emitted per (stream a, stream b) second-client mode: "s"
+subtract, "a" add.
+
 usage: python tools/gen_draw2.py > sfl_amd/csrc/sa_draw2.h
 """
 
@@ -44,18 +52,19 @@ DRAW = [
     ("v_alignbit_b32 v{v5}, v{v0}, v{v1}, v{v2}", set(), set()),
     ("ZMIN", set(), set()),
     ("{cnd_lo}", set(), {"sw"}),
-    ("v_add_co_u32_e64 %[{ulo}], %[{k1}], %[{ulo}], v{v6}", {"k1"}, set()),
-    ("SUBLO", {"k2"}, set()),
+    ("VSUBLO", {"k2"}, set()),
     ("{cnd_hi}", set(), {"sw"}),
-    ("v_addc_co_u32_e64 %[{uhi}], %[{k1}], %[{uhi}], v{v7}, %[{k1}]", {"k1"}, {"k1"}),
-    ("SUBHI", {"k2"}, {"k2"}),
+    ("v_lshl_add_u64 %[{u}], v[{v6}:{v7}], 0, %[{u}]", set(), set()),
+    ("VADD", set(), set()),
+    ("VSUBHI", {"k2"}, {"k2"}),
 ]
 
 
-def stream(tag, base, pair, acc_u, acc_v):
+def stream(tag, base, vmode, acc_u, acc_v):
+    """vmode: None (no second client), "s" (subtract) or "a" (add)."""
     f = {"s0": f"s0{tag}", "s1": f"s1{tag}", "s2": f"s2{tag}", "s3": f"s3{tag}",
          "k1": f"k1{tag}", "k2": f"k2{tag}", "k3": f"k3{tag}",
-         "c01": f"c01{tag}", "c23": f"c23{tag}", "m": f"m{tag}", "ulo": f"{acc_u}lo", "uhi": f"{acc_u}hi"}
+         "c01": f"c01{tag}", "c23": f"c23{tag}", "m": f"m{tag}", "u": acc_u}
     for i in range(10):
         f[f"v{i}"] = str(base + i)
     if tag == "a":
@@ -68,12 +77,16 @@ def stream(tag, base, pair, acc_u, acc_v):
         f["cnd_hi"] = f"v_cndmask_b32_e64 v{base + 7}, v{base + 5}, v{base + 4}, %[swb]"
     out = []
     for asm, w, r in DRAW:
-        if asm == "SUBLO":
-            if not pair:
+        if asm == "VADD":
+            if vmode != "a":
+                continue
+            asm = f"v_lshl_add_u64 %[{acc_v}], v[{base + 6}:{base + 7}], 0, %[{acc_v}]"
+        elif asm == "VSUBLO":
+            if vmode != "s":
                 continue
             asm = f"v_sub_co_u32_e64 %[{acc_v}lo], %[k2{tag}], %[{acc_v}lo], v{base + 6}"
-        elif asm == "SUBHI":
-            if not pair:
+        elif asm == "VSUBHI":
+            if vmode != "s":
                 continue
             asm = f"v_subb_co_u32_e64 %[{acc_v}hi], %[k2{tag}], %[{acc_v}hi], v{base + 7}, %[k2{tag}]"
         elif asm == "ZMIN":
@@ -109,30 +122,35 @@ def interleave(a, b):
     return out
 
 
-def emit(name, pair, same_acc):
+def emit(name, vma, vmb, same_acc):
     acc_ua, acc_va = "ua", "va"
     acc_ub, acc_vb = ("ua", None) if same_acc else ("ub", "vb")
-    a = stream("a", 0, pair, acc_ua, acc_va)
-    b = stream("b", 10, pair, acc_ub, acc_vb)
+    a = stream("a", 0, vma, acc_ua, acc_va)
+    b = stream("b", 10, vmb, acc_ub, acc_vb)
     seq = interleave(a, b)
     n_valu = sum(1 for s in seq if s[0].startswith("v_"))
     n_nop = sum(1 for s in seq if s[0].startswith("s_nop"))
-    accs = ["ua"] + (["va"] if pair else []) + ([] if same_acc else ["ub"] + (["vb"] if pair else []))
+    u64 = ["ua"] + ([] if same_acc else ["ub"]) + [x for x, m in (("va", vma), ("vb", vmb)) if m == "a"]
+    split = [x for x, m in (("va", vma), ("vb", vmb)) if m == "s"]
+    accs = ["ua"] + (["va"] if vma else []) + ([] if same_acc else ["ub"] + (["vb"] if vmb else []))
     lines = []
     lines.append(f"// {name}: {n_valu} VALU + {n_nop} s_nop for two draws")
     params = ["uint32_t& s0a", "uint32_t& s1a", "uint32_t& s2a", "uint32_t& s3a",
               "uint32_t& s0b", "uint32_t& s1b", "uint32_t& s2b", "uint32_t& s3b",
               "uint32_t a0", "uint32_t a1", "uint32_t a2", "uint32_t a3",
               "uint64_t c01a", "uint64_t c23a", "uint32_t ma", "uint64_t c01b", "uint64_t c23b", "uint32_t mb",
-              "uint32_t& zmin"] + [f"uint32_t& {x}{h}" for x in accs for h in ("lo", "hi")]
+              "uint32_t& zmin"] + [f"uint64_t& {x}" for x in accs]
     lines.append(f"__device__ __forceinline__ void {name}(" + ", ".join(params) + ") {")
     lines.append("  uint64_t k1a, k2a, k3a, k1b, k2b, k3b, swb;")
+    for x in split:
+        lines.append(f"  uint32_t {x}lo = (uint32_t){x}, {x}hi = (uint32_t)({x} >> 32);")
     lines.append("  asm volatile(")
     for asm, _, _ in seq:
         lines.append(f'      "{asm}\\n\\t"')
     outs = ['[s0a] "+v"(s0a)', '[s1a] "+v"(s1a)', '[s2a] "+v"(s2a)', '[s3a] "+v"(s3a)',
             '[s0b] "+v"(s0b)', '[s1b] "+v"(s1b)', '[s2b] "+v"(s2b)', '[s3b] "+v"(s3b)', '[zmin] "+v"(zmin)']
-    outs += [f'[{x}{h}] "+v"({x}{h})' for x in accs for h in ("lo", "hi")]
+    outs += [f'[{x}] "+v"({x})' for x in accs if x in u64]
+    outs += [f'[{x}{h}] "+v"({x}{h})' for x in split for h in ("lo", "hi")]
     outs += [f'[{k}] "=&s"({k})' for k in ("k1a", "k2a", "k3a", "k1b", "k2b", "k3b", "swb")]
     ins = ['[a0] "v"(a0)', '[a1] "v"(a1)', '[a2] "v"(a2)', '[a3] "v"(a3)',
            '[c01a] "s"(c01a)', '[c23a] "s"(c23a)', '[ma] "s"(ma)',
@@ -141,6 +159,8 @@ def emit(name, pair, same_acc):
     lines.append("      : " + ", ".join(outs))
     lines.append("      : " + ", ".join(ins))
     lines.append("      : " + ", ".join(clob) + ");")
+    for x in split:
+        lines.append(f"  {x} = ((uint64_t){x}hi << 32) | {x}lo;")
     lines.append("}")
     return "\n".join(lines)
 
@@ -154,11 +174,13 @@ def main():
     print()
     print("namespace sa {")
     print()
-    print(emit("pcg_draw2_pair", pair=True, same_acc=False))
+    for ma in "sa":
+        for mb in "sa":
+            print(emit(f"pcg_draw2_pair_{ma}{mb}", ma, mb, same_acc=False))
+            print()
+    print(emit("pcg_draw2_one", None, None, same_acc=False))
     print()
-    print(emit("pcg_draw2_one", pair=False, same_acc=False))
-    print()
-    print(emit("pcg_draw2_one_same", pair=False, same_acc=True))
+    print(emit("pcg_draw2_one_same", None, None, same_acc=True))
     print()
     print("}  // namespace sa")
 

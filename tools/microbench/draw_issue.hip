@@ -35,26 +35,26 @@ constexpr uint32_t A0 = 0x9FCCF645u, A1 = 0x4385DF64u, A2 = 0x1FC65DA4u, A3 = 0x
   [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c01] "s"(c01), [c23] "s"(c23), [m] "s"(m)
 __device__ __forceinline__ void draw_pair_s(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
                                             uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
-                                            uint32_t m, uint32_t& zmin, uint32_t& ulo, uint32_t& uhi,
-                                            uint32_t& vlo, uint32_t& vhi) {
+                                            uint32_t m, uint32_t& zmin, uint64_t& u, uint64_t& v) {
   uint64_t k1, k2, k3;
+  uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
   asm volatile(SA_PCG_DRAW_ASM
                "v_sub_co_u32_e64 %[vlo], %[k2], %[vlo], v6\n\t"
                "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"
-               "v_addc_co_u32_e64 %[uhi], %[k1], %[uhi], v7, %[k1]\n\t"
+               "v_lshl_add_u64 %[u], v[6:7], 0, %[u]\n\t"
                "v_subb_co_u32_e64 %[vhi], %[k2], %[vhi], v7, %[k2]"
                : SA_PCG_DRAW_OUTS, [vlo] "+v"(vlo), [vhi] "+v"(vhi)
                : SMEM_INS
                : SA_PCG_DRAW_CLOBBERS);
+  v = ((uint64_t)vhi << 32) | vlo;
 }
 __device__ __forceinline__ void draw_one_s(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
                                            uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
-                                           uint32_t m, uint32_t& zmin, uint32_t& ulo, uint32_t& uhi) {
+                                           uint32_t m, uint32_t& zmin, uint64_t& u) {
   uint64_t k1, k2, k3;
   asm volatile(SA_PCG_DRAW_ASM
                "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"
-               "s_nop 0\n\t"
-               "v_addc_co_u32_e64 %[uhi], %[k1], %[uhi], v7, %[k1]"
+               "v_lshl_add_u64 %[u], v[6:7], 0, %[u]"
                : SA_PCG_DRAW_OUTS
                : SMEM_INS
                : SA_PCG_DRAW_CLOBBERS);
@@ -82,11 +82,11 @@ __global__ void __launch_bounds__(256) k_smem(uint64_t* out, int iters, uint32_t
   uint32_t va0, va1, va2, va3;
   asm volatile("v_mov_b32 %0, %4\n\tv_mov_b32 %1, %5\n\tv_mov_b32 %2, %6\n\tv_mov_b32 %3, %7"
                : "=v"(va0), "=v"(va1), "=v"(va2), "=v"(va3) : "s"(a0), "s"(a1), "s"(a2), "s"(a3));
-  uint32_t al[E][L], ah[E][L];
+  uint64_t acc2[E][L];
 #pragma unroll
   for (int k = 0; k < E; k++)
 #pragma unroll
-    for (int c = 0; c < L; c++) al[k][c] = ah[k][c] = c + k;
+    for (int c = 0; c < L; c++) acc2[k][c] = c + k;
   uint32_t zmin = 0xFFFFFFFFu;
   cptr_t cp = (cptr_t)gconst;
   for (int it = 0; it < iters; it++) {
@@ -109,12 +109,11 @@ __global__ void __launch_bounds__(256) k_smem(uint64_t* out, int iters, uint32_t
         if constexpr (PAIRS) {
           constexpr int PI = Pairs<L>::count;
           const int cu = Pairs<L>::u(q % PI), cv = Pairs<L>::v(q % PI);
-          draw_pair_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, c01, c23, sm, zmin, al[k][cu],
-                      ah[k][cu], al[k][cv], ah[k][cv]);
+          draw_pair_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, c01, c23, sm, zmin, acc2[k][cu],
+                      acc2[k][cv]);
         } else {
           const int cu = q % L;
-          draw_one_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, c01, c23, sm, zmin, al[k][cu],
-                     ah[k][cu]);
+          draw_one_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, c01, c23, sm, zmin, acc2[k][cu]);
         }
         if (PREF && k == 0 && q + 1 < P) {
           cptr_t g = cp + 8 * (q + 1);
@@ -130,7 +129,7 @@ __global__ void __launch_bounds__(256) k_smem(uint64_t* out, int iters, uint32_t
 #pragma unroll
   for (int k = 0; k < E; k++)
 #pragma unroll
-    for (int c = 0; c < L; c++) acc += pack64(al[k][c], ah[k][c]);
+    for (int c = 0; c < L; c++) acc += acc2[k][c];
 #pragma unroll
   for (int j = 0; j < P; j++) acc ^= st[j][0] ^ st[j][3];
   out[tid] = acc;
@@ -153,11 +152,11 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
     st[j][3] = ~tid;
   }
   const uint32_t mk[4] = {vreg(A0 + seed), vreg(A1), vreg(A2), vreg(A3)};
-  uint32_t al[2][L], ah[2][L];
+  uint64_t acc2[2][L];
 #pragma unroll
   for (int k = 0; k < 2; k++)
 #pragma unroll
-    for (int c = 0; c < L; c++) al[k][c] = ah[k][c] = c + k;
+    for (int c = 0; c < L; c++) acc2[k][c] = c + k;
   uint32_t zmin = 0xFFFFFFFFu;
   cptr_t cp = (cptr_t)gconst;
   for (int it = 0; it < iters; it++) {
@@ -182,25 +181,37 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
 #pragma unroll
       for (int k = 0; k < 2; k++) {
         uint32_t* sa = st[G.qa];
+        uint64_t* ak = acc2[k];
+        const uint32_t fma_ = ma ^ (G.fa ? 0xFFFFFFFFu : 0u), fmb_ = mb ^ (G.fb ? 0xFFFFFFFFu : 0u);
         if (G.qb < 0) {
-          if (G.va >= 0)
-            pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, ma, zmin, al[k][G.ua],
-                          ah[k][G.ua], al[k][G.va], ah[k][G.va]);
+          if (G.va >= 0 && G.va_add)
+            pcg_draw_pair_a(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, fma_, zmin, ak[G.ua],
+                            ak[G.va]);
+          else if (G.va >= 0)
+            pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, fma_, zmin, ak[G.ua],
+                          ak[G.va]);
           else
-            pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, ma, zmin, al[k][G.ua],
-                         ah[k][G.ua]);
+            pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, fma_, zmin, ak[G.ua]);
         } else {
           uint32_t* sb = st[G.qb];
-          if (G.va >= 0)
-            pcg_draw2_pair(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca, da,
-                           ma, cb, db, mb, zmin, al[k][G.ua], ah[k][G.ua], al[k][G.va], ah[k][G.va], al[k][G.ub],
-                           ah[k][G.ub], al[k][G.vb], ah[k][G.vb]);
+#define DRAW2(fn)                                                                                              \
+  fn(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca, da, fma_, cb, db, fmb_, \
+     zmin, ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb])
+          if (G.va >= 0 && G.va_add && G.vb_add)
+            DRAW2(pcg_draw2_pair_aa);
+          else if (G.va >= 0 && G.va_add)
+            DRAW2(pcg_draw2_pair_as);
+          else if (G.va >= 0 && G.vb_add)
+            DRAW2(pcg_draw2_pair_sa);
+          else if (G.va >= 0)
+            DRAW2(pcg_draw2_pair_ss);
+#undef DRAW2
           else if (G.ua == G.ub)
             pcg_draw2_one_same(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca,
-                               da, ma, cb, db, mb, zmin, al[k][G.ua], ah[k][G.ua]);
+                               da, fma_, cb, db, fmb_, zmin, ak[G.ua]);
           else
             pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca, da,
-                          ma, cb, db, mb, zmin, al[k][G.ua], ah[k][G.ua], al[k][G.ub], ah[k][G.ub]);
+                          fma_, cb, db, fmb_, zmin, ak[G.ua], ak[G.ub]);
         }
         if (k == 0 && g + 1 < S.n) fetch(g + 1);
       }
@@ -210,7 +221,7 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
 #pragma unroll
   for (int k = 0; k < 2; k++)
 #pragma unroll
-    for (int c = 0; c < L; c++) acc += pack64(al[k][c], ah[k][c]);
+    for (int c = 0; c < L; c++) acc += acc2[k][c];
 #pragma unroll
   for (int j = 0; j < P; j++) acc ^= st[j][0] ^ st[j][3];
   out[tid] = acc;
@@ -309,9 +320,9 @@ __global__ void __launch_bounds__(256) k_draws(uint64_t* out, int iters, uint32_
       rm[j] = (uint32_t)sl[j].smask;
     }
   }
-  uint32_t al[L], ah[L];
+  uint64_t acc1[L];
 #pragma unroll
-  for (int c = 0; c < L; c++) al[c] = ah[c] = c;
+  for (int c = 0; c < L; c++) acc1[c] = c;
   uint32_t zmin = 0xFFFFFFFFu;
   lds_ptr slp = (lds_ptr)(sl);
   for (int it = 0; it < iters; it++) {
@@ -334,17 +345,17 @@ __global__ void __launch_bounds__(256) k_draws(uint64_t* out, int iters, uint32_
       if constexpr (PAIRS) {
         constexpr int PI = Pairs<L>::count;
         const int cu = Pairs<L>::u(q % PI), cv = Pairs<L>::v(q % PI);
-        pcg_draw_pair(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, c01, c23, sm, zmin, al[cu], ah[cu],
-                      al[cv], ah[cv]);
+        pcg_draw_pair(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, c01, c23, sm, zmin, acc1[cu],
+                      acc1[cv]);
       } else {
         const int cu = q % L;
-        pcg_draw_one(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, c01, c23, sm, zmin, al[cu], ah[cu]);
+        pcg_draw_one(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, c01, c23, sm, zmin, acc1[cu]);
       }
     }
   }
   uint64_t acc = zmin;
 #pragma unroll
-  for (int c = 0; c < L; c++) acc += pack64(al[c], ah[c]);
+  for (int c = 0; c < L; c++) acc += acc1[c];
 #pragma unroll
   for (int j = 0; j < P; j++) acc ^= st[j][0] ^ st[j][3];
   out[tid] = acc;
