@@ -268,9 +268,10 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
 //
 //   S' = S*A + C (mod 2^128) from 32-bit limbs: three 64-bit column chains
 //   (limbs 0-1: s0a0 + C01; limbs 1-2: s0a1 + s1a0; limbs 2-3: s0a2 + s1a1 +
-//   s2a0 + C23) on v_mad_u64_u32, the four limb-3 products on v_mul_lo_u32,
-//   joined by carry adds whose carry-ins are the mads' own carry-outs -- 6
-//   mads + 4 mul_lo + 8 adds, no register shuffling.  Then t = rotr(hi^lo^m,
+//   s2a0 + C23) on v_mad_u64_u32, the four limb-3 products summed by one
+//   v_mul_lo_u32 and three v_mad_u64_u32 (only the low word is kept), joined
+//   by carry adds whose carry-ins are the mads' own carry-outs -- 9 mads + 1
+//   mul_lo + 7 adds, no register shuffling.  Then t = rotr(hi^lo^m,
 //   hi>>58) in 32-bit halves (v_bitop3 + v_alignbit + swap), the raw==0 test
 //   (hi == lo <=> xl == xh == m) folded into a running minimum, and the
 //   accumulation (below).
@@ -284,22 +285,21 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
   "v_mad_u64_u32 v[0:1], %[k1], %[s0], %[a0], %[c01]\n\t"   /* E0 = s0a0 + C01, kE */   \
   "v_mad_u64_u32 v[2:3], %[k3], %[s0], %[a1], 0\n\t"        /* O1 = s0a1 */             \
   "v_mad_u64_u32 v[4:5], %[k3], %[s0], %[a2], %[c23]\n\t"   /* E2 = s0a2 + C23 */       \
-  "v_mul_lo_u32 v6, %[s0], %[a3]\n\t"                                                    \
+  "v_mul_lo_u32 v6, %[s0], %[a3]\n\t"                       /* L3 = p03 */               \
   "v_mad_u64_u32 v[2:3], %[k2], %[s1], %[a0], v[2:3]\n\t"   /* O1 += s1a0, kO */        \
   "v_mad_u64_u32 v[4:5], %[k3], %[s1], %[a1], v[4:5]\n\t"                                \
-  "v_mul_lo_u32 v7, %[s1], %[a2]\n\t"                                                    \
+  "v_mad_u64_u32 v[6:7], %[k3], %[s1], %[a2], v[6:7]\n\t"   /* L3 += p12 (low word) */  \
   "v_mad_u64_u32 v[4:5], %[k3], %[s2], %[a0], v[4:5]\n\t"                                \
-  "v_mul_lo_u32 v8, %[s2], %[a1]\n\t"                                                    \
-  "v_mul_lo_u32 v9, %[s3], %[a0]\n\t"                                                    \
+  "v_mad_u64_u32 v[6:7], %[k3], %[s2], %[a1], v[6:7]\n\t"   /* L3 += p21 */             \
+  "v_mad_u64_u32 v[6:7], %[k3], %[s3], %[a0], v[6:7]\n\t"   /* L3 += p30 */             \
   "v_add_co_u32_e64 %[s1], %[k3], v1, v2\n\t"              /* r1 = e1 + o1, c1 */       \
-  "v_addc_co_u32_e64 %[s3], %[k2], v5, v6, %[k2]\n\t"      /* r3 = e3 + p03 + kO */     \
-  "v_add_u32_e32 %[s3], %[s3], v9\n\t"                      /* r3 += p30 */              \
+  "v_addc_co_u32_e64 %[s3], %[k2], v5, v6, %[k2]\n\t"      /* r3 = e3 + L3 + kO */      \
+  "v_mov_b32_e32 %[s0], v0\n\t"                             /* r0 = e0 */                \
   "v_addc_co_u32_e64 %[s2], %[k2], v4, v3, %[k3]\n\t"      /* r2 = e2 + o2 + c1, c2 */  \
   "v_addc_co_u32_e64 %[s2], %[k3], %[s2], 0, %[k1]\n\t"    /* r2 += kE, c3 */           \
-  "v_mov_b32_e32 %[s0], v0\n\t"                             /* r0 = e0 */                \
-  "v_addc_co_u32_e64 %[s3], %[k2], %[s3], v7, %[k2]\n\t"   /* r3 += p12 + c2 */         \
-  "v_addc_co_u32_e64 %[s3], %[k3], %[s3], v8, %[k3]\n\t"   /* r3 += p21 + c3 */         \
   "v_bitop3_b32 v0, %[s0], %[s2], %[m] bitop3:0x96\n\t"    /* xl */                     \
+  "v_addc_co_u32_e64 %[s3], %[k2], %[s3], 0, %[k2]\n\t"    /* r3 += c2 */               \
+  "v_addc_co_u32_e64 %[s3], %[k3], %[s3], 0, %[k3]\n\t"    /* r3 += c3 */               \
   "v_bitop3_b32 v1, %[s1], %[s3], %[m] bitop3:0x96\n\t"    /* xh */                     \
   "v_cmp_gt_i32_e32 vcc, 0, %[s3]\n\t"                      /* rot >= 32: swap */        \
   "v_lshrrev_b32_e32 v2, 26, %[s3]\n\t"                     /* rot (& 31 in alignbit) */ \

@@ -31,18 +31,17 @@ DRAW = [
     ("v_mul_lo_u32 v{v6}, %[{s0}], %[a3]", set(), set()),
     ("v_mad_u64_u32 v[{v2}:{v3}], %[{k2}], %[{s1}], %[a0], v[{v2}:{v3}]", {"k2"}, set()),
     ("v_mad_u64_u32 v[{v4}:{v5}], %[{k3}], %[{s1}], %[a1], v[{v4}:{v5}]", {"k3"}, set()),
-    ("v_mul_lo_u32 v{v7}, %[{s1}], %[a2]", set(), set()),
+    ("v_mad_u64_u32 v[{v6}:{v7}], %[{k3}], %[{s1}], %[a2], v[{v6}:{v7}]", {"k3"}, set()),
     ("v_mad_u64_u32 v[{v4}:{v5}], %[{k3}], %[{s2}], %[a0], v[{v4}:{v5}]", {"k3"}, set()),
-    ("v_mul_lo_u32 v{v8}, %[{s2}], %[a1]", set(), set()),
-    ("v_mul_lo_u32 v{v9}, %[{s3}], %[a0]", set(), set()),
+    ("v_mad_u64_u32 v[{v6}:{v7}], %[{k3}], %[{s2}], %[a1], v[{v6}:{v7}]", {"k3"}, set()),
+    ("v_mad_u64_u32 v[{v6}:{v7}], %[{k3}], %[{s3}], %[a0], v[{v6}:{v7}]", {"k3"}, set()),
     ("v_add_co_u32_e64 %[{s1}], %[{k3}], v{v1}, v{v2}", {"k3"}, set()),
     ("v_addc_co_u32_e64 %[{s3}], %[{k2}], v{v5}, v{v6}, %[{k2}]", {"k2"}, {"k2"}),
-    ("v_add_u32_e32 %[{s3}], %[{s3}], v{v9}", set(), set()),
     ("v_addc_co_u32_e64 %[{s2}], %[{k2}], v{v4}, v{v3}, %[{k3}]", {"k2"}, {"k3"}),
     ("v_addc_co_u32_e64 %[{s2}], %[{k3}], %[{s2}], 0, %[{k1}]", {"k3"}, {"k1"}),
     ("v_mov_b32_e32 %[{s0}], v{v0}", set(), set()),
-    ("v_addc_co_u32_e64 %[{s3}], %[{k2}], %[{s3}], v{v7}, %[{k2}]", {"k2"}, {"k2"}),
-    ("v_addc_co_u32_e64 %[{s3}], %[{k3}], %[{s3}], v{v8}, %[{k3}]", {"k3"}, {"k3"}),
+    ("v_addc_co_u32_e64 %[{s3}], %[{k2}], %[{s3}], 0, %[{k2}]", {"k2"}, {"k2"}),
+    ("v_addc_co_u32_e64 %[{s3}], %[{k3}], %[{s3}], 0, %[{k3}]", {"k3"}, {"k3"}),
     ("v_bitop3_b32 v{v0}, %[{s0}], %[{s2}], %[{m}] bitop3:0x96", set(), set()),
     ("v_bitop3_b32 v{v1}, %[{s1}], %[{s3}], %[{m}] bitop3:0x96", set(), set()),
     ("{cmp}", {"sw"}, set()),
