@@ -267,23 +267,25 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
 // gfx950 (the whole inner loop of the kernel is this block, P times per element).
 //
 //   S' = S*A + C (mod 2^128) from 32-bit limbs: three 64-bit column chains
-//   (limbs 0-1: s0a0 + C01; limbs 1-2: s0a1 + s1a0; limbs 2-3: s0a2 + s1a1 +
-//   s2a0 + C23) on v_mad_u64_u32, the four limb-3 products summed by one
-//   v_mul_lo_u32 and three v_mad_u64_u32 (only the low word is kept), joined
-//   by carry adds whose carry-ins are the mads' own carry-outs -- 9 mads + 1
-//   mul_lo + 7 adds, no register shuffling.  Then t = rotr(hi^lo^m,
+//   (limbs 0-1: s0a0 + c0; limbs 1-2: s0a1 + c1 + s1a0; limbs 2-3: s0a2 +
+//   s1a1 + s2a0 + C23) on v_mad_u64_u32 -- the increment's two low words enter
+//   as separate zero-extended addends so the first two mads cannot carry --
+//   the four limb-3 products summed by one v_mul_lo_u32 and three
+//   v_mad_u64_u32 (only the low word is kept), joined by carry adds whose
+//   carry-ins are the mads' own carry-outs -- 9 mads + 1 mul_lo + 4 adds +
+//   1 mov, no register shuffling.  Then t = rotr(hi^lo^m,
 //   hi>>58) in 32-bit halves (v_bitop3 + v_alignbit + swap), the raw==0 test
 //   (hi == lo <=> xl == xh == m) folded into a running minimum, and the
 //   accumulation (below).
 //
-// Carries live in three SGPR pairs, reused as they die (k1: kE; k2: kO, c2,
-// then the acc_v borrow; k3: discarded carry-outs, c1, c3).
+// Carries live in three SGPR pairs, reused as they die (k1: a discarded
+// carry-out; k2: kO, c2, then the acc_v borrow; k3: discarded carry-outs, c1).
 // Every VALU-written SGPR (carries, VCC) is read >= 2 instructions later
 // (gfx950 VALU-SGPR-write -> VALU-read hazard).  v0-v9 are fixed scratch (low
 // registers, so the kernel's VGPR budget is not raised).
 #define SA_PCG_DRAW_ASM                                                                  \
-  "v_mad_u64_u32 v[0:1], %[k1], %[s0], %[a0], %[c01]\n\t"   /* E0 = s0a0 + C01, kE */   \
-  "v_mad_u64_u32 v[2:3], %[k3], %[s0], %[a1], 0\n\t"        /* O1 = s0a1 */             \
+  "v_mad_u64_u32 v[0:1], %[k1], %[s0], %[a0], %[c0]\n\t"    /* E0 = s0a0 + c0 < 2^64 */  \
+  "v_mad_u64_u32 v[2:3], %[k3], %[s0], %[a1], %[c1]\n\t"    /* O1 = s0a1 + c1 < 2^64 */  \
   "v_mad_u64_u32 v[4:5], %[k3], %[s0], %[a2], %[c23]\n\t"   /* E2 = s0a2 + C23 */       \
   "v_mul_lo_u32 v6, %[s0], %[a3]\n\t"                       /* L3 = p03 */               \
   "v_mad_u64_u32 v[2:3], %[k2], %[s1], %[a0], v[2:3]\n\t"   /* O1 += s1a0, kO */        \
@@ -296,10 +298,9 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
   "v_addc_co_u32_e64 %[s3], %[k2], v5, v6, %[k2]\n\t"      /* r3 = e3 + L3 + kO */      \
   "v_mov_b32_e32 %[s0], v0\n\t"                             /* r0 = e0 */                \
   "v_addc_co_u32_e64 %[s2], %[k2], v4, v3, %[k3]\n\t"      /* r2 = e2 + o2 + c1, c2 */  \
-  "v_addc_co_u32_e64 %[s2], %[k3], %[s2], 0, %[k1]\n\t"    /* r2 += kE, c3 */           \
   "v_bitop3_b32 v0, %[s0], %[s2], %[m] bitop3:0x96\n\t"    /* xl */                     \
-  "v_addc_co_u32_e64 %[s3], %[k2], %[s3], 0, %[k2]\n\t"    /* r3 += c2 */               \
-  "v_addc_co_u32_e64 %[s3], %[k3], %[s3], 0, %[k3]\n\t"    /* r3 += c3 */               \
+  "s_nop 0\n\t"                                                                          \
+  "v_addc_co_u32_e64 %[s3], %[k3], %[s3], 0, %[k2]\n\t"    /* r3 += c2 */               \
   "v_bitop3_b32 v1, %[s1], %[s3], %[m] bitop3:0x96\n\t"    /* xh */                     \
   "v_cmp_gt_i32_e32 vcc, 0, %[s3]\n\t"                      /* rot >= 32: swap */        \
   "v_lshrrev_b32_e32 v2, 26, %[s3]\n\t"                     /* rot (& 31 in alignbit) */ \
@@ -316,8 +317,8 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
 // launch), the stream constants SGPRs (scalar-loaded per stream and tile), so
 // every VOP3 reads at most one SGPR (the gfx9 constant-bus limit).
 #define SA_PCG_DRAW_INS                                                                  \
-  [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c01] "s"(c01), [c23] "s"(c23),  \
-      [m] "s"(m)
+  [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c0] "s"((uint64_t)(uint32_t)c01), \
+      [c1] "s"(c01 >> 32), [c23] "s"(c23), [m] "s"(m)
 #define SA_PCG_DRAW_CLOBBERS \
   "vcc", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9"
 

@@ -87,9 +87,11 @@ def test_valu_sgpr_write_read_distance():
 
 
 def test_limb_equations_equal_numpy_pcg64():
-    """The asm computes S' = S*A + C from 32-bit limbs as E0 = s0a0 + C01,
-    O1 = s0a1 + s1a0, E2 = s0a2 + s1a1 + s2a0 + C23, L3 = s0a3+s1a2+s2a1+s3a0;
-    r = E0 + O1<<32 + E2<<64 + L3<<96 mod 2^128.  Check against numpy."""
+    """The asm computes S' = S*A + C from 32-bit limbs as E0 = s0a0 + c0,
+    O1 = s0a1 + c1 + s1a0, E2 = s0a2 + s1a1 + s2a0 + C23 (mod 2^64),
+    L3 = s0a3+s1a2+s2a1+s3a0 (mod 2^32); r = E0 + O1<<32 + E2<<64 + L3<<96
+    mod 2^128, where E0 and the first O1 mad (s0a1 + c1) cannot carry out of
+    64 bits.  Check against numpy."""
     M = (1 << 128) - 1
     A = 0x2360ED051FC65DA44385DF649FCCF645
     a = [(A >> (32 * i)) & 0xFFFFFFFF for i in range(4)]
@@ -99,10 +101,11 @@ def test_limb_equations_equal_numpy_pcg64():
     gen = np.random.PCG64(12345)
     for _ in range(50):
         limbs = [(s >> (32 * i)) & 0xFFFFFFFF for i in range(4)]
-        c01, c23 = inc & ((1 << 64) - 1), inc >> 64
-        e0 = limbs[0] * a[0] + c01
-        o1 = limbs[0] * a[1] + limbs[1] * a[0]
-        e2 = limbs[0] * a[2] + limbs[1] * a[1] + limbs[2] * a[0] + c23
+        c0, c1, c23 = inc & 0xFFFFFFFF, (inc >> 32) & 0xFFFFFFFF, inc >> 64
+        e0 = limbs[0] * a[0] + c0
+        assert e0 < 1 << 64 and limbs[0] * a[1] + c1 < 1 << 64  # no carry-out
+        o1 = limbs[0] * a[1] + c1 + limbs[1] * a[0]
+        e2 = (limbs[0] * a[2] + limbs[1] * a[1] + limbs[2] * a[0] + c23) & ((1 << 64) - 1)
         l3 = (limbs[0] * a[3] + limbs[1] * a[2] + limbs[2] * a[1] + limbs[3] * a[0]) & 0xFFFFFFFF
         s = (e0 + (o1 << 32) + (e2 << 64) + (l3 << 96)) & M
         assert s == (s * 0 + ((limbs[0] | limbs[1] << 32 | limbs[2] << 64 | limbs[3] << 96) * A + inc) & M)

@@ -25,8 +25,8 @@ usage: python tools/gen_draw2.py > sfl_amd/csrc/sa_draw2.h
 
 # one draw: (asm, sgpr_writes, sgpr_reads); {..} fields are renamed per stream
 DRAW = [
-    ("v_mad_u64_u32 v[{v0}:{v1}], %[{k1}], %[{s0}], %[a0], %[{c01}]", {"k1"}, set()),
-    ("v_mad_u64_u32 v[{v2}:{v3}], %[{k3}], %[{s0}], %[a1], 0", {"k3"}, set()),
+    ("v_mad_u64_u32 v[{v0}:{v1}], %[{k1}], %[{s0}], %[a0], %[{c0}]", {"k1"}, set()),
+    ("v_mad_u64_u32 v[{v2}:{v3}], %[{k3}], %[{s0}], %[a1], %[{c1}]", {"k3"}, set()),
     ("v_mad_u64_u32 v[{v4}:{v5}], %[{k3}], %[{s0}], %[a2], %[{c23}]", {"k3"}, set()),
     ("v_mul_lo_u32 v{v6}, %[{s0}], %[a3]", set(), set()),
     ("v_mad_u64_u32 v[{v2}:{v3}], %[{k2}], %[{s1}], %[a0], v[{v2}:{v3}]", {"k2"}, set()),
@@ -37,12 +37,10 @@ DRAW = [
     ("v_mad_u64_u32 v[{v6}:{v7}], %[{k3}], %[{s3}], %[a0], v[{v6}:{v7}]", {"k3"}, set()),
     ("v_add_co_u32_e64 %[{s1}], %[{k3}], v{v1}, v{v2}", {"k3"}, set()),
     ("v_addc_co_u32_e64 %[{s3}], %[{k2}], v{v5}, v{v6}, %[{k2}]", {"k2"}, {"k2"}),
-    ("v_addc_co_u32_e64 %[{s2}], %[{k2}], v{v4}, v{v3}, %[{k3}]", {"k2"}, {"k3"}),
-    ("v_addc_co_u32_e64 %[{s2}], %[{k3}], %[{s2}], 0, %[{k1}]", {"k3"}, {"k1"}),
     ("v_mov_b32_e32 %[{s0}], v{v0}", set(), set()),
-    ("v_addc_co_u32_e64 %[{s3}], %[{k2}], %[{s3}], 0, %[{k2}]", {"k2"}, {"k2"}),
-    ("v_addc_co_u32_e64 %[{s3}], %[{k3}], %[{s3}], 0, %[{k3}]", {"k3"}, {"k3"}),
+    ("v_addc_co_u32_e64 %[{s2}], %[{k2}], v{v4}, v{v3}, %[{k3}]", {"k2"}, {"k3"}),
     ("v_bitop3_b32 v{v0}, %[{s0}], %[{s2}], %[{m}] bitop3:0x96", set(), set()),
+    ("v_addc_co_u32_e64 %[{s3}], %[{k3}], %[{s3}], 0, %[{k2}]", {"k3"}, {"k2"}),
     ("v_bitop3_b32 v{v1}, %[{s1}], %[{s3}], %[{m}] bitop3:0x96", set(), set()),
     ("{cmp}", {"sw"}, set()),
     ("v_lshrrev_b32_e32 v{v2}, 26, %[{s3}]", set(), set()),
@@ -63,7 +61,7 @@ def stream(tag, base, vmode, acc_u, acc_v):
     """vmode: None (no second client), "s" (subtract) or "a" (add)."""
     f = {"s0": f"s0{tag}", "s1": f"s1{tag}", "s2": f"s2{tag}", "s3": f"s3{tag}",
          "k1": f"k1{tag}", "k2": f"k2{tag}", "k3": f"k3{tag}",
-         "c01": f"c01{tag}", "c23": f"c23{tag}", "m": f"m{tag}", "u": acc_u}
+         "c0": f"c0{tag}", "c1": f"c1{tag}", "c23": f"c23{tag}", "m": f"m{tag}", "u": acc_u}
     for i in range(10):
         f[f"v{i}"] = str(base + i)
     if tag == "a":
@@ -141,6 +139,7 @@ def emit(name, vma, vmb, same_acc):
               "uint32_t& zmin"] + [f"uint64_t& {x}" for x in accs]
     lines.append(f"__device__ __forceinline__ void {name}(" + ", ".join(params) + ") {")
     lines.append("  uint64_t k1a, k2a, k3a, k1b, k2b, k3b, swb;")
+    lines.append("  const uint64_t c0a = (uint32_t)c01a, c1a = c01a >> 32, c0b = (uint32_t)c01b, c1b = c01b >> 32;")
     for x in split:
         lines.append(f"  uint32_t {x}lo = (uint32_t){x}, {x}hi = (uint32_t)({x} >> 32);")
     lines.append("  asm volatile(")
@@ -152,8 +151,8 @@ def emit(name, vma, vmb, same_acc):
     outs += [f'[{x}{h}] "+v"({x}{h})' for x in split for h in ("lo", "hi")]
     outs += [f'[{k}] "=&s"({k})' for k in ("k1a", "k2a", "k3a", "k1b", "k2b", "k3b", "swb")]
     ins = ['[a0] "v"(a0)', '[a1] "v"(a1)', '[a2] "v"(a2)', '[a3] "v"(a3)',
-           '[c01a] "s"(c01a)', '[c23a] "s"(c23a)', '[ma] "s"(ma)',
-           '[c01b] "s"(c01b)', '[c23b] "s"(c23b)', '[mb] "s"(mb)']
+           '[c0a] "s"(c0a)', '[c1a] "s"(c1a)', '[c23a] "s"(c23a)', '[ma] "s"(ma)',
+           '[c0b] "s"(c0b)', '[c1b] "s"(c1b)', '[c23b] "s"(c23b)', '[mb] "s"(mb)']
     clob = ['"vcc"'] + [f'"v{i}"' for i in range(20)]
     lines.append("      : " + ", ".join(outs))
     lines.append("      : " + ", ".join(ins))

@@ -32,7 +32,8 @@ typedef __attribute__((address_space(3))) const StreamLds* lds_ptr;
 // SGPR source per VOP3).
 constexpr uint32_t A0 = 0x9FCCF645u, A1 = 0x4385DF64u, A2 = 0x1FC65DA4u, A3 = 0x2360ED05u;
 #define SMEM_INS                                                                                         \
-  [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c01] "s"(c01), [c23] "s"(c23), [m] "s"(m)
+  [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c0] "s"((uint64_t)(uint32_t)c01),          \
+      [c1] "s"(c01 >> 32), [c23] "s"(c23), [m] "s"(m)
 __device__ __forceinline__ void draw_pair_s(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
                                             uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
                                             uint32_t m, uint32_t& zmin, uint64_t& u, uint64_t& v) {
