@@ -35,7 +35,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PCG_PEAK_DRAWS = 1.54e12        # measured PCG64 draw-loop ceiling (one-sided draws, 8 waves/SIMD),
+PCG_PEAK_DRAWS = 1.57e12        # measured PCG64 draw-loop ceiling (one-sided draws, 8 waves/SIMD),
                                 # tools/microbench/draw_issue.hip "dual one7 E2", profiles/r01/draw_issue_microbench.txt
 
 

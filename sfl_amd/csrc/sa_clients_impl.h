@@ -317,8 +317,8 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
 // launch), the stream constants SGPRs (scalar-loaded per stream and tile), so
 // every VOP3 reads at most one SGPR (the gfx9 constant-bus limit).
 #define SA_PCG_DRAW_INS                                                                  \
-  [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c0] "s"((uint64_t)(uint32_t)c01), \
-      [c1] "s"(c01 >> 32), [c23] "s"(c23), [m] "s"(m)
+  [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c0] "s"(inc.w0),                    \
+      [c1] "s"(inc.w1), [c23] "s"(inc.hi), [m] "s"(m)
 #define SA_PCG_DRAW_CLOBBERS \
   "vcc", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9"
 
@@ -327,7 +327,7 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
 // client subtracts on 32-bit halves (pcg_draw_pair) or, when the kernel keeps
 // that client negated, also adds (pcg_draw_pair_a).
 __device__ __forceinline__ void pcg_draw_pair(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
-                                              uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
+                                              uint32_t a1, uint32_t a2, uint32_t a3, const Inc& inc,
                                               uint32_t m, uint32_t& zmin, uint64_t& u, uint64_t& v) {
   uint64_t k1, k2, k3;
   uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
@@ -342,7 +342,7 @@ __device__ __forceinline__ void pcg_draw_pair(uint32_t& s0, uint32_t& s1, uint32
   v = ((uint64_t)vhi << 32) | vlo;
 }
 __device__ __forceinline__ void pcg_draw_pair_a(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
-                                                uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
+                                                uint32_t a1, uint32_t a2, uint32_t a3, const Inc& inc,
                                                 uint32_t m, uint32_t& zmin, uint64_t& u, uint64_t& v) {
   uint64_t k1, k2, k3;
   asm volatile(SA_PCG_DRAW_ASM
@@ -354,7 +354,7 @@ __device__ __forceinline__ void pcg_draw_pair_a(uint32_t& s0, uint32_t& s1, uint
                : SA_PCG_DRAW_CLOBBERS);
 }
 __device__ __forceinline__ void pcg_draw_one(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
-                                             uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
+                                             uint32_t a1, uint32_t a2, uint32_t a3, const Inc& inc,
                                              uint32_t m, uint32_t& zmin, uint64_t& u) {
   uint64_t k1, k2, k3;
   asm volatile(SA_PCG_DRAW_ASM
@@ -472,8 +472,9 @@ constexpr int clients_waves(int P, int L) {
 }
 
 typedef __attribute__((address_space(4))) const uint64_t* kptr_t;
-static_assert(offsetof(StreamArg, inc_lo) == 16 && offsetof(StreamArg, cj_lo) == 32 &&
-                  offsetof(StreamArg, smask) == 48,
+static_assert(offsetof(StreamArg, inc_hi) == 24 && offsetof(StreamArg, cj_hi) == 40 &&
+                  offsetof(StreamArg, smask) == 48 && offsetof(StreamArg, inc_w0) == 64 &&
+                  offsetof(StreamArg, cj_w0) == 80,
               "StreamArg layout (scalar loads below)");
 
 typedef __attribute__((address_space(4))) const KArgs kargs_t;
@@ -627,7 +628,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
     // group g's first draw
     if constexpr (P > 0) {
       constexpr Sched<L, X> S{};
-      uint64_t ni0[2], ni1[2], nj0[2], nj1[2];
+      Inc ni[2], nj[2];  // next group's plain-step / tile-jump addends
       uint32_t nm[2];
       auto fetch = [&](int g) {
 #pragma unroll
@@ -635,10 +636,8 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
           const int q = h == 0 ? S.g[g].qa : S.g[g].qb;
           if (q < 0) continue;
           kptr_t c = (const kptr_t)(&fenced_args()->s[q]);
-          ni0[h] = c[2];
-          ni1[h] = c[3];
-          nj0[h] = c[4];
-          nj1[h] = c[5];
+          ni[h] = Inc{c[8], c[9], c[3]};
+          nj[h] = Inc{c[10], c[11], c[5]};
           nm[h] = (uint32_t)c[6] ^ ((h == 0 ? S.g[g].fa : S.g[g].fb) ? 0xFFFFFFFFu : 0u);
         }
       };
@@ -646,37 +645,35 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
 #pragma unroll
       for (int g = 0; g < S.n; g++) {
         const Group G = S.g[g];
-        uint64_t ci0[2], ci1[2], cj0[2], cj1[2];
+        Inc ci[2], cj[2];
         uint32_t m[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-          ci0[h] = ni0[h];
-          ci1[h] = ni1[h];
-          cj0[h] = nj0[h];
-          cj1[h] = nj1[h];
+          ci[h] = ni[h];
+          cj[h] = nj[h];
           m[h] = nm[h];
         }
 #pragma unroll
         for (int k = 0; k < kE; k++) {
           const uint32_t* mk = k == 0 ? mj : mp;
-          const uint64_t ca = k == 0 ? cj0[0] : ci0[0], da = k == 0 ? cj1[0] : ci1[0];
-          const uint64_t cb = k == 0 ? cj0[1] : ci0[1], db = k == 0 ? cj1[1] : ci1[1];
+          const Inc& ia = k == 0 ? cj[0] : ci[0];
+          const Inc& ib = k == 0 ? cj[1] : ci[1];
           uint32_t* sa = st[G.qa];
           uint64_t* ak = acc[k];
           if (G.qb < 0) {
             if (G.va >= 0 && G.va_add)
-              pcg_draw_pair_a(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], zmin, ak[G.ua],
+              pcg_draw_pair_a(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua],
                               ak[G.va]);
             else if (G.va >= 0)
-              pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], zmin, ak[G.ua],
+              pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua],
                             ak[G.va]);
             else
-              pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], zmin, ak[G.ua]);
+              pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua]);
           } else {
             uint32_t* sb = st[G.qb];
 #define SA_DRAW2_PAIR(fn)                                                                                   \
-  fn(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca, da, m[0], cb, db, \
-     m[1], zmin, ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb])
+  fn(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], ib, m[1], \
+     zmin, ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb])
             if (G.va >= 0 && G.va_add && G.vb_add)
               SA_DRAW2_PAIR(pcg_draw2_pair_aa);
             else if (G.va >= 0 && G.va_add)
@@ -688,10 +685,10 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
 #undef SA_DRAW2_PAIR
             else if (G.ua == G.ub)
               pcg_draw2_one_same(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3],
-                                 ca, da, m[0], cb, db, m[1], zmin, ak[G.ua]);
+                                 ia, m[0], ib, m[1], zmin, ak[G.ua]);
             else
-              pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca,
-                            da, m[0], cb, db, m[1], zmin, ak[G.ua], ak[G.ub]);
+              pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia,
+                            m[0], ib, m[1], zmin, ak[G.ua], ak[G.ub]);
           }
           if (k == 0 && g + 1 < S.n && !(SA_ABLATE & 128)) fetch(g + 1);
         }
@@ -848,6 +845,10 @@ int launch_clients(const KArgs& in, void* stream) {
       const u128 cj = jj.gsum * mk128(a.s[j].inc_hi, a.s[j].inc_lo);
       a.s[j].cj_lo = lo64(cj);
       a.s[j].cj_hi = hi64(cj);
+      a.s[j].inc_w0 = (uint32_t)a.s[j].inc_lo;
+      a.s[j].inc_w1 = a.s[j].inc_lo >> 32;
+      a.s[j].cj_w0 = (uint32_t)a.s[j].cj_lo;
+      a.s[j].cj_w1 = a.s[j].cj_lo >> 32;
     }
     hipLaunchKernelGGL((k_clients<XT, CT, L, X>), dim3(grid), dim3(kBlockThreads), 0,
                        (hipStream_t)stream, a);

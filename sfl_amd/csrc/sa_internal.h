@@ -33,6 +33,9 @@ struct StreamArg {
   uint64_t cj_lo, cj_hi;    // inc * G_J: constant part of the per-tile jump
   uint64_t smask;           // 0 (stream added) or ~0 (stream subtracted)
   uint64_t pad;
+  // the draw's addends (filled by the launcher): inc_lo's and cj_lo's two
+  // 32-bit words, zero-extended
+  uint64_t inc_w0, inc_w1, cj_w0, cj_w1;
 };
 
 struct ClientArg {
@@ -65,6 +68,8 @@ struct KArgs {
   const double* dp_sumsq_layer;
   uint64_t dp_key, dp_block0;  // Philox key; counter block of element 0
 };
+
+static_assert(sizeof(KArgs) <= 4096, "kernel arguments must fit the 4 KiB kernarg segment");
 
 typedef int (*LaunchFn)(const KArgs& a, void* stream);
 

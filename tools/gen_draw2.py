@@ -135,11 +135,10 @@ def emit(name, vma, vmb, same_acc):
     params = ["uint32_t& s0a", "uint32_t& s1a", "uint32_t& s2a", "uint32_t& s3a",
               "uint32_t& s0b", "uint32_t& s1b", "uint32_t& s2b", "uint32_t& s3b",
               "uint32_t a0", "uint32_t a1", "uint32_t a2", "uint32_t a3",
-              "uint64_t c01a", "uint64_t c23a", "uint32_t ma", "uint64_t c01b", "uint64_t c23b", "uint32_t mb",
+              "const Inc& ia", "uint32_t ma", "const Inc& ib", "uint32_t mb",
               "uint32_t& zmin"] + [f"uint64_t& {x}" for x in accs]
     lines.append(f"__device__ __forceinline__ void {name}(" + ", ".join(params) + ") {")
     lines.append("  uint64_t k1a, k2a, k3a, k1b, k2b, k3b, swb;")
-    lines.append("  const uint64_t c0a = (uint32_t)c01a, c1a = c01a >> 32, c0b = (uint32_t)c01b, c1b = c01b >> 32;")
     for x in split:
         lines.append(f"  uint32_t {x}lo = (uint32_t){x}, {x}hi = (uint32_t)({x} >> 32);")
     lines.append("  asm volatile(")
@@ -151,8 +150,8 @@ def emit(name, vma, vmb, same_acc):
     outs += [f'[{x}{h}] "+v"({x}{h})' for x in split for h in ("lo", "hi")]
     outs += [f'[{k}] "=&s"({k})' for k in ("k1a", "k2a", "k3a", "k1b", "k2b", "k3b", "swb")]
     ins = ['[a0] "v"(a0)', '[a1] "v"(a1)', '[a2] "v"(a2)', '[a3] "v"(a3)',
-           '[c0a] "s"(c0a)', '[c1a] "s"(c1a)', '[c23a] "s"(c23a)', '[ma] "s"(ma)',
-           '[c0b] "s"(c0b)', '[c1b] "s"(c1b)', '[c23b] "s"(c23b)', '[mb] "s"(mb)']
+           '[c0a] "s"(ia.w0)', '[c1a] "s"(ia.w1)', '[c23a] "s"(ia.hi)', '[ma] "s"(ma)',
+           '[c0b] "s"(ib.w0)', '[c1b] "s"(ib.w1)', '[c23b] "s"(ib.hi)', '[mb] "s"(mb)']
     clob = ['"vcc"'] + [f'"v{i}"' for i in range(20)]
     lines.append("      : " + ", ".join(outs))
     lines.append("      : " + ", ".join(ins))
@@ -171,6 +170,12 @@ def main():
     print("#include <stdint.h>")
     print()
     print("namespace sa {")
+    print()
+    print("// A stream's increment as the draw's three SGPR addends: the two low words")
+    print("// zero-extended (so s0*a0 + w0 and s0*a1 + w1 cannot carry) and the high half.")
+    print("struct Inc {")
+    print("  uint64_t w0, w1, hi;")
+    print("};")
     print()
     for ma in "sa":
         for mb in "sa":

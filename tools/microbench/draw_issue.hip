@@ -32,10 +32,10 @@ typedef __attribute__((address_space(3))) const StreamLds* lds_ptr;
 // SGPR source per VOP3).
 constexpr uint32_t A0 = 0x9FCCF645u, A1 = 0x4385DF64u, A2 = 0x1FC65DA4u, A3 = 0x2360ED05u;
 #define SMEM_INS                                                                                         \
-  [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c0] "s"((uint64_t)(uint32_t)c01),          \
-      [c1] "s"(c01 >> 32), [c23] "s"(c23), [m] "s"(m)
+  [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c0] "s"(inc.w0), [c1] "s"(inc.w1),             \
+      [c23] "s"(inc.hi), [m] "s"(m)
 __device__ __forceinline__ void draw_pair_s(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
-                                            uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
+                                            uint32_t a1, uint32_t a2, uint32_t a3, const Inc& inc,
                                             uint32_t m, uint32_t& zmin, uint64_t& u, uint64_t& v) {
   uint64_t k1, k2, k3;
   uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
@@ -50,7 +50,7 @@ __device__ __forceinline__ void draw_pair_s(uint32_t& s0, uint32_t& s1, uint32_t
   v = ((uint64_t)vhi << 32) | vlo;
 }
 __device__ __forceinline__ void draw_one_s(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
-                                           uint32_t a1, uint32_t a2, uint32_t a3, uint64_t c01, uint64_t c23,
+                                           uint32_t a1, uint32_t a2, uint32_t a3, const Inc& inc,
                                            uint32_t m, uint32_t& zmin, uint64_t& u) {
   uint64_t k1, k2, k3;
   asm volatile(SA_PCG_DRAW_ASM
@@ -93,16 +93,16 @@ __global__ void __launch_bounds__(256) k_smem(uint64_t* out, int iters, uint32_t
   for (int it = 0; it < iters; it++) {
     cptr_t f = cp;
     asm volatile("" : "+s"(f));
-    uint64_t n01 = f[0], n23 = f[1], nm = f[4];
+    Inc ninc{f[0], f[2], f[1]};
+    uint64_t nm = f[4];
 #pragma unroll
     for (int q = 0; q < P; q++) {
-      uint64_t c01 = n01, c23 = n23;
+      Inc cinc = ninc;
       uint32_t sm = (uint32_t)nm;
       if constexpr (!PREF) {
         cptr_t g = cp + 8 * q;
         asm volatile("" : "+s"(g));
-        c01 = g[0];
-        c23 = g[1];
+        cinc = Inc{g[0], g[2], g[1]};
         sm = (uint32_t)g[4];
       }
 #pragma unroll
@@ -110,17 +110,16 @@ __global__ void __launch_bounds__(256) k_smem(uint64_t* out, int iters, uint32_t
         if constexpr (PAIRS) {
           constexpr int PI = Pairs<L>::count;
           const int cu = Pairs<L>::u(q % PI), cv = Pairs<L>::v(q % PI);
-          draw_pair_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, c01, c23, sm, zmin, acc2[k][cu],
+          draw_pair_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, cinc, sm, zmin, acc2[k][cu],
                       acc2[k][cv]);
         } else {
           const int cu = q % L;
-          draw_one_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, c01, c23, sm, zmin, acc2[k][cu]);
+          draw_one_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, cinc, sm, zmin, acc2[k][cu]);
         }
         if (PREF && k == 0 && q + 1 < P) {
           cptr_t g = cp + 8 * (q + 1);
           asm volatile("" : "+s"(g));
-          n01 = g[0];
-          n23 = g[1];
+          ninc = Inc{g[0], g[2], g[1]};
           nm = g[4];
         }
       }
@@ -161,15 +160,15 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
   uint32_t zmin = 0xFFFFFFFFu;
   cptr_t cp = (cptr_t)gconst;
   for (int it = 0; it < iters; it++) {
-    uint64_t n01[2], n23[2], nm[2];
+    Inc ninc[2];
+    uint64_t nm[2];
     auto fetch = [&](int g) {
       for (int h = 0; h < 2; h++) {
         const int q = h == 0 ? S.g[g].qa : S.g[g].qb;
         if (q < 0) continue;
         cptr_t c = cp + 8 * q;
         asm volatile("" : "+s"(c));
-        n01[h] = c[0];
-        n23[h] = c[1];
+        ninc[h] = Inc{c[0], c[2], c[1]};
         nm[h] = c[4];
       }
     };
@@ -177,7 +176,7 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
 #pragma unroll
     for (int g = 0; g < S.n; g++) {
       const Group G = S.g[g];
-      const uint64_t ca = n01[0], da = n23[0], cb = n01[1], db = n23[1];
+      const Inc ia = ninc[0], ib = ninc[1];
       const uint32_t ma = (uint32_t)nm[0], mb = (uint32_t)nm[1];
 #pragma unroll
       for (int k = 0; k < 2; k++) {
@@ -186,17 +185,17 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
         const uint32_t fma_ = ma ^ (G.fa ? 0xFFFFFFFFu : 0u), fmb_ = mb ^ (G.fb ? 0xFFFFFFFFu : 0u);
         if (G.qb < 0) {
           if (G.va >= 0 && G.va_add)
-            pcg_draw_pair_a(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, fma_, zmin, ak[G.ua],
+            pcg_draw_pair_a(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua],
                             ak[G.va]);
           else if (G.va >= 0)
-            pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, fma_, zmin, ak[G.ua],
+            pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua],
                           ak[G.va]);
           else
-            pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ca, da, fma_, zmin, ak[G.ua]);
+            pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua]);
         } else {
           uint32_t* sb = st[G.qb];
 #define DRAW2(fn)                                                                                              \
-  fn(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca, da, fma_, cb, db, fmb_, \
+  fn(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_,         \
      zmin, ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb])
           if (G.va >= 0 && G.va_add && G.vb_add)
             DRAW2(pcg_draw2_pair_aa);
@@ -208,11 +207,11 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
             DRAW2(pcg_draw2_pair_ss);
 #undef DRAW2
           else if (G.ua == G.ub)
-            pcg_draw2_one_same(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca,
-                               da, fma_, cb, db, fmb_, zmin, ak[G.ua]);
+            pcg_draw2_one_same(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia,
+                               fma_, ib, fmb_, zmin, ak[G.ua]);
           else
-            pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ca, da,
-                          fma_, cb, db, fmb_, zmin, ak[G.ua], ak[G.ub]);
+            pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia,
+                          fma_, ib, fmb_, zmin, ak[G.ua], ak[G.ub]);
         }
         if (k == 0 && g + 1 < S.n) fetch(g + 1);
       }
@@ -311,13 +310,12 @@ __global__ void __launch_bounds__(256) k_draws(uint64_t* out, int iters, uint32_
     st[j][2] = tid + 13u * j;
     st[j][3] = ~tid;
   }
-  uint64_t rc01[MODE == 0 ? P : 1], rc23[MODE == 0 ? P : 1];
+  Inc rinc[MODE == 0 ? P : 1];
   uint32_t rm[MODE == 0 ? P : 1];
   if constexpr (MODE == 0) {
 #pragma unroll
     for (int j = 0; j < P; j++) {
-      rc01[j] = sl[j].inc_lo;
-      rc23[j] = sl[j].inc_hi;
+      rinc[j] = Inc{(uint32_t)sl[j].inc_lo, sl[j].inc_lo >> 32, sl[j].inc_hi};
       rm[j] = (uint32_t)sl[j].smask;
     }
   }
@@ -329,28 +327,26 @@ __global__ void __launch_bounds__(256) k_draws(uint64_t* out, int iters, uint32_
   for (int it = 0; it < iters; it++) {
 #pragma unroll
     for (int q = 0; q < P; q++) {
-      uint64_t c01, c23;
+      Inc cinc;
       uint32_t sm;
       if constexpr (MODE == 0) {
-        c01 = rc01[q];
-        c23 = rc23[q];
+        cinc = rinc[q];
         sm = rm[q];
       } else {
         asm volatile("" : "+v"(slp));
         typedef __attribute__((address_space(3))) const uint64_t* lds_u64;
         const lds_u64 cp = (lds_u64)(slp + q);
-        c01 = cp[0];
-        c23 = cp[1];
+        cinc = Inc{(uint32_t)cp[0], cp[0] >> 32, cp[1]};
         sm = (uint32_t)slp[q].smask;
       }
       if constexpr (PAIRS) {
         constexpr int PI = Pairs<L>::count;
         const int cu = Pairs<L>::u(q % PI), cv = Pairs<L>::v(q % PI);
-        pcg_draw_pair(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, c01, c23, sm, zmin, acc1[cu],
+        pcg_draw_pair(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, cinc, sm, zmin, acc1[cu],
                       acc1[cv]);
       } else {
         const int cu = q % L;
-        pcg_draw_one(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, c01, c23, sm, zmin, acc1[cu]);
+        pcg_draw_one(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, cinc, sm, zmin, acc1[cu]);
       }
     }
   }
@@ -377,7 +373,7 @@ int main() {
     for (int j = 0; j < 64; j++) {
       h[8 * j + 0] = 2ull * j + 7;
       h[8 * j + 1] = (uint64_t)j << 7;
-      h[8 * j + 2] = 3ull * j;
+      h[8 * j + 2] = 3ull * j;  // the increment's second word (zero-extended)
       h[8 * j + 3] = 0;
       h[8 * j + 4] = (j & 1) ? ~0ull : 0ull;
       h[8 * j + 5] = h[8 * j + 6] = h[8 * j + 7] = 0;
