@@ -66,12 +66,70 @@ def cpu_baseline(C: int, fxp_bits: int, seconds: float) -> dict:
     n = int(max(200_000, min(50_000_000, 200_000 * seconds / max(t_cal, 1e-6))))
     t = run(n)
     try:
+        par = cpu_baseline_parallel(C, fxp_bits, n)
+    except Exception as e:  # the single-threaded figure stands on its own
+        par = {"error": repr(e)}
+    try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         cores = os.cpu_count()
     return {"value": C * n / t, "unit": "grad elems/s", "cores": 1, "kind": "port",
             "sample": f"{C} clients x {n} fp32 elems, oracle/secagg.py numpy (single-threaded), "
                       f"{t:.1f} s; host has {cores} cores available",
+            "seconds": round(t, 3), "parallel": par}
+
+
+def _cpu_party(args):
+    """One client of the parallel CPU baseline: quantize + its C-1 pairwise
+    masks (oracle/secagg.py numpy, single-threaded), the masked vector written
+    into the shared server buffer.  Returns its timed region (monotonic)."""
+    c, C, n, fxp_bits, shm_name = args
+    from multiprocessing import shared_memory
+
+    import numpy as np
+
+    from oracle import secagg as o
+
+    names = [f"client{i}" for i in range(C)]
+    seeds = {b: pair_seed(c, j) for j, b in enumerate(names) if j != c}
+    x = np.random.default_rng(20260116 + c).standard_normal(n, dtype=np.float32) * np.float32(1e-2)
+    t0 = time.perf_counter()
+    m = o.mask_client(o.quantize(x, None, fxp_bits), names[c], seeds)
+    shm = shared_memory.SharedMemory(name=shm_name)
+    np.ndarray((C, n), dtype=np.uint64, buffer=shm.buf)[c] = m
+    t1 = time.perf_counter()
+    del m
+    shm.close()
+    return t0, t1
+
+
+def cpu_baseline_parallel(C: int, fxp_bits: int, n: int) -> dict:
+    """SURVEY.md §8d's second CPU figure: one process per client (C cores, as
+    the reference runs one party per process), masked vectors into shared
+    memory, then the server sum.  Forked before this process touches the GPU."""
+    import multiprocessing as mp
+    from multiprocessing import shared_memory
+
+    import numpy as np
+
+    from oracle import secagg as o
+
+    shm = shared_memory.SharedMemory(create=True, size=C * n * 8)
+    try:
+        with mp.get_context("fork").Pool(C) as pool:
+            spans = pool.map(_cpu_party, [(c, C, n, fxp_bits, shm.name) for c in range(C)])
+        masked = np.ndarray((C, n), dtype=np.uint64, buffer=shm.buf)
+        t0 = time.perf_counter()
+        o.server_sum(list(masked))
+        t_sum = time.perf_counter() - t0
+        del masked
+    finally:
+        shm.close()
+        shm.unlink()
+    t = max(b for _, b in spans) - min(a for a, _ in spans) + t_sum
+    return {"value": C * n / t, "unit": "grad elems/s", "cores": C, "kind": "port",
+            "sample": f"{C} client processes x {n} fp32 elems (oracle/secagg.py numpy), masked vectors in "
+                      f"shared memory, then the server sum; {t:.1f} s",
             "seconds": round(t, 3)}
 
 
@@ -118,6 +176,14 @@ def main():
                     help="N>1: masking/reduce pipeline depth (default 8; 1 = reduce after the whole launch)")
     args = ap.parse_args()
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    # CPU baseline first: its per-client worker processes are forked, which
+    # must happen before this process initialises the GPU
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
+        cpu = cpu_baseline(args.clients, args.fxp_bits, args.cpu_baseline_seconds)
+
     import torch
     import torch.distributed as dist
 
@@ -125,8 +191,6 @@ def main():
     from sfl_amd import kernels as K
     from sfl_amd.parallel_sum import PipelinedMaskedSum, RcclComm, plan_generators, plan_rank
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
@@ -222,10 +286,8 @@ def main():
     }
     if args.extra and world == 1:
         out["extra"] = extra_measurements(args, xs, plan, gens, K, torch, dev)
-    if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(C, args.fxp_bits, args.cpu_baseline_seconds)
-    elif rank == 0:
-        out["cpu_baseline"] = None
+    if rank == 0:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:
