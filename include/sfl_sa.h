@@ -217,7 +217,9 @@ int sa_mask_dp(const float* x, uint64_t n, double weight, int fxp_bits, const sa
 int sa_comm_unique_id(void* id_out, int cap);
 int sa_comm_init(void** comm, const void* id, int nranks, int rank, int device);
 /* ncclReduce(ncclUint64, ncclSum): recv (on root) = sum over ranks of send.
- * Bit-exact for any RCCL algorithm: uint64 add is associative mod 2^64. */
+ * Bit-exact for any RCCL algorithm: uint64 add is associative mod 2^64.
+ * recv may be NULL on non-root ranks: the reduce then runs in place on send
+ * (the call pattern torch.distributed.reduce uses), never on a null buffer. */
 int sa_comm_reduce_u64(void* comm, const uint64_t* send, uint64_t* recv, uint64_t n, int root,
                        void* stream);
 int sa_comm_allreduce_u64(void* comm, const uint64_t* send, uint64_t* recv, uint64_t n,

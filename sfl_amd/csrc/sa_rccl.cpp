@@ -54,7 +54,10 @@ extern "C" int sa_comm_reduce_u64(void* comm, const uint64_t* send, uint64_t* re
     sa_set_error("sa_comm_reduce_u64: bad arguments");
     return SA_ERR_ARG;
   }
-  SA_NCCL_CHECK(ncclReduce(send, recv, (size_t)n, ncclUint64, ncclSum, root, (ncclComm_t)comm,
+  // non-root ranks without a receive buffer reduce in place: RCCL is handed
+  // a valid buffer on every rank whatever algorithm it picks
+  uint64_t* rb = recv ? recv : const_cast<uint64_t*>(send);
+  SA_NCCL_CHECK(ncclReduce(send, rb, (size_t)n, ncclUint64, ncclSum, root, (ncclComm_t)comm,
                            (hipStream_t)stream));
   return SA_OK;
 }
