@@ -251,11 +251,6 @@ __device__ __forceinline__ uint64_t exact_q(const Vec2<XT> (&xv)[L], const Vec2<
 // PCG64 draw
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ u128 ld128(uint64_t lo, uint64_t hi) { return mk128(hi, lo); }
-__device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) {
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  const u32x2 v = {lo, hi};
-  return __builtin_bit_cast(uint64_t, v);
-}
 // a wave-uniform value as an opaque VGPR (kept resident, never re-materialised)
 __device__ __forceinline__ uint32_t vreg(uint32_t x) {
   uint32_t r;
