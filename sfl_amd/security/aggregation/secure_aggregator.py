@@ -172,6 +172,9 @@ class SecureAggregator(Aggregator):
         # layers are masked in order with one stream position per (party, peer),
         # exactly like the reference's per-layer rng.integers calls
         sizes = [int(np.prod(sh)) if sh else 1 for sh in shapes]
+        if self._host_fusable(data, layer_lists, as_torch, weights, sum(sizes)):
+            return self._aggregate_host_fused(data, layer_lists, sizes, shapes, weights, average, is_list,
+                                              payloads, flags, digests_keep)
         if (nl > 1 and not as_torch and (weights is None or all(np.ndim(w) == 0 for w in weights))
                 and all(len({np.asarray(a).dtype for a in ll}) == 1 for ll in layer_lists)):
             # host payloads of one dtype: pack on the host, one H2D copy per party
@@ -200,6 +203,77 @@ class SecureAggregator(Aggregator):
 
         return self._finish(data, groups, shapes, weights, average, as_torch, is_list, payloads, flags,
                             masked_keep, digests_keep)
+
+    # ------------------------------------------- host payloads, one launch
+    def _host_fusable(self, data, layer_lists, as_torch, weights, n) -> bool:
+        """Host float32 payloads of co-located parties with scalar weights that
+        keep float32 arithmetic: the latency path below applies (FL rounds
+        of small models)."""
+        if as_torch or not self._fused or self._keep_masked or n == 0:
+            return False
+        if not 2 <= len(data) <= MAX_FUSED_CLIENTS:
+            return False
+        sgpu = self._device.gpu
+        if any(d.device.gpu != sgpu for d in data):
+            return False
+        f32 = np.dtype(np.float32)
+        for i, ll in enumerate(layer_lists):
+            if any(_np_dtype(a) != f32 for a in ll):
+                return False
+            w = None if weights is None else weights[i]
+            if w is not None and (np.ndim(w) != 0 or _compute_dtype(f32, w, self._fxp_bits) != f32):
+                return False
+        return True
+
+    def _staging(self, C: int, n_pad: int, sdev):
+        """Pinned host / device buffers reused across rounds of the same size."""
+        key = (C, n_pad, str(sdev))
+        if getattr(self, "_stage_key", None) != key:
+            self._stage_in = torch.empty((C, n_pad), dtype=torch.float32, pin_memory=True)
+            self._dev_in = torch.empty((C, n_pad), dtype=torch.float32, device=sdev)
+            self._stage_out = torch.empty(n_pad, dtype=torch.float64, pin_memory=True)
+            self._stage_flags = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            self._stage_key = key
+        return self._stage_in, self._dev_in, self._stage_out
+
+    def _aggregate_host_fused(self, data, layer_lists, sizes, shapes, weights, average, is_list, payloads,
+                              flags, digests_keep):
+        """Every party's layers packed into one pinned [C, n] block, ONE H2D
+        copy, the fused masking launch (same kernels and stream positions as
+        the general path: bit-identical), decode, ONE D2H copy of the result
+        (and of the 4-byte PRG flag), one synchronisation."""
+        sdev = self._device.torch_device
+        C, n = len(data), sum(sizes)
+        n_pad = -(-n // 4) * 4  # rows start 16-byte aligned
+        stage_in, dev_in, stage_out = self._staging(C, n_pad, sdev)
+        host = stage_in.numpy()
+        for c, ll in enumerate(layer_lists):
+            np.concatenate([np.asarray(a, dtype=np.float32).reshape(-1) for a in ll], out=host[c, :n])
+        with torch.cuda.device(sdev):
+            dev_in.copy_(stage_in, non_blocking=True)
+            xs = [dev_in[c, :n] for c in range(C)]
+            ws = [1.0 if weights is None else float(w) for w in (weights or [None] * C)]
+            s = self._masked_sum(data, xs, [np.dtype(np.float32)] * C, ws, [None] * C, n, flags, [],
+                                 digests_keep)
+            divisor = 1.0
+            if average:
+                divisor = float(C) if weights is None else float(sum(weights))
+            dec = torch.empty(n, dtype=torch.float64, device=sdev)
+            K.decode(s, dec, fxp_bits=self._fxp_bits, divisor=divisor)
+            stage_out[:n].copy_(dec, non_blocking=True)
+            self._stage_flags.copy_(flags, non_blocking=True)
+            torch.cuda.current_stream(sdev).synchronize()
+        out = stage_out.numpy()[:n].copy()
+        if int(self._stage_flags[0]) & L.SA_FLAG_PRG_REJECT:
+            raise L.SALibraryError(
+                "a PCG64 raw draw was 0 (p=2^-64): numpy would have re-drawn; re-run with the stream "
+                "re-positioned")
+        self.last_digests = digests_keep
+        parts = np.split(out, np.cumsum(sizes)[:-1])
+        result = [p.reshape(sh) for p, sh in zip(parts, shapes)]
+        if not is_list:
+            return PYUObject(self._device, result[0])
+        return PYUObject(self._device, tuple(result) if isinstance(payloads[0], tuple) else result)
 
     def _finish(self, data, groups, shapes, weights, average, as_torch, is_list, payloads, flags, masked_keep,
                 digests_keep):
