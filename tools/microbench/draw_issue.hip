@@ -227,6 +227,99 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
   out[tid] = acc;
 }
 
+// k_dual with E elements per lane and a min-waves/SIMD launch bound W: does
+// a third wave per SIMD pay for the 8-client pair schedule at E = 1?
+template <int L, int X, int E, int W>
+__global__ void __launch_bounds__(256, W) k_dualE(uint64_t* out, int iters, uint32_t seed, const uint64_t* gconst) {
+  constexpr Sched<L, X> S{};
+  constexpr int P = Sched<L, X>::P;
+  extern __shared__ char dyn[];
+  if (dyn[0] == 123 && seed == 77) out[0] = 1;
+  uint32_t st[P][4];
+  const uint32_t tid = threadIdx.x + blockIdx.x * blockDim.x;
+#pragma unroll
+  for (int j = 0; j < P; j++) {
+    st[j][0] = tid * 0x9E3779B9u + j;
+    st[j][1] = seed ^ (j * 77u);
+    st[j][2] = tid + 13u * j;
+    st[j][3] = ~tid;
+  }
+  const uint32_t mk[4] = {vreg(A0 + seed), vreg(A1), vreg(A2), vreg(A3)};  // E = 1: the tile-jump limbs only
+  uint64_t acc2[E][L];
+#pragma unroll
+  for (int k = 0; k < E; k++)
+#pragma unroll
+    for (int c = 0; c < L; c++) acc2[k][c] = c + k;
+  uint32_t zmin = 0xFFFFFFFFu;
+  cptr_t cp = (cptr_t)gconst;
+  for (int it = 0; it < iters; it++) {
+    Inc ninc[2];
+    uint64_t nm[2];
+    auto fetch = [&](int g) {
+      for (int h = 0; h < 2; h++) {
+        const int q = h == 0 ? S.g[g].qa : S.g[g].qb;
+        if (q < 0) continue;
+        cptr_t c = cp + 8 * q;
+        asm volatile("" : "+s"(c));
+        ninc[h] = Inc{c[0], c[2], c[1]};
+        nm[h] = c[4];
+      }
+    };
+    fetch(0);
+#pragma unroll
+    for (int g = 0; g < S.n; g++) {
+      const Group G = S.g[g];
+      const Inc ia = ninc[0], ib = ninc[1];
+      const uint32_t ma = (uint32_t)nm[0], mb = (uint32_t)nm[1];
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        uint32_t* sa = st[G.qa];
+        uint64_t* ak = acc2[k];
+        const uint32_t fma_ = ma ^ (G.fa ? 0xFFFFFFFFu : 0u), fmb_ = mb ^ (G.fb ? 0xFFFFFFFFu : 0u);
+        if (G.qb < 0) {
+          if (G.va >= 0 && G.va_add)
+            pcg_draw_pair_a(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua],
+                            ak[G.va]);
+          else if (G.va >= 0)
+            pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua],
+                          ak[G.va]);
+          else
+            pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua]);
+        } else {
+          uint32_t* sb = st[G.qb];
+#define DRAW2(fn)                                                                                              \
+  fn(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_,         \
+     zmin, ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb])
+          if (G.va >= 0 && G.va_add && G.vb_add)
+            DRAW2(pcg_draw2_pair_aa);
+          else if (G.va >= 0 && G.va_add)
+            DRAW2(pcg_draw2_pair_as);
+          else if (G.va >= 0 && G.vb_add)
+            DRAW2(pcg_draw2_pair_sa);
+          else if (G.va >= 0)
+            DRAW2(pcg_draw2_pair_ss);
+#undef DRAW2
+          else if (G.ua == G.ub)
+            pcg_draw2_one_same(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia,
+                               fma_, ib, fmb_, zmin, ak[G.ua]);
+          else
+            pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia,
+                          fma_, ib, fmb_, zmin, ak[G.ua], ak[G.ub]);
+        }
+        if (k == 0 && g + 1 < S.n) fetch(g + 1);
+      }
+    }
+  }
+  uint64_t acc = zmin;
+#pragma unroll
+  for (int k = 0; k < E; k++)
+#pragma unroll
+    for (int c = 0; c < L; c++) acc += acc2[k][c];
+#pragma unroll
+  for (int j = 0; j < P; j++) acc ^= st[j][0] ^ st[j][3];
+  out[tid] = acc;
+}
+
 // Throughput of the draw's instruction MIX with no dependencies between
 // instructions of one iteration: 6 v_mad_u64_u32 + 4 v_mul_lo_u32 + 22 simple
 // ops (adds / bitop3 / alignbit / cndmask-like) per "draw" -- the issue
@@ -414,6 +507,9 @@ int main() {
   if (run(k_dual<1, 7>, 14, "dual one7 E2", 1000, gc)) return 1;
   if (run(k_dual<8, 0>, 56, "dual pair28 E2", 250, gc)) return 1;
   if (run(k_dual<4, 4>, 44, "dual 4+4x4 E2", 300, gc)) return 1;
+  if (run(k_dualE<8, 0, 1, 2>, 28, "dual pair28 E1 W2", 500, gc)) return 1;
+  if (run(k_dualE<8, 0, 1, 3>, 28, "dual pair28 E1 W3", 500, gc)) return 1;
+  if (run(k_dualE<8, 0, 2, 3>, 56, "dual pair28 E2 W3", 250, gc)) return 1;
   if (run(k_smem<7, 1, false, true, 4>, 28, "one7 L1 smem E4", 1000, gc)) return 1;
   if (run(k_smem<7, 1, false, true, 1>, 7, "one7 L1 smem E1", 4000, gc)) return 1;
   if (run(k_smem<7, 1, false, true, 2>, 14, "one7 L1 smem E2", 2000, gc)) return 1;
