@@ -705,6 +705,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
     const QScale qs{ka->scale_f, ka->scale_d, ka->fxp_bits};
     // elements past n only occur in the wave's last tile (uniform test)
     const bool wave_full = base + wave_off + 64 * kE <= n;
+    const uint32_t mmask = ka->masked_mask;
     uint64_t sum[kE] = {0, 0};
     auto finish = [&](int c, uint64_t q0, uint64_t q1) {
       const uint64_t a0 = negated<L>(c) ? q0 - acc[0][c] : acc[0][c] + q0;
@@ -718,8 +719,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
         else
           dig[kDigLds ? 0 : c] ^= d;
       }
-      uint64_t* mo = ka->c[c].masked_out;
-      if (mo) bstore2_u64(make_rsrc(mo, n * 8), i, a0, a1);
+      if ((mmask >> c) & 1) bstore2_u64(make_rsrc(ka->c[c].masked_out, n * 8), i, a0, a1);
     };
     static_assert(kE == 2, "finish() takes the lane's two elements");
     float p[L][kE];
@@ -823,6 +823,9 @@ int launch_clients(const KArgs& in, void* stream) {
         a.s[j].s_hi = hi64(s);
       }
     }
+    a.masked_mask = 0;
+    for (int c = 0; c < L; c++)
+      if (a.c[c].masked_out) a.masked_mask |= 1u << c;
     const uint64_t tiles = (a.n + kTile - 1) / kTile;
     const int grid = (int)(tiles < (uint64_t)maxb ? tiles : (uint64_t)maxb);
     if (grid >= (1 << kGridBits)) {

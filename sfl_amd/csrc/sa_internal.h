@@ -61,6 +61,9 @@ struct KArgs {
   int32_t sum_mode;       // 0 none, 1 store, 2 accumulate
   int32_t continue_mode;  // acc starts from masked_out instead of quantize(x)
   int32_t do_digest;
+  // bit c set iff c[c].masked_out is non-null (filled by the launcher): the
+  // tile's finish tests one SGPR instead of loading every client's pointer
+  uint32_t masked_mask;
   // GaussianModelDP pre-step fused into quantize (single-client fp32 only)
   int32_t dp_on;
   float dp_clip, dp_sigma, dp_updates;
