@@ -10,11 +10,14 @@ summed into the server's uint64 masked sum.  Rate = C*N / step time
 
 N=1 (default): all 8 clients on one MI355X in ONE fused launch
 (sa_fused_clients: L=8 local clients, 28 pair streams each expanded once).
-N>1 (torchrun, one process per GPU): clients sharded in contiguous blocks
-(8/N per GPU, config 3 at N=8); each rank runs one fused launch over its
-clients (internal pairs + cross streams) and the uint64 partial sums are
-reduced to rank 0 (the server) with ncclReduce over xGMI.  Total work is
-fixed as N grows: "scaling": "strong".
+N>1: one process per GPU, clients sharded in contiguous blocks (8/N per
+GPU, config 3 at N=8); each rank runs the fused masking over its clients
+(internal pairs + cross streams), pipelined in chunks against ncclReduce of
+the uint64 partial sums to rank 0 (the server) over xGMI.  Total work is
+fixed as N grows: "scaling": "strong".  `python bench.py --gpus N` starts
+its N rank processes itself (torch.distributed.run as a child process,
+before this process touches the GPU); under an outer torchrun (WORLD_SIZE
+set) it runs as one rank.
 
 Inputs: synthetic N(0, 0.01^2) fp32 gradients generated on the GPU
 (torch.Generator seeded 20260116+c); pair seeds (0x5ECA66<<32)|(u<<16)|v as
@@ -35,8 +38,12 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PCG_PEAK_DRAWS = 1.57e12        # measured PCG64 draw-loop ceiling (one-sided draws, 8 waves/SIMD),
-                                # tools/microbench/draw_issue.hip "dual one7 E2", profiles/r01/draw_issue_microbench.txt
+# Measured PCG64 draw-loop ceilings (tools/microbench/draw_issue.hip,
+# profiles/r01/draw_issue_microbench.txt), the draw loop alone with the
+# product kernel's operand layout and schedule:
+PCG_PAIR_DRAWS_2WAVE = 1.34e12  # pair draws (both ends accumulated), 2 waves/SIMD = the L=8 kernel's
+                                # occupancy ("dual pair28 E2", best of 1.29-1.34e12 run to run)
+PCG_ONE_DRAWS_8WAVE = 1.57e12   # one-sided draws at 8 waves/SIMD ("dual one7 E2")
 
 
 def pair_seed(u: int, v: int) -> int:
@@ -44,7 +51,20 @@ def pair_seed(u: int, v: int) -> int:
     return (0x5ECA66 << 32) | (a << 16) | b
 
 
-def cpu_baseline(C: int, fxp_bits: int, seconds: float) -> dict:
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(C: int, fxp_bits: int, seconds: float, parallel: bool = True) -> dict:
     """The numpy restatement (oracle/, kind "port") timed on this host on a
     bounded sample of the same workload: C clients, n_sample elements each."""
     import numpy as np
@@ -65,10 +85,12 @@ def cpu_baseline(C: int, fxp_bits: int, seconds: float) -> dict:
     t_cal = run(200_000)
     n = int(max(200_000, min(50_000_000, 200_000 * seconds / max(t_cal, 1e-6))))
     t = run(n)
-    try:
-        par = cpu_baseline_parallel(C, fxp_bits, n)
-    except Exception as e:  # the single-threaded figure stands on its own
-        par = {"error": repr(e)}
+    par = None
+    if parallel:
+        try:
+            par = cpu_baseline_parallel(C, fxp_bits, n)
+        except Exception as e:  # the single-threaded figure stands on its own
+            par = {"error": repr(e)}
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
@@ -76,6 +98,7 @@ def cpu_baseline(C: int, fxp_bits: int, seconds: float) -> dict:
     return {"value": C * n / t, "unit": "grad elems/s", "cores": 1, "kind": "port",
             "sample": f"{C} clients x {n} fp32 elems, oracle/secagg.py numpy (single-threaded), "
                       f"{t:.1f} s; host has {cores} cores available",
+            "cpu_model": cpu_model(), "cores_available": cores,
             "seconds": round(t, 3), "parallel": par}
 
 
@@ -133,30 +156,131 @@ def cpu_baseline_parallel(C: int, fxp_bits: int, n: int) -> dict:
             "seconds": round(t, 3)}
 
 
-PMC_DIR = os.path.join(ROOT, "profiles", "r01")
+PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r02", "r01")]  # newest first
+PMC_ELEMS = 100_000_000  # element positions per launch of the committed PMC passes
 
 
-def pmc_traffic(kernel: str) -> dict | None:
+def pmc_traffic(kernel: str, elems_per_launch: int) -> dict | None:
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (tools/gpu_profile.sh: separate FETCH_SIZE / WRITE_SIZE runs of
-    tools/kernel_bench.py on this workload).  Units are KiB; gfx950 reports
+    tools/kernel_bench.py, every per-rank shape at 100M element positions per
+    launch), scaled to this run's launch size (the kernel streams: its bytes
+    are linear in the element count).  Units are KiB; gfx950 reports
     FETCH_SIZE at half the bytes of 16-B/lane streaming reads, so it is
     doubled (MI355X_MICROARCH.md, HBM); both corrections were checked on the
     k_sum_u64 calibration launch in the same runs (known bytes)."""
     import csv
 
-    vals = {}
-    for counter, fname, scale in (("FETCH_SIZE", "pmc_fetch_size.csv", 2.0), ("WRITE_SIZE", "pmc_write_size.csv", 1.0)):
-        path = os.path.join(PMC_DIR, fname)
-        if not os.path.exists(path):
-            return None
-        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-             if r["Kernel_Name"].startswith(kernel) and r["Counter_Name"] == counter]
-        if not v:
-            return None
-        vals[counter] = scale * 1024.0 * sum(v) / len(v)
-    return {"bytes": vals["FETCH_SIZE"] + vals["WRITE_SIZE"], "read": vals["FETCH_SIZE"], "write": vals["WRITE_SIZE"],
-            "source": os.path.relpath(PMC_DIR, ROOT) + "/pmc_{fetch,write}_size.csv"}
+    for d in PMC_DIRS:
+        vals = {}
+        for counter, fname, scale in (("FETCH_SIZE", "pmc_fetch_size.csv", 2.0),
+                                      ("WRITE_SIZE", "pmc_write_size.csv", 1.0)):
+            path = os.path.join(d, fname)
+            if not os.path.exists(path):
+                break
+            with open(path) as f:
+                v = [float(r["Counter_Value"]) for r in csv.DictReader(f)
+                     if r["Kernel_Name"].startswith(kernel) and r["Counter_Name"] == counter]
+            if not v:
+                break
+            vals[counter] = scale * 1024.0 * sum(v) / len(v) * elems_per_launch / PMC_ELEMS
+        if len(vals) == 2:
+            return {"bytes": vals["FETCH_SIZE"] + vals["WRITE_SIZE"], "read": vals["FETCH_SIZE"],
+                    "write": vals["WRITE_SIZE"],
+                    "source": os.path.relpath(d, ROOT) + "/pmc_{fetch,write}_size.csv",
+                    "scaled_from_elems": PMC_ELEMS}
+    return None
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` without an outer torchrun (WORLD_SIZE unset): measure the CPU
+    baseline here, then start the N rank processes as ONE child process
+    (torch.distributed.run, rendezvous on 127.0.0.1) and return its exit
+    code.  This process never touches the GPU (it imports no torch), so
+    nothing is exec'd from a process that initialised HIP."""
+    import subprocess
+    import tempfile
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    tmp = None
+    if args.cpu_baseline_seconds > 0:
+        cpu = cpu_baseline(args.clients, args.fxp_bits, rank_cpu_seconds(args, args.gpus),
+                           parallel=args.gpus == 1 and not args.dry_run)
+        fd, tmp = tempfile.mkstemp(prefix="sfl_bench_cpu_", suffix=".json")
+        with os.fdopen(fd, "w") as f:
+            json.dump(cpu, f)
+        env["SFL_BENCH_CPU_BASELINE"] = tmp
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    try:
+        return subprocess.run(cmd, env=env).returncode
+    finally:
+        if tmp:
+            os.unlink(tmp)
+
+
+def rank_cpu_seconds(args, world: int) -> float:
+    """CPU-baseline budget: the full sample at N=1; a short single-threaded
+    one at N>1 so the scaling runs stay short (it delays rank 0 only)."""
+    return args.cpu_baseline_seconds if world == 1 else min(3.0, args.cpu_baseline_seconds)
+
+
+def rank_cpu_baseline(args, world: int, rank: int):
+    """rank 0's CPU baseline, always measured before this process touches the
+    GPU: handed over by the launcher (launch_ranks) or measured here."""
+    if rank != 0 or args.cpu_baseline_seconds <= 0:
+        return None
+    path = os.environ.get("SFL_BENCH_CPU_BASELINE")
+    if path and os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return cpu_baseline(args.clients, args.fxp_bits, rank_cpu_seconds(args, world), parallel=world == 1)
+
+
+def dry_run(args, world: int, rank: int, cpu) -> None:
+    """Launcher rehearsal without a GPU (tests/test_bench_launcher.py): every
+    rank joins a gloo group and reports its pid; rank 0 prints one line."""
+    import torch.distributed as dist
+
+    multi = world > 1 or args.dist
+    ranks = [{"rank": rank, "pid": os.getpid(), "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}]
+    if multi:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        allr = [None] * world
+        dist.all_gather_object(allr, ranks[0])
+        ranks = allr
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "dry_run": True, "n_gpus": world, "ranks": ranks,
+                          "config": {"workload": workload(args, world)}, "cpu_baseline": cpu}), flush=True)
+
+
+METRIC = "grad elems/s device-resident: 100M-float quantize+mask+sum, 8 clients"
+
+
+def workload(args, world: int) -> str:
+    from sfl_amd.parallel_sum import client_shard
+
+    C, N = args.clients, args.elems
+    L = len(client_shard(C, world, 0))
+    X = C - L
+    pairs = L * (L - 1) // 2
+    if world == 1:
+        return (f"{C} clients x {N} fp32 grad elems on 1 GPU, fxp {args.fxp_bits}, ring 2^64: one fused launch "
+                f"k_clients<float,float,{L},{X}> ({pairs} pair streams)")
+    return (f"{C} clients x {N} fp32 grad elems over {world} GPUs, fxp {args.fxp_bits}, ring 2^64; per rank: "
+            f"{L} local client(s), {pairs} internal pair + {L * X} cross streams "
+            f"(k_clients<float,float,{L},{X}>), pipelined ncclReduce(uint64) of the partial sum to rank 0")
 
 
 def main():
@@ -170,19 +294,26 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0, help="0 disables")
     ap.add_argument("--extra", action="store_true", help="also time the wire chain and H2D/D2H-inclusive rate")
     ap.add_argument("--dist", action="store_true",
-                    help="run the multi-GPU code path (RCCL communicator, pipelined reduce) even at N=1 "
-                         "(rehearsal of the N>1 path on one GPU under torchrun)")
+                    help="run the multi-GPU code path (RCCL communicator, reduce) even at N=1 "
+                         "(rehearsal of the N>1 path on one GPU)")
     ap.add_argument("--chunks", type=int, default=None,
-                    help="N>1: masking/reduce pipeline depth (default 8; 1 = reduce after the whole launch)")
+                    help="masking/reduce pipeline depth (default 8 for N>1, 1 at N=1)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher rehearsal without a GPU: ranks join a gloo group, rank 0 prints one line")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dist):
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # CPU baseline first: its per-client worker processes are forked, which
     # must happen before this process initialises the GPU
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
-        cpu = cpu_baseline(args.clients, args.fxp_bits, args.cpu_baseline_seconds)
+    cpu = rank_cpu_baseline(args, world, rank)
+    if args.dry_run:
+        dry_run(args, world, rank, cpu)
+        return
 
     import torch
     import torch.distributed as dist
@@ -192,8 +323,6 @@ def main():
     from sfl_amd.parallel_sum import PipelinedMaskedSum, RcclComm, plan_generators, plan_rank
 
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     _lib.lib()
@@ -212,19 +341,20 @@ def main():
         g = torch.Generator(device=dev).manual_seed(20260116 + c)
         xs.append(torch.randn(N, generator=g, device=dev, dtype=torch.float32) * 1e-2)
     total_steps = args.warmup + args.steps
-    chunks = args.chunks if args.chunks is not None else (8 if multi else 1)
+    chunks = args.chunks if args.chunks is not None else (8 if world > 1 else 1)
     pipe = PipelinedMaskedSum(comm, dev, N, chunks)
     # every step is a new round: streams start i*N draws in, chunk j at +lo_j
     gens = [[plan_generators(plan, pair_seed, offset=i * N + lo) for lo, _ in pipe.bounds]
             for i in range(total_steps)]
+    # the partial sum is reduced IN PLACE (rank 0, the server, receives the
+    # masked sum in sum_buf; at N=1 the reduce is a no-op)
     sum_buf = torch.empty(N, dtype=torch.int64, device=dev)
-    recv = torch.empty(N, dtype=torch.int64, device=dev) if (rank == 0 and multi) else None
     digests = torch.zeros(Lc, dtype=torch.int64, device=dev)
     flags = torch.zeros(1, dtype=torch.int32, device=dev)
     kev = []  # (start, end) events around every masking launch of the timed steps (compute stream)
 
     def step(i, timed_idx=None):
-        pipe.run(xs, [1.0] * Lc, gens[i], plan.n_cross, sum_buf, recv, fxp_bits=args.fxp_bits,
+        pipe.run(xs, [1.0] * Lc, gens[i], plan.n_cross, sum_buf, None, fxp_bits=args.fxp_bits,
                  digests=digests, flags=flags, kernel_events=kev if timed_idx is not None else None)
 
     for i in range(args.warmup):
@@ -252,13 +382,14 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     value = C * N / (ms_per_step / 1e3)
     draws = (len(plan.pairs) + len(plan.cross)) * N
-    bytes_alg = 4 * Lc * N + 8 * N  # fp32 reads of the local clients + one u64 sum write
+    bytes_alg = 4 * Lc * N + 8 * N  # per step: fp32 reads of the local clients + one u64 sum write
+    launches = len(pipe.bounds)
     achieved = bytes_alg / (kern_ms / 1e3) / 1e9
     kname = f"k_clients<float, float, {Lc}, {plan.n_cross}>"  # the launch's kernel
-    # PMC bytes were collected on the default single-GPU workload only
-    pmc = pmc_traffic(f"void sa::{kname}") if (world, C, N) == (1, 8, 100_000_000) else None
+    pmc = pmc_traffic(f"void sa::{kname}", N // launches)
+    draws_s = draws / (kern_ms / 1e3)
     out = {
-        "metric": "grad elems/s device-resident: 100M-float quantize+mask+sum, 8 clients",
+        "metric": METRIC,
         "value": value,
         "unit": "grad elems/s",
         "n_gpus": world,
@@ -270,25 +401,30 @@ def main():
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (N(0,0.01^2) fp32 gradients generated on device)",
-        "config": {"workload": f"{C} clients x {N} fp32 grad elems, fxp {args.fxp_bits}, ring 2^64, "
-                               f"{'1 GPU fused' if world == 1 else f'{Lc} clients/GPU + RCCL reduce'}",
+        "config": {"workload": workload(args, world),
                    "clients": C, "elems_per_client": N, "clients_per_gpu": Lc,
-                   "parallelism": f"clients{world}", "pipeline_chunks": len(pipe.bounds)},
+                   "parallelism": f"clients{world}", "pipeline_chunks": launches},
+        # per launch: algorithmic bytes of one launch / its average duration
+        # (HIP events on the launch stream); the step's launches are equal
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": pmc["bytes"] if pmc else None, "traffic_detail": pmc,
-                     "kernel": f"{kname} (sa_fused_clients)", "kernel_ms": kern_ms,
-                     "launches_per_step": len(pipe.bounds),
-                     "algorithmic_bytes_per_launch": bytes_alg,
-                     "valu": {"pcg64_draws_per_launch": draws, "draws_per_s": draws / (kern_ms / 1e3),
-                              "peak_draws_per_s": PCG_PEAK_DRAWS,
-                              "frac": draws / (kern_ms / 1e3) / PCG_PEAK_DRAWS}},
+                     "kernel": f"{kname} (sa_fused_clients)", "kernel_ms_per_step": kern_ms,
+                     "launches_per_step": launches,
+                     "algorithmic_bytes_per_launch": bytes_alg / launches,
+                     "kernel_ms_per_launch": kern_ms / launches,
+                     "valu": {"pcg64_draws_per_step": draws, "draws_per_s": draws_s,
+                              "peak_draws_per_s": PCG_PAIR_DRAWS_2WAVE,
+                              "peak_note": "draw loop alone, pair draws at 2 waves/SIMD (the L=8 kernel's "
+                                           "occupancy); one-sided draws at 8 waves/SIMD reach "
+                                           f"{PCG_ONE_DRAWS_8WAVE:.3g}",
+                              "frac": draws_s / PCG_PAIR_DRAWS_2WAVE,
+                              "frac_vs_one_sided_8wave": draws_s / PCG_ONE_DRAWS_8WAVE}},
     }
     if args.extra and world == 1:
         out["extra"] = extra_measurements(args, xs, plan, gens, K, torch, dev)
     if rank == 0:
         out["cpu_baseline"] = cpu
-    if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:
         comm.close()
@@ -296,49 +432,115 @@ def main():
 
 
 def extra_measurements(args, xs, plan, gens, K, torch, dev) -> dict:
-    """Wire-faithful chain (each client's masked vector materialised, then the
-    server sum) and the host-resident rate (H2D of fp32 inputs + D2H of the
-    masked vectors, pinned buffers), both on one GPU."""
+    """Secondary rates on one GPU, none of them `value`:
+
+    * wire chain: every client's masked vector materialised by its own
+      sa_mask launch (7 streams each, no pair sharing), then sa_sum_u64;
+    * fused wire images: the fused launch storing every client's masked
+      vector as well (pair streams still expanded once);
+    * host-resident (PCIe-inclusive): fp32 inputs in pinned host memory,
+      results back in pinned host memory, chunked so that H2D, the fused
+      launch + decode and D2H overlap on three streams; once with only the
+      decoded float64 aggregate coming back, once also with every client's
+      masked u64 vector (the wire images a loopback party would send);
+    * the round-1 serial variant (per client H2D -> sa_mask -> D2H, one
+      stream) for comparison."""
     from sfl_amd import _lib as L
+    from sfl_amd.parallel_sum import chunk_bounds
 
     C, N = args.clients, args.elems
     names = [f"client{c}" for c in range(C)]
     outs = [torch.empty(N, dtype=torch.int64, device=dev) for _ in range(C)]
     s = torch.empty(N, dtype=torch.int64, device=dev)
+    res = {}
+
+    def timeit(fn, reps=3):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    def client_streams(c):
+        return [(L.pcg64_from_seed(pair_seed(c, v)), 1 if names[v] > names[c] else -1, v)
+                for v in range(C) if v != c]
 
     def wire():
         for c in range(C):
-            st = [(L.pcg64_from_seed(pair_seed(c, v)), 1 if names[v] > names[c] else -1, v)
-                  for v in range(C) if v != c]
-            K.mask(xs[c], outs[c], st)
+            K.mask(xs[c], outs[c], client_streams(c))
         K.sum_u64(outs, s)
 
-    wire()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    reps = 3
-    for _ in range(reps):
-        wire()
-    torch.cuda.synchronize()
-    t_wire = (time.perf_counter() - t0) / reps
-    res = {"wire_chain_ms": t_wire * 1e3, "wire_chain_grad_elems_per_s": C * N / t_wire}
+    t = timeit(wire)
+    res.update({"wire_chain_ms": t * 1e3, "wire_chain_grad_elems_per_s": C * N / t})
+    pg, ps, cross = plan_generators_full(plan)
 
-    host_x = [x.cpu().pin_memory() for x in xs]
-    host_m = [torch.empty(N, dtype=torch.int64).pin_memory() for _ in range(C)]
-    dev_x = [torch.empty_like(x) for x in xs]
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for c in range(C):
-        dev_x[c].copy_(host_x[c], non_blocking=True)
-        st = [(L.pcg64_from_seed(pair_seed(c, v)), 1 if names[v] > names[c] else -1, v)
-              for v in range(C) if v != c]
-        K.mask(dev_x[c], outs[c], st)
-        host_m[c].copy_(outs[c], non_blocking=True)
-    torch.cuda.synchronize()
-    t_h = time.perf_counter() - t0
-    res.update({"host_resident_ms": t_h * 1e3, "host_resident_grad_elems_per_s": C * N / t_h,
-                "host_resident_note": "H2D fp32 in + mask + D2H u64 masked vector per client, pinned, one stream"})
+    def fused_wire():
+        K.fused_clients(xs, [1.0] * C, pg, ps, cross, plan.n_cross, s, masked_outs=outs)
+
+    t = timeit(fused_wire)
+    res.update({"fused_wire_images_ms": t * 1e3, "fused_wire_images_grad_elems_per_s": C * N / t})
+
+    # ---- host-resident, overlapped
+    host_x = torch.stack([x.cpu() for x in xs]).pin_memory()        # [C, N] fp32
+    host_dec = torch.empty(N, dtype=torch.float64).pin_memory()
+    host_m = torch.empty((C, N), dtype=torch.int64).pin_memory()
+    dev_x = torch.empty((C, N), dtype=torch.float32, device=dev)
+    dec = torch.empty(N, dtype=torch.float64, device=dev)
+    s_h2d, s_cmp, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    bounds = chunk_bounds(N, 16)
+    cg = [plan_generators_full(plan, lo) for lo, _ in bounds]
+
+    def host_round(with_images: bool):
+        for j, (lo, hi) in enumerate(bounds):
+            e_in, e_k = torch.cuda.Event(), torch.cuda.Event()
+            with torch.cuda.stream(s_h2d):
+                dev_x[:, lo:hi].copy_(host_x[:, lo:hi], non_blocking=True)
+                e_in.record(s_h2d)
+            with torch.cuda.stream(s_cmp):
+                s_cmp.wait_event(e_in)
+                p, sg, cr = cg[j]
+                K.fused_clients([dev_x[c, lo:hi] for c in range(C)], [1.0] * C, p, sg, cr, plan.n_cross, s[lo:hi],
+                                masked_outs=[o[lo:hi] for o in outs] if with_images else None)
+                K.decode(s[lo:hi], dec[lo:hi])
+                e_k.record(s_cmp)
+            with torch.cuda.stream(s_d2h):
+                s_d2h.wait_event(e_k)
+                host_dec[lo:hi].copy_(dec[lo:hi], non_blocking=True)
+                if with_images:
+                    for c in range(C):
+                        host_m[c, lo:hi].copy_(outs[c][lo:hi], non_blocking=True)
+
+    for with_images in (False, True):
+        t = timeit(lambda: host_round(with_images), reps=2)
+        key = "host_resident_with_wire_images" if with_images else "host_resident"
+        h2d, d2h = 4 * C * N, 8 * N + (8 * C * N if with_images else 0)
+        res.update({f"{key}_ms": t * 1e3, f"{key}_grad_elems_per_s": C * N / t,
+                    f"{key}_pcie_bytes": {"h2d": h2d, "d2h": d2h}})
+    res["host_resident_note"] = ("pinned host fp32 inputs -> H2D -> fused quantize+mask+sum -> decode -> D2H of the "
+                                 "float64 aggregate (and of every client's masked u64 vector), 16 chunks, H2D / "
+                                 "compute / D2H on three streams")
+
+    # ---- round-1 serial variant
+    host_m1 = [host_m[c] for c in range(C)]
+
+    def serial():
+        for c in range(C):
+            dev_x[c].copy_(host_x[c], non_blocking=True)
+            K.mask(dev_x[c], outs[c], client_streams(c))
+            host_m1[c].copy_(outs[c], non_blocking=True)
+
+    t = timeit(serial, reps=1)
+    res.update({"host_serial_ms": t * 1e3, "host_serial_grad_elems_per_s": C * N / t,
+                "host_serial_note": "H2D fp32 in + sa_mask + D2H u64 masked vector per client, one stream"})
     return res
+
+
+def plan_generators_full(plan, offset: int = 0):
+    from sfl_amd.parallel_sum import plan_generators
+
+    return plan_generators(plan, pair_seed, offset=offset)
 
 
 if __name__ == "__main__":

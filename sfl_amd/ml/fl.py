@@ -4,7 +4,10 @@ reference so the aggregator can be swapped in exactly where FLModel uses it.
 
 Reference interfaces followed:
 
-* ``FLModel.fit`` aggregation hook -- every ``aggregate_freq`` local steps the
+* ``FLModel.fit`` aggregation hooks -- the initial weights of every worker
+  are averaged through the aggregator and installed everywhere before the
+  first epoch (``fl_model.py:473`` -> ``initialize_weights``, ``:126-138``);
+  every ``aggregate_freq`` local steps the
   clients' ``train_step`` outputs go to ``aggregator.average(params, axis=0,
   weights=sample_nums)`` and the result is sent back to every party
   (``sfl/ml/nn/fl/fl_model.py:492-517``, ``:578-583``); the last batch of an
@@ -330,8 +333,10 @@ class FLModel:
             for d in self.device_list}
 
     def initialize_weights(self):
-        """Average the clients' initial weights and install them everywhere
-        (reference fl_model.py:126-137)."""
+        """Average the clients' initial weights through the aggregator and
+        install the result on every worker (reference fl_model.py:126-138):
+        one secure aggregation before the first round, which also advances
+        every pair's mask streams by the model's parameter count."""
         ws = [PYUObject(d, w.get_weights()) for d, w in self._workers.items()]
         init = self._aggregator.average(ws, axis=0)
         for d, w in self._workers.items():
@@ -341,11 +346,17 @@ class FLModel:
     def fit(self, x: Dict[PYU, np.ndarray], y: Dict[PYU, np.ndarray], batch_size: int = 32, epochs: int = 1,
             aggregate_freq: int = 1, validation_data=None, round_hook: Callable | None = None) -> dict:
         """``round_hook(round_index, aggregated_params)`` is called after every
-        aggregation (the test oracle checks rounds with it)."""
+        aggregation, with index -1 for the initial-weights average (the test
+        oracle checks rounds with it)."""
         for d, w in self._workers.items():
             w.set_data(x[d], y[d], batch_size)
         steps = max(w.steps_per_epoch() for w in self._workers.values())
         history = {"train_loss": [], "val_loss": [], "val_accuracy": [], "aggregation_s": [], "round_s": []}
+        # reference fit (fl_model.py:473): the initial weights are averaged
+        # through the aggregator before the first epoch
+        init = self.initialize_weights()
+        if round_hook is not None:
+            round_hook(-1, reveal(init))
         rnd = 0
         for epoch in range(epochs):
             model_params_list = None

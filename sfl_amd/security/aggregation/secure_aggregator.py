@@ -81,7 +81,8 @@ class SecureAggregator(Aggregator):
             orders accepted); default is a Diffie-Hellman agreement.
         fused: allow the single-launch simulation of co-located clients.
         keep_masked: also materialise every party's masked vector (the wire
-            image) and expose the last ones as ``last_masked``.
+            image) and expose the last ones as ``last_masked``; co-located
+            parties still take the fused launch, which stores the images.
     """
 
     def __init__(self, device: PYU, participants: List[PYU], fxp_bits: int = 18, *,
@@ -373,7 +374,7 @@ class SecureAggregator(Aggregator):
         C = len(names)
         s = torch.empty(n, dtype=K.U64, device=sdev)
         digests = torch.zeros(C, dtype=K.U64, device=sdev)
-        fusable = (self._fused and not self._keep_masked and 2 <= C <= MAX_FUSED_CLIENTS
+        fusable = (self._fused and 2 <= C <= MAX_FUSED_CLIENTS
                    and all(p.gpu == server.gpu for p in parties)
                    and all(ct == np.dtype(np.float32) for ct in cts)
                    and all(x.dtype == torch.float32 for x in xs)
@@ -387,9 +388,14 @@ class SecureAggregator(Aggregator):
                     assert mu.position(names[v]) == mv.position(names[u]), "pair streams out of step"
                     pair_gens.append(mu.generator(names[v]))
                     pair_signs.append(mu.sign(names[v]))
+            # keep_masked: the same launch also stores every party's masked
+            # vector (the wire image) -- pair streams are still expanded once
+            masked = [torch.empty(n, dtype=K.U64, device=sdev) for _ in range(C)] if self._keep_masked else None
             with torch.cuda.device(sdev):
                 K.fused_clients(xs, ws, pair_gens, pair_signs, [], 0, s, fxp_bits=self._fxp_bits,
-                                digests=digests, flags=flags)
+                                digests=digests, flags=flags, masked_outs=masked)
+            if self._keep_masked:
+                masked_keep.append(masked)
         else:
             masked = []
             for ci, p in enumerate(parties):

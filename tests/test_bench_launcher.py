@@ -1,0 +1,76 @@
+"""bench.py's multi-GPU launch contract, rehearsed on the CPU (--dry-run: the
+ranks join a gloo group instead of touching a GPU).
+
+* ``python bench.py --gpus N`` with no outer torchrun starts N rank processes
+  itself (one torch.distributed.run child) and exactly ONE JSON line comes
+  back, from rank 0, carrying the CPU baseline the parent measured before
+  any rank started;
+* under an outer ``torch.distributed.run`` (the driver's form) every rank is
+  a worker and rank 0 measures the CPU baseline itself, before GPU init;
+* ``config.workload`` names the per-rank kernel shape.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _json_lines(out: str):
+    return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+
+
+def _env():
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    return env
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_self_launch_spawns_n_ranks_and_prints_one_line(n):
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--dry-run", "--cpu-baseline-seconds", "0.2"],
+                       capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["dry_run"] and line["n_gpus"] == n
+    ranks = line["ranks"]
+    assert sorted(x["rank"] for x in ranks) == list(range(n))
+    assert len({x["pid"] for x in ranks}) == n  # N distinct processes
+    assert all(x["pid"] != os.getpid() for x in ranks)
+    cpu = line["cpu_baseline"]
+    assert cpu["kind"] == "port" and cpu["cores"] == 1 and cpu["value"] > 0 and cpu["cpu_model"]
+    per = 8 // n
+    assert f"k_clients<float,float,{per},{8 - per}>" in line["config"]["workload"]
+
+
+def test_outer_torchrun_rank0_measures_cpu_baseline():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "2",
+                        "--dry-run", "--cpu-baseline-seconds", "0.2"],
+                       capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    assert lines[0]["n_gpus"] == 2 and lines[0]["cpu_baseline"]["value"] > 0
+
+
+def test_world_one_runs_in_process():
+    r = subprocess.run([sys.executable, BENCH, "--dry-run", "--cpu-baseline-seconds", "0"],
+                       capture_output=True, text=True, timeout=120, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    assert line["n_gpus"] == 1 and line["ranks"][0]["pid"] != os.getpid()
+    assert line["cpu_baseline"] is None
+    assert "k_clients<float,float,8,0>" in line["config"]["workload"]

@@ -93,6 +93,39 @@ def test_fl_round_with_oracle_aggregator_learns():
         assert all(np.array_equal(a, b) for a, b in zip(w0, fl.get_weights(p)))
 
 
+def test_fit_averages_initial_weights_first():
+    """Reference fit (fl_model.py:473 -> :126-138): the first aggregation is
+    the unweighted average of every worker's initial weights, installed on
+    every worker before the first round; later rounds are weighted by the
+    sample counts (:516-518)."""
+    from sfl_amd.device import PYU
+
+    class Recording(OracleAggregator):
+        def __init__(self, *a):
+            super().__init__(*a)
+            self.calls = []
+
+        def average(self, data, axis=0, weights=None):
+            self.calls.append((weights, [[np.array(a) for a in d.data] for d in data]))
+            return super().average(data, axis=axis, weights=weights)
+
+    pyus = [PYU(n, None) for n in NAMES]
+    agg = Recording(NAMES, o.seeds_for(NAMES))
+    hooks = []
+    _fl(agg, pyus, epochs=1, hook=lambda r, p: hooks.append(r))
+    assert hooks == [-1, 0, 1, 2]
+    assert len(agg.calls) == 4
+    w0, init_payloads = agg.calls[0]
+    assert w0 is None
+    # every worker was seeded alike (fl_base.py:51-52): identical initial weights
+    for p in init_payloads[1:]:
+        assert all(np.array_equal(a, b) for a, b in zip(init_payloads[0], p))
+    assert all(w == [32] * 8 for w, _ in agg.calls[1:])  # per-round sample counts (batch 32)
+    # the first round's global weights are the decoded init average (a 2^-18 grid), not the raw init
+    first_round_inputs = agg.calls[1][1]
+    assert not all(np.array_equal(a, b) for a, b in zip(init_payloads[0], first_round_inputs[0]))
+
+
 @pytest.mark.gpu
 def test_fl_round_hip_aggregator_bit_exact_vs_oracle():
     if not torch.cuda.is_available():
@@ -107,7 +140,7 @@ def test_fl_round_hip_aggregator_bit_exact_vs_oracle():
     fl_ref, h_ref = _fl(OracleAggregator(NAMES, seeds), pyus, hook=lambda r, p: ref_rounds.append(p))
     agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
     fl_hip, h_hip = _fl(agg, pyus, hook=lambda r, p: hip_rounds.append(p))
-    assert len(ref_rounds) == len(hip_rounds) == 3 * 3
+    assert len(ref_rounds) == len(hip_rounds) == 1 + 3 * 3  # init average + rounds
     for r, (a, b) in enumerate(zip(ref_rounds, hip_rounds)):
         for li, (x, y) in enumerate(zip(a, b)):
             assert x.dtype == y.dtype == np.float64
@@ -136,7 +169,7 @@ def test_fl_round_with_gaussian_dp_hip_vs_oracle_aggregator():
     _fl(OracleAggregator(NAMES, seeds), pyus, epochs=1, hook=lambda r, p: ref_rounds.append(p), dp_strategy=mk())
     agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
     _, h = _fl(agg, pyus, epochs=1, hook=lambda r, p: hip_rounds.append(p), dp_strategy=mk())
-    assert len(ref_rounds) == len(hip_rounds) == 3
+    assert len(ref_rounds) == len(hip_rounds) == 1 + 3
     for a, b in zip(ref_rounds, hip_rounds):
         for x, y in zip(a, b):
             assert np.array_equal(x, y)

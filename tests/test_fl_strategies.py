@@ -69,7 +69,7 @@ def test_strategy_hip_aggregator_bit_exact_vs_oracle(strategy):
     fl_ref, h_ref = _fl(strategy, OracleAggregator(NAMES, seeds), pyus, hook=lambda r, p: ref_rounds.append(p))
     agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
     fl_hip, h_hip = _fl(strategy, agg, pyus, hook=lambda r, p: hip_rounds.append(p))
-    assert len(ref_rounds) == len(hip_rounds) == 9
+    assert len(ref_rounds) == len(hip_rounds) == 1 + 9  # init average + rounds
     for r, (a, b) in enumerate(zip(ref_rounds, hip_rounds)):
         for li, (x, y) in enumerate(zip(a, b)):
             assert np.array_equal(x, y), (r, li)

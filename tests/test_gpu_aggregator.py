@@ -119,11 +119,13 @@ def test_notebook_kat_through_the_plugin():
     assert np.abs(avg - np.array(k["secure_average"])).max() < 1e-8
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_rounds_match_oracle_bit_exact(fused):
+@pytest.mark.parametrize("fused,keep", [(True, False), (False, True), (True, True)])
+def test_rounds_match_oracle_bit_exact(fused, keep):
     """Several FL-style rounds with explicit seeds: decoded results equal the
     oracle's float64 bit for bit, and the per-party masked vectors (wire
-    images) equal the oracle's, round after round (stream positions advance)."""
+    images) equal the oracle's, round after round (stream positions advance).
+    fused + keep: the fused launch (pair streams expanded once) stores the
+    wire images; not fused: one sa_mask launch per party."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from sfl_amd.device import PYU, reveal as rv
@@ -134,7 +136,7 @@ def test_rounds_match_oracle_bit_exact(fused):
     pair = {(a, b): seeds[a][b] for a in names for b in names if a != b}
     pyus = [PYU(nm, 0) for nm in names]
     server = PYU("server", 0)
-    agg = SecureAggregator(server, pyus, seeds=pair, fused=fused, keep_masked=not fused)
+    agg = SecureAggregator(server, pyus, seeds=pair, fused=fused, keep_masked=keep)
     rng = np.random.default_rng(4)
     offset = 0
     for rnd in range(3):
@@ -147,9 +149,11 @@ def test_rounds_match_oracle_bit_exact(fused):
             xs = [d[li] for d in data]
             exp, s, masked = o.secure_average(xs, names, weights=w, seeds=seeds, offset=offset)
             assert np.array_equal(got[li], exp.reshape(xs[0].shape)), (rnd, li)
-            if not fused:
+            if keep:
                 for c in range(len(names)):
                     assert np.array_equal(agg.last_masked[li][c].cpu().numpy().view(np.uint64), masked[c].reshape(-1))
+        if keep:
+            assert len(agg.last_masked) == 2
             offset += xs[0].size
 
 
