@@ -496,7 +496,8 @@ def extra_measurements(args, xs, plan, gens, K, torch, dev) -> dict:
         for j, (lo, hi) in enumerate(bounds):
             e_in, e_k = torch.cuda.Event(), torch.cuda.Event()
             with torch.cuda.stream(s_h2d):
-                dev_x[:, lo:hi].copy_(host_x[:, lo:hi], non_blocking=True)
+                for c in range(C):  # contiguous rows: one DMA each (a 2-D slice would be staged)
+                    dev_x[c, lo:hi].copy_(host_x[c, lo:hi], non_blocking=True)
                 e_in.record(s_h2d)
             with torch.cuda.stream(s_cmp):
                 s_cmp.wait_event(e_in)

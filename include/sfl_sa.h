@@ -47,8 +47,9 @@ extern "C" {
 #define SA_FLAG_PRG_REJECT 1u /* a PCG64 raw draw was 0: numpy's Lemire bounded
                                  draw would have rejected it and re-drawn (p=2^-64
                                  per draw).  The mask stream then differs from
-                                 numpy's from that element on; the host must
-                                 re-run with the stream re-positioned. */
+                                 numpy's from that element on; the host
+                                 re-positions it (sa_pcg64_find_zero,
+                                 sa_stream_shift, sa_xor_u64 below). */
 
 typedef struct sa_u128 {
   uint64_t lo, hi;
@@ -165,6 +166,30 @@ int sa_decode(const uint64_t* s, uint64_t n, int fxp_bits, double divisor,
  * averages: out[i] = sum_k w[k][i] (float64), `w` a HOST array of k device
  * pointers. */
 int sa_sum_f64(const double* const* w, int k, uint64_t n, double* out, void* stream);
+
+/* ------------------------------------------------------------------ */
+/* numpy's rejection re-draw, reproduced after a SA_FLAG_PRG_REJECT     */
+/* (never on the hot path).  Generator.integers(int64.min, int64.max)   */
+/* rejects a raw PCG64 output of 0 and takes the next one, so from that */
+/* element on the stream runs one raw draw further along.  A pair       */
+/* stream enters its two clients with opposite signs: the masked SUM is */
+/* unchanged, only per-client masked vectors and digests move.          */
+/* ------------------------------------------------------------------ */
+
+/* first_out[j] = min(first_out[j], smallest i in [0, n) whose raw draw i of
+ * gens[j] (the output after i + 1 steps) is 0).  `gens` is a HOST array;
+ * first_out is device memory the caller fills with UINT64_MAX first. */
+int sa_pcg64_find_zero(const sa_pcg64* gens, int n_gens, uint64_t n, uint64_t* first_out, void* stream);
+
+/* out[e] += sign * (raw[e + shift] - raw[e + shift - 1])  (mod 2^64) for e in
+ * [k, n), raw relative to `gen` (raw[0] = the first step's output): moves a
+ * masked vector that used raw[e + shift - 1] for element e onto
+ * raw[e + shift] (the mask offset K cancels in the difference). */
+int sa_stream_shift(uint64_t* out, uint64_t n, const sa_pcg64* gen, int sign, uint64_t k, uint64_t shift,
+                    void* stream);
+
+/* *digest ^= XOR of v[0..n) (the per-client digest of sa_fused_clients). */
+int sa_xor_u64(const uint64_t* v, uint64_t n, uint64_t* digest, void* stream);
 
 /* ------------------------------------------------------------------ */
 /* GaussianModelDP pre-step (sfl/security/privacy/mechanism/            */

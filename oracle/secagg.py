@@ -211,3 +211,48 @@ def pcg64_jump_py(state: int, inc: int, delta: int) -> int:
         cur_mult = (cur_mult * cur_mult) & M
         d >>= 1
     return (acc_mult * state + acc_plus) & M
+
+
+# ----- persistent per-party generators (the reference _Masker's view) -----
+
+def generator_from_state(state: int, inc: int) -> np.random.Generator:
+    """numpy Generator over PCG64 with an explicit (state, inc)."""
+    bg = np.random.PCG64()
+    bg.state = {"bit_generator": "PCG64", "state": {"state": int(state), "inc": int(inc)},
+                "has_uint32": 0, "uinteger": 0}
+    return np.random.Generator(bg)
+
+
+class OracleMaskers:
+    """Every party's persistent ``np.random.Generator`` per peer, advanced by
+    ``Generator.integers(int64.min, int64.max, n)`` round after round --
+    numpy's own rejection of a raw 0 included, exactly as the un-vendored
+    ``_Masker`` keeps one generator per peer across rounds.  ``pair_states``
+    maps (a, b) -> seed (int) or (state, inc)."""
+
+    def __init__(self, names: list, pair_states: dict):
+        self.names = list(names)
+        self.gens = {}
+        for a in names:
+            for b in names:
+                if a == b:
+                    continue
+                st = pair_states.get((a, b), pair_states.get((b, a)))
+                self.gens[(a, b)] = (generator_from_state(*st) if isinstance(st, tuple)
+                                     else np.random.Generator(np.random.PCG64(st)))
+
+    def mask(self, q: np.ndarray, me: str) -> np.ndarray:
+        out = np.array(q, dtype=np.uint64, copy=True).reshape(-1)
+        for peer in sorted(p for p in self.names if p != me):
+            m = self.gens[(me, peer)].integers(INT64_MIN, INT64_MAX, size=out.size).astype(np.uint64)
+            if peer > me:
+                out += m
+            else:
+                out -= m
+        return out
+
+    def round(self, xs: list, weights=None, fxp_bits: int = FXP_BITS):
+        """(masked vectors, uint64 sum) of one round; xs in ``names`` order."""
+        masked = [self.mask(quantize(x, None if weights is None else weights[i], fxp_bits), nm)
+                  for i, (x, nm) in enumerate(zip(xs, self.names))]
+        return masked, server_sum(masked)

@@ -31,6 +31,7 @@ EXPORTED = (
     "sa_pcg64_raw_host", "sa_mask", "sa_fused_clients", "sa_sum_u64", "sa_decode",
     "sa_sum_f64", "sa_comm_unique_id", "sa_comm_init", "sa_comm_reduce_u64",
     "sa_comm_allreduce_u64", "sa_comm_destroy", "sa_sumsq_f32", "sa_dp_perturb_f32", "sa_mask_dp",
+    "sa_pcg64_find_zero", "sa_stream_shift", "sa_xor_u64",
 )
 
 
@@ -102,6 +103,9 @@ def _declare(lib):
     lib.sa_sumsq_f32.argtypes = [vp, u64, vp, vp, i32, vp]
     lib.sa_dp_perturb_f32.argtypes = [vp, u64, P(DP), vp, vp]
     lib.sa_mask_dp.argtypes = [vp, u64, dbl, i32, P(MaskStream), i32, P(DP), vp, vp, vp, vp, vp]
+    lib.sa_pcg64_find_zero.argtypes = [P(PCG64), i32, u64, vp, vp]
+    lib.sa_stream_shift.argtypes = [vp, u64, P(PCG64), i32, u64, u64, vp]
+    lib.sa_xor_u64.argtypes = [vp, u64, vp, vp]
     for name in EXPORTED:
         if name not in ("sa_last_error",):
             getattr(lib, name).restype = i32

@@ -217,3 +217,53 @@ def mask_dp(x: torch.Tensor, out: torch.Tensor, streams: Sequence[tuple], dp: L.
                                _ptr(out), _ptr(sum_accum), _ptr(digest), _ptr(flags), C.c_void_p(_stream(out))),
             "sa_mask_dp")
     return out
+
+
+# ---------------------------------------------------------------------------
+# numpy's rejection re-draw (after SA_FLAG_PRG_REJECT; never on the hot path)
+# ---------------------------------------------------------------------------
+U64_MAX = (1 << 64) - 1
+
+
+def find_zero_draws(gens: Sequence, n: int, device) -> list:
+    """For each generator, the first raw draw index in [0, n) whose PCG64
+    output is 0 (numpy's Generator.integers rejects it), or None."""
+    if not gens:
+        return []
+    first = torch.full((len(gens),), -1, dtype=torch.int64, device=device)  # all ones = UINT64_MAX
+    arr = (L.PCG64 * len(gens))(*gens)
+    L.check(L.lib().sa_pcg64_find_zero(arr, len(gens), int(n), _ptr(first), C.c_void_p(_stream(first))),
+            "sa_pcg64_find_zero")
+    return [None if v == U64_MAX else int(v) for v in as_u64(first).tolist()]
+
+
+def stream_shift(out: torch.Tensor, gen, sign: int, k: int, shift: int) -> torch.Tensor:
+    """out[e] += sign * (raw[e+shift] - raw[e+shift-1]) for e >= k (in place)."""
+    _require_gpu(out)
+    g = L.PCG64(gen.state, gen.inc)
+    L.check(L.lib().sa_stream_shift(_ptr(out), out.numel(), C.byref(g), int(sign), int(k), int(shift),
+                                    C.c_void_p(_stream(out))), "sa_stream_shift")
+    return out
+
+
+def xor_digest(v: torch.Tensor, digest: torch.Tensor) -> torch.Tensor:
+    """digest[0] ^= XOR of every uint64 element of v."""
+    _require_gpu(v, digest)
+    L.check(L.lib().sa_xor_u64(_ptr(v), v.numel(), _ptr(digest), C.c_void_p(_stream(v))), "sa_xor_u64")
+    return digest
+
+
+def rejected_draws(gen, n: int, device) -> tuple[list, int]:
+    """numpy's Generator.integers over n elements from ``gen``: the
+    (element, shift) points where a rejected raw 0 moves the stream one raw
+    draw further (element e >= k uses raw[e + shift]), and the total number
+    of raw draws consumed (n + rejections)."""
+    pts, e0, s = [], 0, 0
+    while e0 < n:
+        # elements >= e0 use raw[e + s]: search raw[e0 + s, n + s)
+        z = find_zero_draws([L.pcg64_advance(gen, e0 + s)], n - e0, device)[0]
+        if z is None:
+            break
+        e0, s = e0 + z, s + 1
+        pts.append((e0, s))
+    return pts, n + s

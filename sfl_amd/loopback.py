@@ -188,7 +188,11 @@ class LoopbackClient:
         if self._seeds is not None:  # explicit pair seeds (tests / benches)
             for peer in keys:
                 if peer != self.party:
-                    self.masker.set_seed(peer, int(self._seeds[peer]))
+                    sd = self._seeds[peer]
+                    if isinstance(sd, (tuple, list)):  # explicit numpy PCG64 (state, inc)
+                        self.masker.set_state(peer, *sd)
+                    else:
+                        self.masker.set_seed(peer, int(sd))
         else:
             self.masker.agree(keys)
         return sorted(keys)
@@ -240,9 +244,23 @@ class LoopbackClient:
                 K.mask_dp(dx, dm, self.masker.streams(), dp.params(dp.sumsq([dx]), n), weight=w,
                           fxp_bits=self.fxp_bits, digest=dig, flags=flags)
         cs.synchronize()
+        extra = {}
         if int(flags.item()) & L.SA_FLAG_PRG_REJECT:
-            raise L.SALibraryError("a PCG64 raw draw was 0 (p=2^-64): re-position the streams")
+            # numpy's Generator.integers rejected a raw 0 on some stream: move
+            # the masked vector onto numpy's stream from there (sa_stream_shift)
+            with torch.cuda.stream(cs):
+                for peer, (gen, sign, _) in zip(self.masker.peers, self.masker.streams()):
+                    pts, total = K.rejected_draws(gen, n, dev)
+                    for k, shift in pts:
+                        K.stream_shift(dm, gen, sign, k, shift)
+                    if total > n:
+                        extra[peer] = total - n
+                dig.zero_()
+                K.xor_digest(dm, dig)
+            cs.synchronize()
         self.masker.consume(n)
+        for peer, k in extra.items():
+            self.masker.skip(peer, k)
         t1 = time.perf_counter()
         W.send_frame(self.sock, META, json.dumps({"weight": weight}).encode(), sender=self.index, rnd=rnd)
         self.sock.sendall(W.pack_header(W.MASKED, W.U64, self.index, rnd, n,

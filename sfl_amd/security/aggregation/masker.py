@@ -89,3 +89,20 @@ class Masker:
 
     def position(self, peer: str) -> int:
         return self._pos[peer]
+
+    def skip(self, peer: str, k: int) -> None:
+        """Raw draws consumed on top of one per element: numpy's
+        Generator.integers rejected k raw outputs of 0 on this pair stream."""
+        self._pos[peer] += int(k)
+
+    def set_state(self, peer: str, state: int, inc: int) -> None:
+        """Start the pair stream from an explicit numpy PCG64 (state, inc)
+        (tests: a state whose next raw draws include a 0)."""
+        self._gens[peer] = L.PCG64.of(int(state), int(inc))
+        self._pos[peer] = 0
+
+    def snapshot(self) -> dict:
+        return dict(self._pos)
+
+    def restore(self, snap: dict) -> None:
+        self._pos = dict(snap)

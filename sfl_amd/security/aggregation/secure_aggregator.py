@@ -42,6 +42,10 @@ _T2NP = {v: k for k, v in _NP2T.items()}
 MAX_FUSED_CLIENTS = 8
 
 
+class _Rejected(Exception):
+    """A masking launch flagged a raw PCG64 draw of 0 (SA_FLAG_PRG_REJECT)."""
+
+
 def _layers(payload):
     if isinstance(payload, (list, tuple)):
         return list(payload), True
@@ -78,7 +82,8 @@ class SecureAggregator(Aggregator):
         participants: the client PYUs (distinct parties).
         fxp_bits: fixed-point fraction bits (reference default 18).
         seeds: optional ``{(party_a, party_b): seed}`` pairwise seeds (both
-            orders accepted); default is a Diffie-Hellman agreement.
+            orders accepted; a ``(state, inc)`` tuple is an explicit numpy
+            PCG64 state); default is a Diffie-Hellman agreement.
         fused: allow the single-launch simulation of co-located clients.
         keep_masked: also materialise every party's masked vector (the wire
             image) and expose the last ones as ``last_masked``; co-located
@@ -97,6 +102,7 @@ class SecureAggregator(Aggregator):
         self._keep_masked = keep_masked
         self.last_masked = None
         self.last_digests = None
+        self._careful = False  # replay mode after a flagged rejection (see _aggregate)
         self._maskers = {n: Masker(n, self._fxp_bits) for n in names}
         if seeds is None:
             keys = {n: m.public_key for n, m in self._maskers.items()}
@@ -109,7 +115,10 @@ class SecureAggregator(Aggregator):
                         s = seeds.get((a, b), seeds.get((b, a)))
                         if s is None:
                             raise ValueError(f"missing seed for pair ({a}, {b})")
-                        self._maskers[a].set_seed(b, int(s))
+                        if isinstance(s, tuple):  # an explicit numpy PCG64 (state, inc)
+                            self._maskers[a].set_state(b, *s)
+                        else:
+                            self._maskers[a].set_seed(b, int(s))
 
     @property
     def device(self) -> PYU:
@@ -128,6 +137,24 @@ class SecureAggregator(Aggregator):
 
     # ------------------------------------------------------------ internals
     def _aggregate(self, data, axis, weights, average: bool) -> DeviceObject:
+        """One aggregation.  The masking kernels only FLAG a raw PCG64 draw
+        of 0 (numpy's Generator.integers rejects it and draws again, p =
+        2^-64 per draw); when that happens the round is replayed from the
+        same stream positions in careful mode, which re-positions the
+        affected streams exactly as numpy does (``_fix_rejections``)."""
+        snap = {nm: m.snapshot() for nm, m in self._maskers.items()}
+        try:
+            return self._aggregate_once(data, axis, weights, average)
+        except _Rejected:
+            for nm, m in self._maskers.items():
+                m.restore(snap[nm])
+            self._careful = True
+            try:
+                return self._aggregate_once(data, axis, weights, average)
+            finally:
+                self._careful = False
+
+    def _aggregate_once(self, data, axis, weights, average: bool) -> DeviceObject:
         assert data, "Data to aggregate should not be None or empty!"
         if axis not in (0, None):
             raise NotImplementedError("SecureAggregator aggregates over parties (axis=0)")
@@ -266,9 +293,7 @@ class SecureAggregator(Aggregator):
             torch.cuda.current_stream(sdev).synchronize()
         out = stage_out.numpy()[:n].copy()
         if int(self._stage_flags[0]) & L.SA_FLAG_PRG_REJECT:
-            raise L.SALibraryError(
-                "a PCG64 raw draw was 0 (p=2^-64): numpy would have re-drawn; re-run with the stream "
-                "re-positioned")
+            raise _Rejected()
         self.last_digests = digests_keep
         parts = np.split(out, np.cumsum(sizes)[:-1])
         result = [p.reshape(sh) for p, sh in zip(parts, shapes)]
@@ -314,9 +339,7 @@ class SecureAggregator(Aggregator):
                 out_layers[li] = part.reshape(shapes[li])
 
         if int(flags.item()) & L.SA_FLAG_PRG_REJECT:
-            raise L.SALibraryError(
-                "a PCG64 raw draw was 0 (p=2^-64): numpy would have re-drawn; re-run with the stream "
-                "re-positioned")
+            raise _Rejected()
         if self._keep_masked:
             self.last_masked = masked_keep
         self.last_digests = digests_keep
@@ -380,14 +403,15 @@ class SecureAggregator(Aggregator):
                    and all(x.dtype == torch.float32 for x in xs)
                    and all(wv is None for wv in wvecs)
                    and set(names) == set(self._maskers))
+        pair_gens, pair_signs = [], []
+        for u in range(C):
+            for v in range(u + 1, C):
+                mu, mv = self._maskers[names[u]], self._maskers[names[v]]
+                assert mu.position(names[v]) == mv.position(names[u]), "pair streams out of step"
+                pair_gens.append(mu.generator(names[v]))
+                pair_signs.append(mu.sign(names[v]))
+        client_streams = [self._maskers[p.party].streams(self._maskers[p.party].peers) for p in parties]
         if fusable:
-            pair_gens, pair_signs = [], []
-            for u in range(C):
-                for v in range(u + 1, C):
-                    mu, mv = self._maskers[names[u]], self._maskers[names[v]]
-                    assert mu.position(names[v]) == mv.position(names[u]), "pair streams out of step"
-                    pair_gens.append(mu.generator(names[v]))
-                    pair_signs.append(mu.sign(names[v]))
             # keep_masked: the same launch also stores every party's masked
             # vector (the wire image) -- pair streams are still expanded once
             masked = [torch.empty(n, dtype=K.U64, device=sdev) for _ in range(C)] if self._keep_masked else None
@@ -399,13 +423,11 @@ class SecureAggregator(Aggregator):
         else:
             masked = []
             for ci, p in enumerate(parties):
-                m = self._maskers[p.party]
-                peers = [q for q in m.peers]
                 out = torch.empty(n, dtype=K.U64, device=p.torch_device)
                 dig = torch.zeros(1, dtype=K.U64, device=p.torch_device)
                 fl = flags if p.torch_device == sdev else torch.zeros(1, dtype=torch.int32, device=p.torch_device)
                 with torch.cuda.device(p.torch_device):
-                    K.mask(xs[ci], out, m.streams(peers), weight=ws[ci], weight_vec=wvecs[ci],
+                    K.mask(xs[ci], out, client_streams[ci], weight=ws[ci], weight_vec=wvecs[ci],
                            compute_dtype=_NP2T[cts[ci]], fxp_bits=self._fxp_bits, digest=dig, flags=fl)
                 if fl is not flags:
                     flags |= fl.to(sdev)
@@ -415,7 +437,60 @@ class SecureAggregator(Aggregator):
                 K.sum_u64(masked, s)
             if self._keep_masked:
                 masked_keep.append(masked)
+        wire = masked  # materialised masked vectors (None: fused launch without wire images)
+        extra = {}
+        if self._careful:
+            torch.cuda.synchronize(sdev)
+            if int(flags.item()) & L.SA_FLAG_PRG_REJECT:
+                extra = self._fix_rejections(names, pair_gens, pair_signs, client_streams, xs, ws, wvecs, cts, n,
+                                             wire, digests, s)
+                flags.zero_()
         for ci, p in enumerate(parties):
             self._maskers[p.party].consume(n)
+        for (a, b), k in extra.items():  # the rejected raw draws consumed on top
+            self._maskers[a].skip(b, k)
+            self._maskers[b].skip(a, k)
         digests_keep.append(digests)
         return s
+
+    def _fix_rejections(self, names, pair_gens, pair_signs, client_streams, xs, ws, wvecs, cts, n, wire, digests,
+                        s) -> dict:
+        """numpy's rejection re-draw for one launch group (careful mode).
+
+        For every pair stream: the elements from which it runs one more raw
+        draw along (``kernels.rejected_draws``); the two clients' masked
+        vectors are shifted there (``sa_stream_shift``, opposite signs, so
+        the masked sum is unchanged) and their digests recomputed.  Without
+        materialised vectors (fused launch, no wire images) an affected
+        client's vector is re-masked into scratch for its digest.  Returns
+        {(party_a, party_b): extra raw draws} for the stream positions."""
+        sdev = self._device.torch_device
+        C = len(names)
+        fixes = {c: [] for c in range(C)}  # client -> [(gen, sign, points)]
+        extra = {}
+        p = 0
+        for u in range(C):
+            for v in range(u + 1, C):
+                pts, total = K.rejected_draws(pair_gens[p], n, sdev)
+                if pts:
+                    fixes[u].append((pair_gens[p], pair_signs[p], pts))
+                    fixes[v].append((pair_gens[p], -pair_signs[p], pts))
+                    extra[(names[u], names[v])] = total - n
+                p += 1
+        for c in range(C):
+            if not fixes[c]:
+                continue
+            if wire is not None:
+                vec = wire[c]
+            else:
+                vec = torch.empty(n, dtype=K.U64, device=sdev)
+                K.mask(xs[c], vec, client_streams[c], weight=ws[c], weight_vec=wvecs[c],
+                       compute_dtype=_NP2T[cts[c]], fxp_bits=self._fxp_bits)
+            for gen, sign, pts in fixes[c]:
+                for k, shift in pts:
+                    K.stream_shift(vec, gen, sign, k, shift)
+            digests[c] = 0
+            K.xor_digest(vec, digests[c:c + 1])
+        if wire is not None:  # the server sums the wire images it received
+            K.sum_u64(wire, s)
+        return extra

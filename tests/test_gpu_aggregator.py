@@ -152,9 +152,9 @@ def test_rounds_match_oracle_bit_exact(fused, keep):
             if keep:
                 for c in range(len(names)):
                     assert np.array_equal(agg.last_masked[li][c].cpu().numpy().view(np.uint64), masked[c].reshape(-1))
+            offset += xs[0].size
         if keep:
             assert len(agg.last_masked) == 2
-            offset += xs[0].size
 
 
 def test_torch_payload_stays_on_device():

@@ -69,3 +69,29 @@ def test_loopback_chunked_streaming_multi_party_processes(monkeypatch):
         assert np.array_equal(res[r], o.decode(o.server_sum(masked_o)))
         for c in range(len(names)):
             assert np.array_equal(masked[r][c], masked_o[c])
+
+
+def test_loopback_client_reproduces_numpy_rejection():
+    """A pair stream whose raw draw 777 is 0 (numpy rejects it): the client
+    party moves its masked vector onto numpy's stream before sending, so the
+    wire images (digest-verified) equal numpy's in both rounds."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from test_gpu_rejection import forced_zero_state
+
+    from sfl_amd.loopback import run_loopback, synthetic_gradient
+
+    names = ["alice", "bob", "carol"]
+    n = 2048
+    seeds = o.seeds_for(names)
+    st = forced_zero_state(777)
+    seeds["alice"]["carol"] = seeds["carol"]["alice"] = st
+    res, _, _, masked = run_loopback(names, n, 2, seeds=seeds, keep_masked=True, verify_digest=True, timeout=300)
+    pair = {(a, b): seeds[a][b] for a in names for b in names if a < b}
+    ora = o.OracleMaskers(names, pair)
+    for r in range(2):
+        xs = [synthetic_gradient(c, n, r) for c in range(len(names))]
+        m, ssum = ora.round(xs)
+        assert np.array_equal(res[r], o.decode(ssum)), r
+        for c in range(len(names)):
+            assert np.array_equal(masked[r][c], m[c]), (r, c)
