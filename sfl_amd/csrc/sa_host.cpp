@@ -29,7 +29,15 @@ void sa_set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+// A tuning build (ablations that make results WRONG, or the wave-timeline
+// instrumentation; sa_clients_impl.h) reports a different ABI version, so
+// the product loader (sfl_amd/_lib.py) refuses it: such a library can never
+// be measured or shipped as the product.
+#if (defined(SA_ABLATE) && SA_ABLATE != 0) || defined(SA_TIMING)
+extern "C" int sa_abi_version(void) { return SA_ABI_VERSION + 1000; }
+#else
 extern "C" int sa_abi_version(void) { return SA_ABI_VERSION; }
+#endif
 extern "C" const char* sa_last_error(void) { return g_err; }
 
 namespace {

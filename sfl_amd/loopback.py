@@ -285,8 +285,10 @@ class LoopbackClient:
         t2 = time.perf_counter()
         return {"h2d_mask_s": t1 - t0, "d2h_send_s": t2 - t1}
 
-    def result(self) -> np.ndarray:
-        h, mv = W.recv_frame(self.sock, expect_kind=W.RESULT)
+    def result(self, n: int | None = None) -> np.ndarray:
+        """The server's float64 aggregate (``n`` elements when given: a larger
+        announced frame is refused before anything is allocated)."""
+        h, mv = W.recv_frame(self.sock, expect_kind=W.RESULT, max_bytes=None if n is None else 8 * int(n))
         return W.as_array(h, mv).copy()
 
     def close(self):
@@ -319,7 +321,7 @@ def client_process(parties: list, port: int, n: int, rounds: int, gpu: int, fxp_
             stats = []
             for r in range(rounds):
                 st = cl.submit(xs[r], r, weight)
-                res = cl.result()
+                res = cl.result(n)
                 st["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))
                 stats.append(st)
             W.recv_header(cl.sock, expect_kind=W.BYE)

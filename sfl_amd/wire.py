@@ -40,6 +40,11 @@ BYTES, U64, F64, F32 = 0, 1, 2, 3
 _ITEMSIZE = {BYTES: 1, U64: 8, F64: 8, F32: 4}
 _NP = {U64: np.uint64, F64: np.float64, F32: np.float32}
 MAX_FRAME_BYTES = 1 << 40
+KINDS = (HELLO, KEYS, MASKED, RESULT, BYE, META)
+# control frames (handshake, key table, per-round metadata, goodbye) are tiny:
+# a peer announcing more is rejected before anything is allocated for it
+CONTROL_KINDS = (HELLO, KEYS, META, BYE)
+MAX_CONTROL_BYTES = 1 << 20
 
 
 class WireError(RuntimeError):
@@ -86,8 +91,12 @@ def unpack_header(b: bytes) -> Header:
         raise WireError(f"unsupported wire version {ver}")
     if dtype not in _ITEMSIZE:
         raise WireError(f"unknown dtype code {dtype}")
+    if kind not in KINDS:
+        raise WireError(f"unknown frame kind {kind}")
     if nbytes != count * _ITEMSIZE[dtype] or nbytes > MAX_FRAME_BYTES:
         raise WireError(f"inconsistent frame size: {count} x {_ITEMSIZE[dtype]} != {nbytes}")
+    if kind in CONTROL_KINDS and nbytes > MAX_CONTROL_BYTES:
+        raise WireError(f"control frame (kind {kind}) of {nbytes} bytes exceeds {MAX_CONTROL_BYTES}")
     return Header(kind, dtype, sender, rnd, count, nbytes, digest)
 
 
@@ -150,11 +159,15 @@ def recv_payload_chunked(sock: socket.socket, h: Header, buffers, on_chunk) -> N
         j += 1
 
 
-def recv_frame(sock: socket.socket, into=None, *, expect_kind: int | None = None):
+def recv_frame(sock: socket.socket, into=None, *, expect_kind: int | None = None, max_bytes: int | None = None):
     """Receive one frame -> (Header, memoryview of the payload).  With
     ``into`` (a writable buffer: numpy array / pinned CPU tensor), the payload
-    lands there directly and must fit."""
+    lands there directly and must fit; otherwise a buffer of the announced
+    size is allocated, which must not exceed ``max_bytes`` when given
+    (control frames are capped at MAX_CONTROL_BYTES by the header check)."""
     h = recv_header(sock, expect_kind=expect_kind)
+    if into is None and max_bytes is not None and h.nbytes > max_bytes:
+        raise WireError(f"frame payload of {h.nbytes} bytes exceeds the expected {max_bytes}")
     if into is not None:
         a = into.numpy() if hasattr(into, "numpy") and not isinstance(into, np.ndarray) else into
         mv = memoryview(a).cast("B")

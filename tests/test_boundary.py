@@ -121,3 +121,20 @@ def test_every_entry_point_has_ctypes_signature():
         if name in ("sa_abi_version", "sa_last_error"):
             continue
         assert getattr(lib, name).argtypes, name
+
+
+def test_tuning_builds_report_a_refused_abi_version(tmp_path):
+    """SA_ABLATE (results WRONG) and SA_TIMING builds report ABI version
+    1000 + 1, which sfl_amd._lib refuses unless a tuning tool opts in: a
+    tuning library can never be loaded as the product."""
+    import ctypes
+    import subprocess
+
+    from sfl_amd import _lib as L
+
+    src = os.path.join(ROOT, "sfl_amd", "csrc", "sa_host.cpp")
+    for define, want in (("", 1), ("-DSA_ABLATE=8", 1 + L.TUNING_ABI_OFFSET), ("-DSA_TIMING", 1 + L.TUNING_ABI_OFFSET)):
+        so = tmp_path / f"host{abs(hash(define))}.so"
+        cmd = ["g++", "-std=c++17", "-shared", "-fPIC", "-O1", src, "-o", str(so)] + ([define] if define else [])
+        subprocess.run(cmd, check=True, capture_output=True)
+        assert ctypes.CDLL(str(so)).sa_abi_version() == want, define

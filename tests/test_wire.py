@@ -121,3 +121,25 @@ def test_chunked_receive_through_buffer_ring():
     t.join()
     assert np.array_equal(got, v)
     assert [s[0] for s in seen] == [i % 2 for i in range(len(seen))] and len(seen) == 11
+
+
+def test_oversized_control_frames_are_refused_before_allocation():
+    """A peer announcing a huge HELLO / KEYS / META frame (the
+    server read HELLO with an allocation sized by the peer's header) is
+    refused at the header; unknown kinds too; RESULT frames respect the
+    caller's expected size."""
+    for kind in (W.HELLO, W.KEYS, W.META, W.BYE):
+        hdr = W.pack_header(kind, W.BYTES, 0, 0, (1 << 20) + 1)
+        with pytest.raises(W.WireError, match="control frame"):
+            W.unpack_header(hdr)
+        W.unpack_header(W.pack_header(kind, W.BYTES, 0, 0, 1 << 20))  # at the cap: fine
+    with pytest.raises(W.WireError, match="unknown frame kind"):
+        W.unpack_header(W.HEADER.pack(W.MAGIC, W.VERSION, 99, W.BYTES, 0, 0, 0, 4, 4, 0))
+    a, b = _pair()
+    a.sendall(W.pack_header(W.HELLO, W.BYTES, 0, 0, 1 << 39))  # 512 GiB claimed, nothing sent
+    with pytest.raises(W.WireError, match="control frame"):
+        W.recv_frame(b, expect_kind=W.HELLO)
+    a, b = _pair()
+    a.sendall(W.pack_header(W.RESULT, W.F64, 0, 0, 1 << 36))
+    with pytest.raises(W.WireError, match="exceeds the expected"):
+        W.recv_frame(b, expect_kind=W.RESULT, max_bytes=8 * 1000)

@@ -13,6 +13,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# timing tool: may load a tuning variant (SFL_SA_LIB) that the product loader refuses
+os.environ.setdefault("SFL_SA_ALLOW_TUNING_BUILD", "1")
 sys.path.insert(0, ROOT)
 
 
