@@ -174,6 +174,7 @@ int sa_mask_impl(const void* x, int x_type, int compute_type, uint64_t n, double
     a.c[0].wvec = weight_vec;
     a.c[0].masked_out = out;
     a.c[0].w = weight;
+    a.c[0].ws[0] = a.c[0].ws[1] = (float)weight * a.scale_f;  // IEEE single multiply, as __fmul_rn on the device
     uint64_t bias = 0;
     for (int j = 0; j < cnt; j++) {
       const sa_mask_stream& ms = streams[j0 + j];
@@ -255,6 +256,7 @@ extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, i
     a.c[c].wvec = nullptr;
     a.c[c].masked_out = clients[c].masked_out;
     a.c[c].w = clients[c].weight;
+    a.c[c].ws[0] = a.c[c].ws[1] = (float)clients[c].weight * a.scale_f;
   }
   int p = 0;
   for (int u = 0; u < L; u++)

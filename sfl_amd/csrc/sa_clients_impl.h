@@ -222,16 +222,26 @@ __device__ __forceinline__ bool fast_products(const Vec2<XT> (&xv)[L], const Vec
                                               const __attribute__((address_space(4))) KArgs* ka,
                                               const QScale& qs, float (&p)[L][kE]) {
   if constexpr (std::is_same<CT, float>::value) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
     bool ok = true;
 #pragma unroll
     for (int c = 0; c < L; c++) {
       const bool has_wv = kGeneral && ka->c[c].wvec;
+      if (has_wv) {
 #pragma unroll
-      for (int k = 0; k < kE; k++) {
-        const float w = has_wv ? (float)wv[kGeneral ? c : 0].v[k] : scalar_weight<float>(ka->c[c].w);
-        p[c][k] = __fmul_rn((float)xv[c].v[k], __fmul_rn(w, qs.f));
-        ok = ok && (__builtin_fabsf(p[c][k]) < 0x1p31f);
+        for (int k = 0; k < kE; k++)
+          p[c][k] = __fmul_rn((float)xv[c].v[k], __fmul_rn((float)wv[kGeneral ? c : 0].v[k], qs.f));
+      } else {
+        // scalar weight: the host rounded w * 2^fxp once (ClientArg::ws);
+        // both elements in one packed multiply (v_pk_mul_f32, per-lane RN)
+        const f2 w2 = {ka->c[c].ws[0], ka->c[c].ws[1]};
+        const f2 x2 = {(float)xv[c].v[0], (float)xv[c].v[1]};
+        const f2 p2 = x2 * w2;
+        p[c][0] = p2[0];
+        p[c][1] = p2[1];
       }
+#pragma unroll
+      for (int k = 0; k < kE; k++) ok = ok && (__builtin_fabsf(p[c][k]) < 0x1p31f);
     }
     return !__any(!ok) || (SA_ABLATE & 2);
   } else {

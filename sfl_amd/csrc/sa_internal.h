@@ -44,6 +44,8 @@ struct ClientArg {
   uint64_t* masked_out;  // optional masked vector out (required in continue mode)
   double w;              // scalar weight
   uint64_t bias;         // sum of the folded +/- mask offsets (see sa_kernels.hip)
+  float ws[2];           // (float)w * 2^fxp twice, rounded once on the host: the fp32 fast
+                         // path's packed scale (one SGPR pair for v_pk_mul_f32)
 };
 
 struct KArgs {
