@@ -74,15 +74,22 @@ def mask_stream(seed, n: int, offset: int = 0) -> np.ndarray:
 def quantize(x: np.ndarray, weight=None, fxp_bits: int = FXP_BITS) -> np.ndarray:
     """``trunc(x * w * 2^fxp)`` as int64, viewed as uint64 (two's complement).
 
-    numpy promotion rules decide the arithmetic type exactly as in the
-    reference: float32 data with a python-int weight stays float32; an int64
-    weight array promotes float32 data to float64; int data stays int64.
+    numpy promotion rules decide the arithmetic type as in the reference's
+    pinned numpy 1.23.5: float32 data with a python-int weight stays float32,
+    and so does float32 data with a numpy-scalar weight (value-based casting,
+    ``legacy_scalar_dtype``); an int64 weight array promotes float32 data to
+    float64; int data stays int64.
     Non-finite or out-of-int64-range values map to INT64_MIN, which is what
     ``ndarray.astype(np.int64)`` yields on x86-64 (cvttsd2si "integer
     indefinite"); we spell it out so the oracle is platform independent."""
     x = np.asarray(x)
     with np.errstate(over="ignore", invalid="ignore"):
-        d = x if weight is None else x * weight
+        if weight is None:
+            d = x
+        elif (isinstance(weight, (bool, int, float)) and not isinstance(weight, np.generic)) or np.ndim(weight):
+            d = x * weight
+        else:  # numpy scalar / 0-d weight: numpy 1.23.5's value-based casting
+            d = np.multiply(x, weight, dtype=legacy_scalar_dtype(x.dtype, weight))
         d = d * (1 << fxp_bits)
     if np.issubdtype(d.dtype, np.integer):
         return d.astype(np.int64).astype(np.uint64)
@@ -92,6 +99,15 @@ def quantize(x: np.ndarray, weight=None, fxp_bits: int = FXP_BITS) -> np.ndarray
     q = t.astype(np.int64)
     q = np.where(ok, q, np.int64(INT64_MIN))
     return q.astype(np.int64).astype(np.uint64)
+
+
+def legacy_scalar_dtype(x_dtype, scalar) -> np.dtype:
+    """``array * numpy_scalar`` result dtype under numpy 1.23.5, the version
+    the reference pins (``uv.lock:1189-1190``): value-based casting -- the
+    scalar takes part with the smallest dtype that holds its value
+    (``np.min_scalar_type``), so float32 data times ``np.float64(3.0)`` or
+    ``np.int64(5)`` stays float32 (numpy 2's NEP 50 would give float64)."""
+    return np.result_type(np.dtype(x_dtype), np.min_scalar_type(np.asarray(scalar)))
 
 
 def mask_client(q: np.ndarray, self_name, peer_seeds: dict, offset: int = 0) -> np.ndarray:

@@ -63,14 +63,23 @@ def _shape(a):
 
 
 def _compute_dtype(ldt: np.dtype, w, fxp_bits: int) -> np.dtype:
-    """numpy's result dtype of ``(datum * w) * (1 << fxp)`` (NEP 50 rules)."""
+    """Result dtype of ``(datum * w) * (1 << fxp)`` under the numpy the
+    reference pins, 1.23.5 (``uv.lock:1189-1190``): value-based casting, so a
+    scalar weight -- python OR numpy scalar / 0-d array -- does not widen
+    the array's dtype when its value fits (``result_type(dtype,
+    min_scalar_type(w))``); array weights promote as usual.  numpy 2's NEP 50
+    would make a numpy-scalar weight "strong" (float32 data * np.float64(w)
+    -> float64); no reference fixture pins either (parity
+    unpinned), the pinned version decides.  Python scalars behave alike
+    under both rules."""
     probe = np.zeros(1, dtype=ldt)
     if w is not None:
-        if isinstance(w, (bool, int, float)):
+        if isinstance(w, (bool, int, float)) and not isinstance(w, np.generic):  # np.float64 is a float
             probe = probe * w
         else:
             wa = np.asarray(w)
-            probe = probe * np.zeros(1, dtype=wa.dtype) if wa.ndim else probe * wa.dtype.type(0)
+            dt = np.result_type(ldt, wa.dtype if wa.ndim else np.min_scalar_type(wa))
+            probe = probe.astype(dt)
     return (probe * (1 << fxp_bits)).dtype
 
 

@@ -239,3 +239,28 @@ def test_subclass_with_reference_constructor_contract():
     out = rv(agg.average([p(lambda x=x: x)() for p, x in zip(parties, xs)], axis=0, weights=[1, 1]))
     assert out["generator_params"] == "gen-weights"
     assert np.allclose(rv(out["model_params"]), (xs[0] + xs[1]) / 2, atol=2 * 2.0**-18)
+
+
+@pytest.mark.parametrize("as_list", [False, True])
+def test_numpy_scalar_weights_numpy_1_23_semantics(as_list):
+    """numpy-scalar weights on float32 payloads: float32 arithmetic with the
+    weight rounded to float32, as numpy 1.23.5 (the reference's pinned
+    version, uv.lock:1189-1190) computes x * w; bit-exact vs the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    names = ["alice", "bob", "carol"]
+    seeds = o.seeds_for(names)
+    pair = {(a, b): seeds[a][b] for a in names for b in names if a != b}
+    pyus = [PYU(nm, 0) for nm in names]
+    agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
+    rng = np.random.default_rng(8)
+    xs = [(rng.standard_normal(1001) * 0.1).astype(np.float32) for _ in names]
+    w = [np.float64(1.3), np.int64(3), np.float32(0.7)]
+    objs = [p(lambda x=x: [x] if as_list else x)() for p, x in zip(pyus, xs)]
+    got = rv(agg.average(objs, axis=0, weights=w))
+    got = got[0] if as_list else got
+    exp, _, _ = o.secure_average(xs, names, weights=w, seeds=seeds)
+    assert np.array_equal(got, exp)

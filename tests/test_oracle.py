@@ -113,3 +113,27 @@ def test_single_party_has_no_masks():
     dec, s, masked = o.secure_sum([x], ["alice"])
     assert np.array_equal(masked[0], o.quantize(x))
     assert np.array_equal(dec, x.astype(np.float64))
+
+
+def test_numpy_scalar_weights_follow_numpy_1_23_value_based_casting():
+    """The reference pins numpy 1.23.5 (uv.lock:1189-1190): a numpy-scalar
+    weight does not widen float32 data (numpy 2's NEP 50 would).  Oracle and
+    plugin agree on the arithmetic type; python scalars and array weights
+    promote as before."""
+    import numpy as np
+
+    from sfl_amd.security.aggregation.secure_aggregator import _compute_dtype
+
+    f32, f64, i64 = np.dtype(np.float32), np.dtype(np.float64), np.dtype(np.int64)
+    cases = [(f32, np.float64(3.0), f32), (f32, np.int64(5), f32), (f32, np.float64(1e300), f64),
+             (f32, 3, f32), (f32, 2.5, f32), (f32, np.array([1, 2], dtype=np.int64), f64),
+             (f64, np.float32(2), f64), (i64, np.int64(3), i64), (i64, np.float64(0.5), f64),
+             (f32, np.array(7.0), f32)]
+    for dt, w, want in cases:
+        if isinstance(w, np.generic) or (isinstance(w, np.ndarray) and w.ndim == 0):
+            assert o.legacy_scalar_dtype(dt, w) == want, (dt, w)
+        assert _compute_dtype(dt, w, 18) == want, (dt, w)
+    x = np.float32([0.1, -0.3, 1.7])
+    # float32 arithmetic with the weight rounded to float32, like numpy 1.23.5
+    exp = np.trunc((x * np.float32(3.3)) * np.float32(1 << 18)).astype(np.int64).astype(np.uint64)
+    assert np.array_equal(o.quantize(x, np.float64(3.3)), exp)
