@@ -1,11 +1,13 @@
 #!/bin/bash
 # Round profile of the headline path (run on the GPU box from the repo root):
-#   1. bench.py (default workload) -> gpurun_out/bench.jsonl
+#   1. bench.py (default workload, then --extra) -> gpurun_out/bench*.jsonl
 #   2. rocprofv3 --kernel-trace --stats of the same bench command
-#   3. PMC passes (one counter group per run): FETCH_SIZE, WRITE_SIZE, SQ census
-#      on tools/kernel_bench.py (8 clients x 100M on one GPU + the k_sum_u64
-#      calibration launch whose bytes are known)
-# Copy what should be judged into profiles/<round>/ afterwards.
+#   3. PMC passes, one counter group per run: FETCH_SIZE, WRITE_SIZE on
+#      tools/kernel_bench.py over every per-rank shape (8 clients over 1, 2, 4, 8
+#      GPUs at 100M element positions) + the k_sum_u64 calibration launch whose
+#      bytes are known; the SQ issue census (tools/pmc_sq.sh)
+# Copy what should be judged into profiles/<round>/ afterwards
+# (tools/save_profiles.sh <round>).
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -15,8 +17,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
   python3 bench.py --cpu-baseline-seconds 0 > gpurun_out/bench_prof.jsonl 2> gpurun_out/bench_prof.err
 tail -1 gpurun_out/bench_prof.jsonl
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
-  python3 tools/kernel_bench.py --shapes 8:1 --rounds 1 --reps 2 --calib 8 > gpurun_out/pmc_fetch.log 2>&1
+  python3 tools/kernel_bench.py --shapes 8:1,8:2,8:4,8:8 --rounds 1 --reps 2 --calib 8 > gpurun_out/pmc_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- \
-  python3 tools/kernel_bench.py --shapes 8:1 --rounds 1 --reps 2 --calib 8 > gpurun_out/pmc_write.log 2>&1
+  python3 tools/kernel_bench.py --shapes 8:1,8:2,8:4,8:8 --rounds 1 --reps 2 --calib 8 > gpurun_out/pmc_write.log 2>&1
 tools/pmc_sq.sh 8:1,8:8 > /dev/null
+timeout -k 10 120 python -u tools/kernel_bench.py --rounds 5 > gpurun_out/kb_shapes.jsonl
+timeout -k 10 400 python bench.py --extra --cpu-baseline-seconds 0 > gpurun_out/bench_extra.jsonl 2> gpurun_out/bench_extra.err
 echo PROFILE_OK
