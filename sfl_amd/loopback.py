@@ -10,10 +10,11 @@ RayFed actor transport of the reference (``sfl/distributed/op_strategy.py:131-14
 2. round -- each client copies its host gradient to its GPU, quantizes and
    masks it there (``sa_mask``), copies the masked uint64 vector back to
    pinned host memory and sends it (META with its weight, then MASKED); the
-   server receives all C frames concurrently straight into pinned buffers,
-   copies each to its GPU as soon as it lands, sums them mod 2^64
-   (``sa_sum_u64``), decodes (``sa_decode``) and sends the float64 result
-   back to every client (RESULT).
+   server receives all C frames concurrently straight into pinned buffers
+   and copies each chunk to its GPU as it lands; as soon as a chunk of every
+   client is there it sums those slices mod 2^64 (``sa_sum_u64``), decodes
+   them (``sa_decode``) and streams that chunk of the float64 result back
+   to every client (RESULT) while later chunks are still arriving.
 
 This is the path that "starts and ends in host memory" (BASELINE north
 star): the per-round rate here includes H2D, D2H and the loopback copies.
@@ -88,72 +89,150 @@ class LoopbackServer:
             ring = [[torch.empty(ce, dtype=torch.int64).pin_memory() for _ in range(2)] for _ in self.conns]
             devb = [torch.empty(n, dtype=torch.int64, device=dev) for _ in self.conns]
             streams = [torch.cuda.Stream(dev) for _ in self.conns]
-            self._bufs = (n, ring, devb, streams)
+            agg = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.float64, device=dev),
+                   torch.empty(n, dtype=torch.float64).pin_memory(), torch.cuda.Stream(dev))
+            self._bufs = (n, ring, devb, streams, agg)
         return self._bufs[1:]
 
     def round(self, n: int, rnd: int, *, average: bool = False, verify_digest: bool = False,
-              keep_masked: bool = False):
+              keep_masked: bool = False, timeout: float = 600.0):
         """One aggregation round over n-element vectors -> (float64 result, timings).
 
-        Each connection's frame streams through a ring of two pinned chunk
-        buffers (chunk_elems() u64): chunk j is copied to the device while chunk
-        j+1 is received, so host memory stays O(chunk) per client."""
+        Pipelined per chunk (chunk_elems() elements): every connection's frame
+        streams through a ring of two pinned buffers and each chunk is copied
+        to the device as it lands (one stream per client); as soon as chunk j
+        of EVERY client is on the device, the server sums those slices mod
+        2^64, decodes them and copies the float64 chunk to pinned host memory
+        (its own stream), and one sender thread per client streams the RESULT
+        frame chunk by chunk -- so the broadcast of early chunks overlaps the
+        reception of later ones and host memory stays O(chunk) per client."""
+        import threading
+
         import torch
 
         from . import kernels as K
 
-        dev = torch.device("cuda", self.gpu)
-        ring, devb, streams = self._buffers(n)
+        ring, devb, streams, (s_sum, dec, res_host, agg) = self._buffers(n)
+        C = len(self.conns)
+        ce = ring[0][0].numel()
+        bounds = [(lo, min(n, lo + ce)) for lo in range(0, n, ce)] or [(0, 0)]
+        J = len(bounds)
         t0 = time.perf_counter()
-        weights = [None] * len(self.conns)
+        weights = [None] * C
+        arrived = [0] * J
+        ev_in = [[None] * J for _ in range(C)]
+        cond = threading.Condition()
+        errors = []
+        done_rx = [0]  # receivers finished (an empty frame has no chunks)
+        ready = [threading.Event() for _ in range(J)]
+        stamps = {}
 
         def receive(i):
-            conn = self.conns[i]
-            _, mv = W.recv_frame(conn, expect_kind=META)
-            weights[i] = json.loads(bytes(mv)).get("weight")
-            h = W.recv_header(conn, expect_kind=W.MASKED)
-            if h.count != n or h.round != rnd or h.dtype != W.U64:
-                raise W.WireError(f"client {i}: frame of {h.count} elems for round {h.round}, want {n} / {rnd}")
-            events = [None, None]
-            dig = [0]
+            try:
+                conn = self.conns[i]
+                _, mv = W.recv_frame(conn, expect_kind=META)
+                weights[i] = json.loads(bytes(mv)).get("weight")
+                h = W.recv_header(conn, expect_kind=W.MASKED)
+                if h.count != n or h.round != rnd or h.dtype != W.U64:
+                    raise W.WireError(f"client {i}: frame of {h.count} elems for round {h.round}, want {n} / {rnd}")
+                events = [None, None]
+                dig = [0]
 
-            def on_chunk(b, off, nbytes):
-                k, e0 = nbytes // 8, off // 8
-                if verify_digest:
-                    dig[0] ^= W.xor_digest(ring[i][b].numpy()[:k])
-                with torch.cuda.stream(streams[i]):
-                    devb[i][e0:e0 + k].copy_(ring[i][b][:k], non_blocking=True)
-                    events[b] = torch.cuda.Event()
-                    events[b].record(streams[i])
-                if events[1 - b] is not None:  # the other buffer is received into next
-                    events[1 - b].synchronize()
+                def on_chunk(b, off, nbytes):
+                    k, e0 = nbytes // 8, off // 8
+                    if verify_digest:
+                        dig[0] ^= W.xor_digest(ring[i][b].numpy()[:k])
+                    with torch.cuda.stream(streams[i]):
+                        devb[i][e0:e0 + k].copy_(ring[i][b][:k], non_blocking=True)
+                        events[b] = torch.cuda.Event()
+                        events[b].record(streams[i])
+                    with cond:
+                        j = e0 // ce
+                        ev_in[i][j] = events[b]
+                        arrived[j] += 1
+                        cond.notify_all()
+                    if events[1 - b] is not None:  # the other buffer is received into next
+                        events[1 - b].synchronize()
 
-            W.recv_payload_chunked(conn, h, ring[i], on_chunk)
-            if verify_digest and h.digest != dig[0]:
-                raise W.WireError(f"client {i}: payload digest mismatch")
-            return time.perf_counter()
+                W.recv_payload_chunked(conn, h, ring[i], on_chunk)
+                if verify_digest and h.digest != dig[0]:
+                    raise W.WireError(f"client {i}: payload digest mismatch")
+                with cond:
+                    done_rx[0] += 1
+                    cond.notify_all()
+            except BaseException as e:  # noqa: BLE001 - reported by the coordinator
+                with cond:
+                    errors.append(e)
+                    cond.notify_all()
 
-        with ThreadPoolExecutor(len(self.conns)) as ex:
-            t_recv = max(ex.map(receive, range(len(self.conns))))
-        main = torch.cuda.current_stream(dev)
-        for s in streams:
-            main.wait_stream(s)
-        t1 = time.perf_counter()
-        s_sum = K.sum_u64(devb, torch.empty(n, dtype=torch.int64, device=dev))
-        div = 1.0
-        if average:
-            div = float(len(self.conns)) if all(w is None for w in weights) else float(
-                sum(1.0 if w is None else w for w in weights))
-        dec = K.decode(s_sum, torch.empty(n, dtype=torch.float64, device=dev), fxp_bits=self.fxp_bits, divisor=div)
-        out = dec.cpu().numpy()
-        t2 = time.perf_counter()
+        def send(i):
+            try:
+                conn = self.conns[i]
+                conn.sendall(W.pack_header(W.RESULT, W.F64, 0, rnd, n))
+                host = res_host.numpy()
+                for j, (lo, hi) in enumerate(bounds):
+                    if not ready[j].wait(timeout):
+                        raise TimeoutError(f"result chunk {j} not ready")
+                    if errors:
+                        return
+                    if hi > lo:
+                        conn.sendall(memoryview(host[lo:hi]).cast("B"))
+            except BaseException as e:  # noqa: BLE001
+                with cond:
+                    errors.append(e)
+                    cond.notify_all()
+
+        rx = [threading.Thread(target=receive, args=(i,), daemon=True) for i in range(C)]
+        tx = [threading.Thread(target=send, args=(i,), daemon=True) for i in range(C)]
+        for t in rx + tx:
+            t.start()
+        try:
+            div = None
+            for j, (lo, hi) in enumerate(bounds):
+                with cond:
+                    if not cond.wait_for(lambda: errors or arrived[j] == C or done_rx[0] == C, timeout):
+                        raise TimeoutError(f"chunk {j} not received from every client")
+                    if errors:
+                        raise errors[0]
+                if j == 0:
+                    stamps["first_chunk_all"] = time.perf_counter()
+                if div is None:
+                    div = 1.0
+                    if average:
+                        div = float(C) if all(w is None for w in weights) else float(
+                            sum(1.0 if w is None else w for w in weights))
+                with torch.cuda.stream(agg):
+                    for i in range(C):
+                        if ev_in[i][j] is not None:
+                            agg.wait_event(ev_in[i][j])
+                    if hi > lo:
+                        K.sum_u64([d[lo:hi] for d in devb], s_sum[lo:hi])
+                        K.decode(s_sum[lo:hi], dec[lo:hi], fxp_bits=self.fxp_bits, divisor=div)
+                        res_host[lo:hi].copy_(dec[lo:hi], non_blocking=True)
+                    e = torch.cuda.Event()
+                    e.record(agg)
+                e.synchronize()
+                ready[j].set()
+            stamps["recv_done"] = time.perf_counter()
+            for t in rx:
+                t.join(timeout)
+            for t in tx:
+                t.join(timeout)
+            if errors:
+                raise errors[0]
+        finally:
+            for r in ready:  # release senders on an error
+                r.set()
+        t_end = time.perf_counter()
+        out = res_host.numpy()[:n].copy()
         if keep_masked:
+            for st in streams:
+                st.synchronize()
             self.last_masked = [d.cpu().numpy().view(np.uint64) for d in devb]
-        with ThreadPoolExecutor(len(self.conns)) as ex:  # concurrent sends (sendall drops the GIL)
-            list(ex.map(lambda c: W.send_frame(c, W.RESULT, out, rnd=rnd), self.conns))
-        t3 = time.perf_counter()
-        return out, {"recv_h2d_s": t_recv - t0, "sum_decode_d2h_s": t2 - t1, "broadcast_s": t3 - t2,
-                     "round_s": t3 - t0}
+        return out, {"first_chunk_all_s": stamps["first_chunk_all"] - t0,
+                     "recv_sum_decode_s": stamps["recv_done"] - t0,
+                     "broadcast_tail_s": t_end - stamps["recv_done"],
+                     "round_s": t_end - t0, "chunks": J}
 
     def close(self):
         for c in self.conns:
