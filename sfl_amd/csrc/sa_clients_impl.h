@@ -39,6 +39,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "../../include/sfl_sa.h"
 #include "pcg128.h"
@@ -409,14 +410,24 @@ constexpr bool negated(int c) {
 
 // Draw schedule of a launch: the P streams grouped into interleaved pairs
 // (sa_draw2.h) wherever two streams touch disjoint accumulators (or, for
-// two cross streams of the same client, one shared accumulator), singles
+// two cross streams of one client, one shared accumulator), singles
 // otherwise.  Internal pairs of L clients are matched greedily
 // (for L = 8: 14 disjoint pairs of pairs), cross streams by client.
+//
+// Groups are then ORDERED so that every client is first touched by a draw
+// that ADDS to it (as the adding client u, or as a partner kept negated):
+// such a first touch writes the accumulator from the client's bias constant
+// (an SGPR pair) instead of reading it, so the tile presets no accumulator
+// with v_movs (sa_draw2.h, first-touch variants F).  A client first touched
+// as a subtracting partner or by a single draw (or never, P = 0) is preset
+// instead (`preset`); for every instantiated shape that set is empty or
+// holds only single-draw clients.
 struct Group {
   int qa, qb;          // streams (qb < 0: single draw)
   int ua, va, ub, vb;  // accumulators: u adds t; v < 0: a cross stream (no partner)
   bool va_add, vb_add;  // the partner adds t (it is stored negated) instead of subtracting
   bool fa, fb;          // cross stream of a negated client: inverted sign mask
+  int F;                // first-touch bits: 1 ua, 2 va, 4 ub, 8 vb (sa_draw2.h template argument)
 };
 template <int L, int X>
 struct Sched {
@@ -424,6 +435,7 @@ struct Sched {
   static constexpr int P = PI + L * X;
   int n = 0;
   Group g[P > 0 ? P : 1] = {};
+  uint32_t preset = 0;  // clients whose accumulators the tile presets to the bias
   struct Role {
     int u, v;  // add target, partner (-1: none)
     bool v_add, flip;
@@ -440,6 +452,8 @@ struct Sched {
   }
   constexpr Sched() {
     bool used[P > 0 ? P : 1] = {};
+    Group tmp[P > 0 ? P : 1] = {};
+    int m = 0;
     for (int q = 0; q < P; q++) {
       if (used[q]) continue;
       used[q] = true;
@@ -454,10 +468,60 @@ struct Sched {
       }
       if (mate >= 0) used[mate] = true;
       const Role b = mate >= 0 ? role(mate) : Role{-1, -1, false, false};
-      g[n++] = Group{q, mate, a.u, a.v, b.u, b.v, a.v_add, b.v_add, a.flip, b.flip};
+      tmp[m++] = Group{q, mate, a.u, a.v, b.u, b.v, a.v_add, b.v_add, a.flip, b.flip, 0};
     }
+    // order: repeatedly take the first remaining pair-group none of whose
+    // subtracting partners is untouched yet; singles last among the candidates
+    bool taken[P > 0 ? P : 1] = {};
+    bool seen[kMaxLocal] = {};
+    for (int k = 0; k < m; k++) {
+      int pick = -1;
+      for (int pass = 0; pass < 3 && pick < 0; pass++) {
+        for (int i = 0; i < m && pick < 0; i++) {
+          if (taken[i]) continue;
+          const Group& G = tmp[i];
+          const bool single = G.qb < 0;
+          const bool sub_a = G.va >= 0 && !G.va_add && !seen[G.va];
+          const bool sub_b = G.vb >= 0 && !G.vb_add && !seen[G.vb];
+          if (pass == 0 && !single && !sub_a && !sub_b) pick = i;
+          if (pass == 1 && !sub_a && !sub_b) pick = i;
+          if (pass == 2) pick = i;
+        }
+      }
+      taken[pick] = true;
+      Group G = tmp[pick];
+      int F = 0;
+      const bool single = G.qb < 0;
+      // first touch of each accumulator of this group (u before v, a before b)
+      auto touch = [&](int c, bool adds, int bit) {
+        if (c < 0 || seen[c]) return;
+        seen[c] = true;
+        if (adds && !single) F |= bit;
+        else preset |= 1u << c;
+      };
+      touch(G.ua, true, 1);
+      touch(G.va, G.va_add, 2);
+      touch(G.ub, true, 4);
+      if (G.ub != G.ua) touch(G.vb, G.vb_add, 8);
+      G.F = F;
+      g[n++] = G;
+    }
+    for (int c = 0; c < L; c++)
+      if (!seen[c]) preset |= 1u << c;
   }
 };
+
+template <int L, int X>
+struct SchedOf {
+  static constexpr Sched<L, X> value{};
+};
+
+// f(std::integral_constant<int, 0>{}), ..., f(std::integral_constant<int, N-1>{}):
+// a compile-time loop whose index is a constant expression in the body
+template <typename Fn, int... I>
+__device__ __forceinline__ void for_each_index(Fn&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
 
 // ----------------------------------------------------------------------------
 // the kernel
@@ -621,10 +685,14 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
           pv[c] = bload2<uint64_t>(make_rsrc(ka->c[c].masked_out, cont ? n * 8 : 0), i);
         }
         // accumulators start at the client's folded bias constant (negated
-        // clients: X - bias, see negated<L>)
-        const uint64_t bias = negated<L>(c) ? (uint64_t)X - ka->c[c].bias : ka->c[c].bias;
+        // clients: X - bias, see negated<L>): written by the client's first
+        // draw (first-touch variants), preset here only where the schedule
+        // cannot (Sched::preset)
+        if ((SchedOf<L, X>::value.preset >> c) & 1) {
+          const uint64_t bias = negated<L>(c) ? (uint64_t)X - ka->c[c].bias : ka->c[c].bias;
 #pragma unroll
-        for (int k = 0; k < kE; k++) acc[k][c] = bias;
+          for (int k = 0; k < kE; k++) acc[k][c] = bias;
+        }
       }
     }
 
@@ -632,24 +700,30 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
     // schedule pairs them; group g+1's constants are scalar-loaded during
     // group g's first draw
     if constexpr (P > 0) {
-      constexpr Sched<L, X> S{};
+      using SO = SchedOf<L, X>;  // the schedule (a static constexpr: usable in the lambdas)
       Inc ni[2], nj[2];  // next group's plain-step / tile-jump addends
       uint32_t nm[2];
       auto fetch = [&](int g) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-          const int q = h == 0 ? S.g[g].qa : S.g[g].qb;
+          const int q = h == 0 ? SO::value.g[g].qa : SO::value.g[g].qb;
           if (q < 0) continue;
           kptr_t c = (const kptr_t)(&fenced_args()->s[q]);
           ni[h] = Inc{c[8], c[9], c[3]};
           nj[h] = Inc{c[10], c[11], c[5]};
-          nm[h] = (uint32_t)c[6] ^ ((h == 0 ? S.g[g].fa : S.g[g].fb) ? 0xFFFFFFFFu : 0u);
+          nm[h] = (uint32_t)c[6] ^ ((h == 0 ? SO::value.g[g].fa : SO::value.g[g].fb) ? 0xFFFFFFFFu : 0u);
         }
       };
+      // a first-touched accumulator starts from its client's bias (SGPRs)
+      auto bias_of = [&](int c) -> uint64_t {
+        if (c < 0) return 0;
+        kargs_t* ka = fenced_args();
+        return negated<L>(c) ? (uint64_t)X - ka->c[c].bias : ka->c[c].bias;
+      };
       fetch(0);
-#pragma unroll
-      for (int g = 0; g < S.n; g++) {
-        const Group G = S.g[g];
+      for_each_index([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        constexpr Group G = SO::value.g[g];
         Inc ci[2], cj[2];
         uint32_t m[2];
 #pragma unroll
@@ -658,6 +732,8 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
           cj[h] = nj[h];
           m[h] = nm[h];
         }
+        const uint64_t bua = (G.F & 1) ? bias_of(G.ua) : 0, bva = (G.F & 2) ? bias_of(G.va) : 0;
+        const uint64_t bub = (G.F & 4) ? bias_of(G.ub) : 0, bvb = (G.F & 8) ? bias_of(G.vb) : 0;
 #pragma unroll
         for (int k = 0; k < kE; k++) {
           const uint32_t* mk = k == 0 ? mj : mp;
@@ -665,39 +741,39 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
           const Inc& ib = k == 0 ? cj[1] : ci[1];
           uint32_t* sa = st[G.qa];
           uint64_t* ak = acc[k];
-          if (G.qb < 0) {
-            if (G.va >= 0 && G.va_add)
+          if constexpr (G.qb < 0) {  // singles never first-touch: their clients are preset
+            if constexpr (G.va >= 0 && G.va_add)
               pcg_draw_pair_a(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua],
                               ak[G.va]);
-            else if (G.va >= 0)
+            else if constexpr (G.va >= 0)
               pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua],
                             ak[G.va]);
             else
               pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua]);
           } else {
             uint32_t* sb = st[G.qb];
-#define SA_DRAW2_PAIR(fn)                                                                                   \
-  fn(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], ib, m[1], \
-     zmin, ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb])
-            if (G.va >= 0 && G.va_add && G.vb_add)
+#define SA_DRAW2_PAIR(fn)                                                                                     \
+  fn<G.F>(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], ib, m[1], \
+          zmin, ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb], bua, bva, bub, bvb)
+            if constexpr (G.va >= 0 && G.va_add && G.vb_add)
               SA_DRAW2_PAIR(pcg_draw2_pair_aa);
-            else if (G.va >= 0 && G.va_add)
+            else if constexpr (G.va >= 0 && G.va_add)
               SA_DRAW2_PAIR(pcg_draw2_pair_as);
-            else if (G.va >= 0 && G.vb_add)
+            else if constexpr (G.va >= 0 && G.vb_add)
               SA_DRAW2_PAIR(pcg_draw2_pair_sa);
-            else if (G.va >= 0)
+            else if constexpr (G.va >= 0)
               SA_DRAW2_PAIR(pcg_draw2_pair_ss);
 #undef SA_DRAW2_PAIR
-            else if (G.ua == G.ub)
-              pcg_draw2_one_same(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3],
-                                 ia, m[0], ib, m[1], zmin, ak[G.ua]);
+            else if constexpr (G.ua == G.ub)
+              pcg_draw2_one_same<G.F>(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2],
+                                      mk[3], ia, m[0], ib, m[1], zmin, ak[G.ua], bua);
             else
-              pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia,
-                            m[0], ib, m[1], zmin, ak[G.ua], ak[G.ub]);
+              pcg_draw2_one<G.F>(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3],
+                                 ia, m[0], ib, m[1], zmin, ak[G.ua], ak[G.ub], bua, bub);
           }
-          if (k == 0 && g + 1 < S.n && !(SA_ABLATE & 128)) fetch(g + 1);
+          if (k == 0 && g + 1 < SO::value.n && !(SA_ABLATE & 128)) fetch(g + 1);
         }
-      }
+      }, std::make_integer_sequence<int, SO::value.n>{});
     }
 
     // ---- finish: add the quantized value (or the prior pass), digest, sums

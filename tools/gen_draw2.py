@@ -20,8 +20,20 @@ negated) or subtracts with v_sub_co + v_subb on the pair's 32-bit halves.
 Functions are emitted per (stream a, stream b) second-client mode: "s"
 subtract, "a" add.
 
+First touch: each function is a template over F, a bit set of the block's
+accumulators (bit 0 ua, 1 va, 2 ub, 3 vb) that the tile has not touched yet.
+A first-touched accumulator is not read: its add takes the client's bias
+constant from an SGPR pair instead (v_lshl_add_u64 u, t, 0, s[bias]), so the
+kernel needs no per-tile v_mov to preset the accumulators.  Subtracting
+partners (v_sub_co + v_subb on halves) have no first-touch form: the subb
+would read two SGPRs (bias and borrow), one more than the gfx9 constant bus
+allows; the kernel's schedule orders groups so that no client is first
+touched as a subtracting partner (and presets any that would be).
+
 usage: python tools/gen_draw2.py > sfl_amd/csrc/sa_draw2.h
 """
+
+import re
 
 # one draw: (asm, sgpr_writes, sgpr_reads); {..} fields are renamed per stream
 DRAW = [
@@ -119,43 +131,83 @@ def interleave(a, b):
     return out
 
 
-def emit(name, vma, vmb, same_acc):
+def valid_flags(vma, vmb, same_acc):
+    """First-touch bit sets F a function supports (see the docstring)."""
+    out = []
+    for f in range(16):
+        if (f & 2) and vma != "a":
+            continue
+        if (f & 8) and vmb != "a":
+            continue
+        if same_acc and (f & 4):
+            continue
+        out.append(f)
+    return out
+
+
+def block(vma, vmb, same_acc, f):
+    """(asm lines, outputs, inputs) of one variant."""
     acc_ua, acc_va = "ua", "va"
     acc_ub, acc_vb = ("ua", None) if same_acc else ("ub", "vb")
     a = stream("a", 0, vma, acc_ua, acc_va)
     b = stream("b", 10, vmb, acc_ub, acc_vb)
     seq = interleave(a, b)
-    n_valu = sum(1 for s in seq if s[0].startswith("v_"))
-    n_nop = sum(1 for s in seq if s[0].startswith("s_nop"))
+    first = {"ua": bool(f & 1), "va": bool(f & 2), "ub": bool(f & 4), "vb": bool(f & 8)}
+    lines = []
+    for asm, _, _ in seq:
+        m = re.match(r"v_lshl_add_u64 %\[(\w+)\], (v\[\d+:\d+\]), 0, %\[(\w+)\]$", asm)
+        if m and m.group(1) == m.group(3) and first.get(m.group(1)):
+            if same_acc and m.group(1) == "ua" and any("%[bua]" in x for x in lines):
+                pass  # second cross stream of the same client: adds to the first's result
+            else:
+                asm = f"v_lshl_add_u64 %[{m.group(1)}], {m.group(2)}, 0, %[b{m.group(1)}]"
+        lines.append(asm)
     u64 = ["ua"] + ([] if same_acc else ["ub"]) + [x for x, m in (("va", vma), ("vb", vmb)) if m == "a"]
     split = [x for x, m in (("va", vma), ("vb", vmb)) if m == "s"]
     accs = ["ua"] + (["va"] if vma else []) + ([] if same_acc else ["ub"] + (["vb"] if vmb else []))
-    lines = []
-    lines.append(f"// {name}: {n_valu} VALU + {n_nop} s_nop for two draws")
-    params = ["uint32_t& s0a", "uint32_t& s1a", "uint32_t& s2a", "uint32_t& s3a",
-              "uint32_t& s0b", "uint32_t& s1b", "uint32_t& s2b", "uint32_t& s3b",
-              "uint32_t a0", "uint32_t a1", "uint32_t a2", "uint32_t a3",
-              "const Inc& ia", "uint32_t ma", "const Inc& ib", "uint32_t mb",
-              "uint32_t& zmin"] + [f"uint64_t& {x}" for x in accs]
-    lines.append(f"__device__ __forceinline__ void {name}(" + ", ".join(params) + ") {")
-    lines.append("  uint64_t k1a, k2a, k3a, k1b, k2b, k3b, swb;")
-    for x in split:
-        lines.append(f"  uint32_t {x}lo = (uint32_t){x}, {x}hi = (uint32_t)({x} >> 32);")
-    lines.append("  asm volatile(")
-    for asm, _, _ in seq:
-        lines.append(f'      "{asm}\\n\\t"')
     outs = ['[s0a] "+v"(s0a)', '[s1a] "+v"(s1a)', '[s2a] "+v"(s2a)', '[s3a] "+v"(s3a)',
             '[s0b] "+v"(s0b)', '[s1b] "+v"(s1b)', '[s2b] "+v"(s2b)', '[s3b] "+v"(s3b)', '[zmin] "+v"(zmin)']
-    outs += [f'[{x}] "+v"({x})' for x in accs if x in u64]
+    outs += [f'[{x}] "=&v"({x})' if first[x] else f'[{x}] "+v"({x})' for x in accs if x in u64]
     outs += [f'[{x}{h}] "+v"({x}{h})' for x in split for h in ("lo", "hi")]
     outs += [f'[{k}] "=&s"({k})' for k in ("k1a", "k2a", "k3a", "k1b", "k2b", "k3b", "swb")]
     ins = ['[a0] "v"(a0)', '[a1] "v"(a1)', '[a2] "v"(a2)', '[a3] "v"(a3)',
            '[c0a] "s"(ia.w0)', '[c1a] "s"(ia.w1)', '[c23a] "s"(ia.hi)', '[ma] "s"(ma)',
            '[c0b] "s"(ib.w0)', '[c1b] "s"(ib.w1)', '[c23b] "s"(ib.hi)', '[mb] "s"(mb)']
-    clob = ['"vcc"'] + [f'"v{i}"' for i in range(20)]
-    lines.append("      : " + ", ".join(outs))
-    lines.append("      : " + ", ".join(ins))
-    lines.append("      : " + ", ".join(clob) + ");")
+    ins += [f'[b{x}] "s"(b{x})' for x in accs if x in u64 and first[x]]
+    return lines, outs, ins, seq, split, accs
+
+
+def emit(name, vma, vmb, same_acc):
+    flags = valid_flags(vma, vmb, same_acc)
+    _, _, _, seq, split, accs = block(vma, vmb, same_acc, 0)
+    n_valu = sum(1 for s in seq if s[0].startswith("v_"))
+    n_nop = sum(1 for s in seq if s[0].startswith("s_nop"))
+    lines = []
+    lines.append(f"// {name}: {n_valu} VALU + {n_nop} s_nop for two draws; first-touch sets F in {{{', '.join(map(str, flags))}}}")
+    params = ["uint32_t& s0a", "uint32_t& s1a", "uint32_t& s2a", "uint32_t& s3a",
+              "uint32_t& s0b", "uint32_t& s1b", "uint32_t& s2b", "uint32_t& s3b",
+              "uint32_t a0", "uint32_t a1", "uint32_t a2", "uint32_t a3",
+              "const Inc& ia", "uint32_t ma", "const Inc& ib", "uint32_t mb",
+              "uint32_t& zmin"] + [f"uint64_t& {x}" for x in accs] + [f"uint64_t b{x}" for x in accs]
+    lines.append("template <int F>")
+    lines.append(f"__device__ __forceinline__ void {name}(" + ", ".join(params) + ") {")
+    lines.append("  uint64_t k1a, k2a, k3a, k1b, k2b, k3b, swb;")
+    for x in split:
+        lines.append(f"  uint32_t {x}lo = (uint32_t){x}, {x}hi = (uint32_t)({x} >> 32);")
+    for x in accs:
+        lines.append(f"  (void)b{x};")
+    for i, f in enumerate(flags):
+        body, outs, ins, _, _, _ = block(vma, vmb, same_acc, f)
+        lines.append(f"  {'if' if i == 0 else '} else if'} constexpr (F == {f}) {{")
+        lines.append("    asm volatile(")
+        for asm in body:
+            lines.append(f'        "{asm}\\n\\t"')
+        lines.append("        : " + ", ".join(outs))
+        lines.append("        : " + ", ".join(ins))
+        lines.append("        : " + ", ".join(['"vcc"'] + [f'"v{i}"' for i in range(20)]) + ");")
+    lines.append("  } else {")
+    lines.append("    __builtin_trap();  // no such first-touch variant (the kernel's schedule never asks)")
+    lines.append("  }")
     for x in split:
         lines.append(f"  {x} = ((uint64_t){x}hi << 32) | {x}lo;")
     lines.append("}")
