@@ -220,8 +220,13 @@ class LoopbackServer:
                 t.join(timeout)
             if errors:
                 raise errors[0]
+        except BaseException as e:
+            with cond:  # senders released below must see the failure and send nothing more
+                if e not in errors:
+                    errors.append(e)
+            raise
         finally:
-            for r in ready:  # release senders on an error
+            for r in ready:  # release senders (on an error they stop before sending)
                 r.set()
         t_end = time.perf_counter()
         out = res_host.numpy()[:n].copy()
