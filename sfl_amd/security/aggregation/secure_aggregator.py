@@ -419,7 +419,10 @@ class SecureAggregator(Aggregator):
                 assert mu.position(names[v]) == mv.position(names[u]), "pair streams out of step"
                 pair_gens.append(mu.generator(names[v]))
                 pair_signs.append(mu.sign(names[v]))
-        client_streams = [self._maskers[p.party].streams(self._maskers[p.party].peers) for p in parties]
+        # per-party (generator, sign, peer) lists: the wire path's launches and the
+        # careful-mode rejection fix-up need them (built lazily: 7 jump-aheads a party)
+        client_streams = (None if fusable and not self._careful else
+                          [self._maskers[p.party].streams(self._maskers[p.party].peers) for p in parties])
         if fusable:
             # keep_masked: the same launch also stores every party's masked
             # vector (the wire image) -- pair streams are still expanded once
