@@ -792,13 +792,17 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
     // elements past n only occur in the wave's last tile (uniform test)
     const bool wave_full = base + wave_off + 64 * kE <= n;
     const uint32_t mmask = ka->masked_mask;
+    // per-client XOR digests only when the caller asked for them (a
+    // checksum for tests and the wire path, not part of the reference's
+    // arithmetic): one wave-uniform branch per tile
+    const bool dig_on = ka->do_digest;
     uint64_t sum[kE] = {0, 0};
     auto finish = [&](int c, uint64_t q0, uint64_t q1) {
       const uint64_t a0 = negated<L>(c) ? q0 - acc[0][c] : acc[0][c] + q0;
       const uint64_t a1 = negated<L>(c) ? q1 - acc[1][c] : acc[1][c] + q1;
       sum[0] += a0;
       sum[1] += a1;
-      if (!(SA_ABLATE & 32)) {
+      if (dig_on && !(SA_ABLATE & 32)) {
         const uint64_t d = wave_full ? a0 ^ a1 : (i < n ? a0 : 0) ^ (i + 1 < n ? a1 : 0);
         if constexpr (kDigLds)
           __hip_atomic_fetch_xor(&dig_lds[c][threadIdx.x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
