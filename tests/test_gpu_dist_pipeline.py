@@ -1,0 +1,103 @@
+"""The multi-GPU data path with REAL ranks: W processes, each running its
+block of clients through ``PipelinedMaskedSum`` (the bench's chunked fused
+launches, the comm stream and its per-chunk events, the in-place reduce) on
+the one GPU of the test box.
+
+RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so the
+exchange here is a gloo-backed stand-in with RcclComm's ``reduce_u64``
+contract: on the comm stream, after the chunk's event, the partial sum is
+reduced to the root IN PLACE (recv=None) -- int64 addition wraps like the
+uint64 reduce.  Everything else is the product code path the N > 1 bench
+runs.  The root's buffer must equal the oracle's server sum bit for bit, and
+every client's digest the oracle's."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class GlooReduce:
+    """RcclComm.reduce_u64 stand-in: host round trip through gloo."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+
+    def reduce_u64(self, send, recv, root: int = 0):
+        import torch.distributed as dist
+
+        host = send.cpu()  # on the current (comm) stream: waits for the chunk's launch
+        dist.reduce(host, dst=root, op=dist.ReduceOp.SUM)
+        if self.rank == root:
+            (recv if recv is not None else send).copy_(host, non_blocking=False)
+        return recv
+
+
+def _worker(rank, world, port, n, chunks, offset, q):
+    import torch
+    import torch.distributed as dist
+
+    from oracle import secagg as o
+    from sfl_amd.parallel_sum import PipelinedMaskedSum, plan_generators, plan_rank
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        C = 8
+        names = [f"client{c}" for c in range(C)]
+        seeds = o.seeds_for(names)
+        seed_of = lambda u, v: seeds[names[u]][names[v]]  # noqa: E731
+        rng = np.random.default_rng(77)
+        xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
+        dev = torch.device("cuda", 0)
+        plan = plan_rank(names, world, rank)
+        pipe = PipelinedMaskedSum(GlooReduce(rank, world), dev, n, chunks)
+        gens = [plan_generators(plan, seed_of, offset=offset + lo) for lo, _ in pipe.bounds]
+        part = torch.empty(n, dtype=torch.int64, device=dev)
+        dig = torch.zeros(len(plan.clients), dtype=torch.int64, device=dev)
+        flags = torch.zeros(1, dtype=torch.int32, device=dev)
+        pipe.run([torch.from_numpy(xs[c]).to(dev) for c in plan.clients], [1.0] * len(plan.clients), gens,
+                 plan.n_cross, part, None, digests=dig, flags=flags)
+        torch.cuda.synchronize()
+        masked = o.secure_masked(xs, names, seeds=seeds, offset=offset)
+        dig_ok = [int(d) for d in dig.cpu().numpy().view(np.uint64)] == [o.digest(masked[c]) for c in plan.clients]
+        sum_ok = True
+        if rank == 0:
+            sum_ok = bool(np.array_equal(part.cpu().numpy().view(np.uint64), o.server_sum(masked)))
+        q.put((rank, dig_ok, sum_ok, int(flags.item())))
+        dist.destroy_process_group()
+    except BaseException as e:  # noqa: BLE001 - reported to the parent
+        q.put((rank, repr(e), False, -1))
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 4), (4, 3), (8, 8)])
+def test_ranks_pipeline_and_in_place_reduce(world, chunks):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    n = 50_003
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, chunks, 10**9 + 5, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for rank, dig_ok, sum_ok, fl in res:
+        assert dig_ok is True, (rank, dig_ok)
+        assert sum_ok, f"rank {rank}: root's in-place reduced sum differs from the oracle"
+        assert fl == 0
