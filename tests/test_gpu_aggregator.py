@@ -264,3 +264,32 @@ def test_numpy_scalar_weights_numpy_1_23_semantics(as_list):
     got = got[0] if as_list else got
     exp, _, _ = o.secure_average(xs, names, weights=w, seeds=seeds)
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_zero_size_and_ragged_layers(fused):
+    """Empty arrays (alone and as one layer of a list) aggregate to empty
+    float64 arrays of the same shape; the other layers and the stream
+    positions are unaffected (the next round still matches the oracle)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    names = ["alice", "bob", "carol"]
+    seeds = o.seeds_for(names)
+    pair = {(a, b): seeds[a][b] for a in names for b in names if a != b}
+    pyus = [PYU(nm, 0) for nm in names]
+    agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair, fused=fused)
+    e = rv(agg.sum([p(lambda: np.zeros((0, 3), np.float32))() for p in pyus], axis=0))
+    assert e.shape == (0, 3) and e.dtype == np.float64
+    rng = np.random.default_rng(2)
+    data = [[np.zeros(0, np.float32), (rng.standard_normal(5) * 0.1).astype(np.float32)] for _ in names]
+    got = rv(agg.sum([p(lambda d=d: d)() for p, d in zip(pyus, data)], axis=0))
+    assert got[0].shape == (0,)
+    exp, _, _ = o.secure_sum([d[1] for d in data], names, seeds=seeds)
+    assert np.array_equal(got[1], exp)
+    xs = [(rng.standard_normal(9) * 0.1).astype(np.float32) for _ in names]
+    got = rv(agg.sum([p(lambda x=x: x)() for p, x in zip(pyus, xs)], axis=0))
+    exp, _, _ = o.secure_sum(xs, names, seeds=seeds, offset=5)
+    assert np.array_equal(got, exp)
