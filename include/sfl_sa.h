@@ -15,6 +15,8 @@
  *    on the caller's hipStream_t (passed as void*; NULL = legacy stream).
  *  - the launch functions never allocate, copy or synchronise, so they can be
  *    captured into a hipGraph.  Re-entrant per stream.
+ *  - n == 0 is a no-op that returns SA_OK; the vector pointers of an empty
+ *    call may be NULL (an empty framework tensor has no storage).
  *  - mask-stream generator states are numpy PCG64 states (state, inc) as
  *    128-bit little-endian pairs; the caller advances them between rounds
  *    with sa_pcg64_advance(), exactly like the reference's persistent

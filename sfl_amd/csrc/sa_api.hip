@@ -146,6 +146,7 @@ int sa_mask_impl(const void* x, int x_type, int compute_type, uint64_t n, double
                  uint64_t* digest, uint32_t* flags, void* stream, const sa_dp* dp) {
   if (check_type(x_type, "sa_mask x_type") || check_type(compute_type, "sa_mask compute_type"))
     return SA_ERR_ARG;
+  if (n == 0 && n_streams >= 0 && fxp_bits >= 0 && fxp_bits <= 62) return SA_OK;  // nothing to touch
   if (!out || n_streams < 0 || (n_streams > 0 && !streams) || fxp_bits < 0 || fxp_bits > 62) {
     sa_set_error("sa_mask: bad arguments (out=%p n_streams=%d fxp_bits=%d)", (void*)out,
                  n_streams, fxp_bits);
@@ -221,6 +222,7 @@ extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, i
   if (check_type(x_type, "sa_fused_clients x_type")) return SA_ERR_ARG;
   const int L = n_clients;
   const int PI = L * (L - 1) / 2;
+  if (n == 0 && L >= 1 && n_cross >= 0 && fxp_bits >= 0 && fxp_bits <= 62) return SA_OK;  // empty vectors
   if (!clients || L < 1 || n_cross < 0 || !sum_out || fxp_bits < 0 ||
       fxp_bits > 62 || (PI > 0 && (!pair_gens || !pair_sign)) || (n_cross > 0 && !cross)) {
     sa_set_error("sa_fused_clients: bad arguments (n_clients=%d n_cross=%d)", L, n_cross);
@@ -302,6 +304,7 @@ extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, i
 
 extern "C" int sa_sum_u64(const uint64_t* const* in, int k, uint64_t n, uint64_t* out,
                           void* stream) {
+  if (k >= 1 && n == 0) return SA_OK;  // empty vectors (their pointers may be null)
   if (!in || k < 1 || !out) {
     sa_set_error("sa_sum_u64: bad arguments (k=%d)", k);
     return SA_ERR_ARG;
@@ -336,7 +339,7 @@ extern "C" int sa_sum_u64(const uint64_t* const* in, int k, uint64_t n, uint64_t
 
 extern "C" int sa_decode(const uint64_t* s, uint64_t n, int fxp_bits, double divisor,
                          const double* divisor_vec, double* out, void* stream) {
-  if (!s || !out || fxp_bits < 0 || fxp_bits > 62) {
+  if (fxp_bits < 0 || fxp_bits > 62 || (n > 0 && (!s || !out))) {
     sa_set_error("sa_decode: bad arguments");
     return SA_ERR_ARG;
   }
@@ -351,11 +354,11 @@ extern "C" int sa_decode(const uint64_t* s, uint64_t n, int fxp_bits, double div
 }
 
 extern "C" int sa_sum_f64(const double* const* w, int k, uint64_t n, double* out, void* stream) {
+  if (k >= 1 && n == 0) return SA_OK;
   if (!w || k < 1 || !out) {
     sa_set_error("sa_sum_f64: bad arguments");
     return SA_ERR_ARG;
   }
-  if (n == 0) return SA_OK;
   const int grid = stream_grid(n, (const void*)&k_sum_f64);
   if (grid < 0) return SA_ERR_HIP;
   for (int j0 = 0; j0 < k;) {

@@ -90,7 +90,7 @@ static bool dp_ok(const sa_dp* dp, const char* who) {
 
 extern "C" int sa_sumsq_f32(const float* x, uint64_t n, double* partials, double* sumsq, int accumulate,
                             void* stream) {
-  if (!x || !partials || !sumsq || ((uintptr_t)x & 15)) {
+  if ((n > 0 && !x) || !partials || !sumsq || ((uintptr_t)x & 15)) {  // n == 0: x unread, *sumsq (+)= 0
     sa_set_error("sa_sumsq_f32: bad arguments (x must be 16-byte aligned)");
     return SA_ERR_ARG;
   }
@@ -109,7 +109,7 @@ extern "C" int sa_sumsq_f32(const float* x, uint64_t n, double* partials, double
 }
 
 extern "C" int sa_dp_perturb_f32(const float* x, uint64_t n, const sa_dp* dp, float* out, void* stream) {
-  if (!x || !out || ((uintptr_t)x & 15) || ((uintptr_t)out & 15)) {
+  if ((n > 0 && (!x || !out)) || ((uintptr_t)x & 15) || ((uintptr_t)out & 15)) {
     sa_set_error("sa_dp_perturb_f32: bad arguments (16-byte aligned x and out required)");
     return SA_ERR_ARG;
   }
@@ -129,7 +129,7 @@ extern "C" int sa_dp_perturb_f32(const float* x, uint64_t n, const sa_dp* dp, fl
 extern "C" int sa_mask_dp(const float* x, uint64_t n, double weight, int fxp_bits, const sa_mask_stream* streams,
                           int n_streams, const sa_dp* dp, uint64_t* out, uint64_t* sum_accum, uint64_t* digest,
                           uint32_t* flags, void* stream) {
-  if (!x) {
+  if (!x && n > 0) {
     sa_set_error("sa_mask_dp: x is required");
     return SA_ERR_ARG;
   }
