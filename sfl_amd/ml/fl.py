@@ -263,14 +263,17 @@ class FedAvgU(FedAvgW):
 
 class FedAvgG(FedAvgW):
     """``fed_avg_g`` worker (sfl/ml/nn/fl/backend/torch/strategy/fed_avg_g.py:
-    28-112): clients upload the gradients accumulated over the round and step
-    their optimizer with the aggregated gradients.  Two deviations, both
-    about the reference's plumbing rather than the aggregation: the
-    reference's ``local_gradients_sum += local_gradients`` (:91) concatenates
-    the Python lists, so here the per-step gradients are summed element-wise
-    (identical for ``train_steps == 1``, i.e. ``aggregate_freq=1``); and the
-    aggregate (float64 out of the secure decode) is cast to each parameter's
-    dtype before it becomes ``p.grad`` (mixins.py:99-111 assigns it as is)."""
+    28-112): clients upload the gradients of the round and step their
+    optimizer with the aggregated gradients.  As in the reference,
+    ``local_gradients_sum += local_gradients`` (:91) CONCATENATES the
+    per-step gradient lists, so with ``aggregate_freq = k`` the payload the
+    aggregator sees is k x the parameter list (k x the mask-stream draws per
+    round), and ``set_gradients`` zips it with the parameters
+    (mixins.py:99-111), i.e. steps with the first local step's aggregated
+    gradients.  One deviation, about the reference's plumbing rather than
+    the aggregation: the aggregate (float64 out of the secure decode) is cast
+    to each parameter's dtype before it becomes ``p.grad`` (the reference
+    assigns it as is, which torch rejects for float32 parameters)."""
 
     def _set_gradients(self, gradients):
         for g, prm in zip(gradients, self.model.parameters()):
@@ -296,7 +299,7 @@ class FedAvgG(FedAvgW):
             loss.backward()
             grads = [None if prm.grad is None else prm.grad.detach().cpu().numpy().copy()
                      for prm in self.model.parameters()]  # mixins.py:91-97
-            grad_sum = grads if grad_sum is None else [a + b for a, b in zip(grad_sum, grads)]
+            grad_sum = grads if grad_sum is None else grad_sum + grads  # list += list: concatenation (:91)
         self.last_loss = float(loss.item()) if loss is not None else float("nan")
         if dp_strategy is not None and dp_strategy.model_gdp is not None:
             grad_sum = dp_strategy.model_gdp(grad_sum)
