@@ -447,3 +447,36 @@ def test_chunked_launch_past_4gib():
         assert np.array_equal(_u64(outs[0][lo:lo + 40]), q0.view(np.uint64) + m), lo
     del xs, outs, mo
     torch.cuda.empty_cache()
+
+
+def test_launches_capture_into_a_graph():
+    """include/sfl_sa.h promises launch functions that never allocate, copy
+    or synchronise: the fused masking launch and the decode captured into a
+    HIP graph (torch.cuda.CUDAGraph on ROCm) replay to the eager results."""
+    K, L = _K(), _L()
+    C, n = 4, 100_003
+    names, xs, seeds, pg, ps = _fused_setup(C, n, 0)
+    xd = [torch.from_numpy(x).to(DEV) for x in xs]
+    s_e = torch.empty(n, dtype=torch.int64, device=DEV)
+    d_e = torch.empty(n, dtype=torch.float64, device=DEV)
+    K.fused_clients(xd, [1.0] * C, pg, ps, [], 0, s_e)
+    K.decode(s_e, d_e, divisor=float(C))
+    s_g = torch.zeros(n, dtype=torch.int64, device=DEV)
+    d_g = torch.zeros(n, dtype=torch.float64, device=DEV)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g):
+            K.fused_clients(xd, [1.0] * C, pg, ps, [], 0, s_g)
+            K.decode(s_g, d_g, divisor=float(C))
+    torch.cuda.current_stream().wait_stream(side)
+    for _ in range(2):
+        s_g.zero_()
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(s_g, s_e)
+    assert torch.equal(d_g, d_e)
+    masked = o.secure_masked(xs, names, seeds=seeds)
+    assert np.array_equal(_u64(s_g), o.server_sum(masked))
