@@ -214,12 +214,12 @@ class LoopbackServer:
                 e.synchronize()
                 ready[j].set()
             stamps["recv_done"] = time.perf_counter()
-            for t in rx:
-                t.join(timeout)
-            for t in tx:
+            for t in rx + tx:
                 t.join(timeout)
             if errors:
                 raise errors[0]
+            if any(t.is_alive() for t in rx + tx):
+                raise TimeoutError("a party's receive or result send did not finish")
         except BaseException as e:
             with cond:  # senders released below must see the failure and send nothing more
                 if e not in errors:
