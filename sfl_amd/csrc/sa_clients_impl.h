@@ -817,9 +817,40 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
 #pragma unroll
       for (int c = 0; c < L; c++) finish(c, pv[kGeneral ? c : 0].v[0], pv[kGeneral ? c : 0].v[1]);
     } else if (__builtin_expect(fast_products<XT, CT, L, kGeneral>(xv, wv, ka, qs, p), 1)) {
+      if (!dig_on && mmask == 0) {
+        // Only the sum leaves the tile: sum = sum_plain (acc + q) +
+        // sum_negated (q - st) = A - B with A = sum_plain acc + sum_plain q
+        // and B = sum_negated st - sum_negated q; each int32 q enters
+        // sign-extended through one v_mad_i64_i32 (q * (+-1) + A), instead
+        // of a sign extension plus a 64-bit add per client (and a subtract
+        // pair for negated clients).
 #pragma unroll
-      for (int c = 0; c < L; c++)
-        finish(c, (uint64_t)(int64_t)(int32_t)p[c][0], (uint64_t)(int64_t)(int32_t)p[c][1]);
+        for (int k = 0; k < kE; k++) {
+          uint64_t A = 0, B = 0;
+          bool a0 = false, b0 = false;
+#pragma unroll
+          for (int c = 0; c < L; c++) {
+            uint64_t& t = negated<L>(c) ? B : A;
+            bool& t0 = negated<L>(c) ? b0 : a0;
+            t = t0 ? t + acc[k][c] : acc[k][c];
+            t0 = true;
+          }
+#pragma unroll
+          for (int c = 0; c < L; c++) {
+            const int32_t q = (int32_t)p[c][k];
+            uint64_t kc;
+            if (negated<L>(c))
+              asm("v_mad_i64_i32 %[d], %[k], %[q], -1, %[d]" : [d] "+v"(B), [k] "=s"(kc) : [q] "v"(q));
+            else
+              asm("v_mad_i64_i32 %[d], %[k], %[q], 1, %[d]" : [d] "+v"(A), [k] "=s"(kc) : [q] "v"(q));
+          }
+          sum[k] = A - B;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < L; c++)
+          finish(c, (uint64_t)(int64_t)(int32_t)p[c][0], (uint64_t)(int64_t)(int32_t)p[c][1]);
+      }
     } else {
 #pragma unroll
       for (int c = 0; c < L; c++)

@@ -191,6 +191,13 @@ def test_fused_clients_bit_exact(C, n):
     ref = o.decode(s_exp)
     assert np.array_equal(dec.cpu().numpy(), ref)
     assert np.abs(ref - np.sum(np.stack(xs).astype(np.float64), axis=0)).max() < C * 2.0**-18
+    # the sum-only finish (no digests, no wire images: the bench's launch),
+    # stored and accumulated
+    s2 = torch.empty(n, dtype=torch.int64, device=DEV)
+    K.fused_clients(xt, [1.0] * C, pg, ps, [], 0, s2, flags=flags)
+    K.fused_clients(xt, [1.0] * C, pg, ps, [], 0, s2, accumulate=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(s2), s_exp + s_exp)
 
 
 @pytest.mark.parametrize("C", [4, 8])
