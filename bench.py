@@ -286,10 +286,11 @@ def workload(args, world: int) -> str:
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    # 200 timed steps (~0.5 s of kernels at N=1): long enough for an outside
-    # utilisation sampler to see the GPU busy; 20 warm-up steps cover the
+    # 2000 timed steps (~4.3 s of kernels at N=1, ~5-30 s at N>1 where the
+    # exchange bounds a step): long enough for an outside utilisation sampler
+    # to catch the GPU busy; 20 warm-up steps cover the
     # clock ramp after idle (the first ~8 launches run long)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--elems", type=int, default=100_000_000)
