@@ -354,9 +354,13 @@ def test_full_size_properties(C, n):
         K.mask(xs[c], out, st, digest=wdig[c:c + 1])
         wire.append(out)
     s2 = K.sum_u64(wire, torch.empty(n, dtype=torch.int64, device=DEV))
+    # the bench's launch: no digests, no wire images (the sum-only finish)
+    s3 = torch.empty(n, dtype=torch.int64, device=DEV)
+    K.fused_clients(xs, [1.0] * C, pg, ps, [], 0, s3)
     torch.cuda.synchronize()
     assert torch.equal(s, q_sum)
     assert torch.equal(s, s2)
+    assert torch.equal(s, s3)
     assert torch.equal(dig, wdig)
     assert int(flags.item()) == 0
     # (3) oracle spot checks of individual masked elements at far offsets

@@ -109,6 +109,12 @@ def test_per_rank_shapes_full_size(W):
         flags = torch.zeros(1, dtype=torch.int32, device=dev)
         pipe.run(local, [1.0] * Lc, gens, plan.n_cross, part, None, digests=dig, flags=flags)
         total += part
+        # as bench.py launches it: no digests (the kernel's sum-only finish)
+        part_so = torch.empty(n, dtype=torch.int64, device=dev)
+        pipe.run(local, [1.0] * Lc, gens, plan.n_cross, part_so, None)
+        torch.cuda.synchronize()
+        assert torch.equal(part_so, part), r
+        del part_so
         wire, wdig = [], torch.zeros(Lc, dtype=torch.int64, device=dev)
         for i, c in enumerate(plan.clients):
             st = [(L.pcg64_advance(L.pcg64_from_seed(seed_of(c, v)), offset), 1 if names[v] > names[c] else -1, v)
