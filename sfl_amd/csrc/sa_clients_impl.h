@@ -578,7 +578,13 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
 
   // ---- prologue: park every stream one tile jump before S_{first+1}, the
   // state element `first` is drawn from: V = A^-J (S_{first+1} - inc*G_J)
-  uint32_t st[P > 0 ? P : 1][4];  // 128-bit states as 32-bit limbs
+  // 128-bit states: limbs 0-1 as one 64-bit VGPR pair (the draw's first
+  // mad writes it in place, sa_draw2.h), limbs 2 and 3 as 32-bit VGPRs
+  struct State {
+    uint64_t p01;
+    uint32_t s2, s3;
+  };
+  State st[P > 0 ? P : 1];
   if constexpr (P > 0) {
     // J(first + 1) = J(blockIdx * kTile) o J(lane * kE + 1)
     // Block part: a fixed, fully unrolled bit loop (grids stay below 2^12
@@ -600,10 +606,9 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
       const StreamArg& s = a.s[j];
       const u128 sf = apply(jl, ld128(s.s_lo, s.s_hi), ld128(s.inc_lo, s.inc_hi));
       const u128 v = aji * (sf - ld128(s.cj_lo, s.cj_hi));
-      st[j][0] = (uint32_t)lo64(v);
-      st[j][1] = (uint32_t)(lo64(v) >> 32);
-      st[j][2] = (uint32_t)hi64(v);
-      st[j][3] = (uint32_t)(hi64(v) >> 32);
+      st[j].p01 = lo64(v);
+      st[j].s2 = (uint32_t)hi64(v);
+      st[j].s3 = (uint32_t)(hi64(v) >> 32);
     }
   }
   // multiplier limbs: jump (first element of a tile) and plain step
@@ -739,22 +744,22 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
           const uint32_t* mk = k == 0 ? mj : mp;
           const Inc& ia = k == 0 ? cj[0] : ci[0];
           const Inc& ib = k == 0 ? cj[1] : ci[1];
-          uint32_t* sa = st[G.qa];
+          State& sa = st[G.qa];
           uint64_t* ak = acc[k];
           if constexpr (G.qb < 0) {  // singles never first-touch: their clients are preset
+            uint32_t s0 = (uint32_t)sa.p01, s1 = (uint32_t)(sa.p01 >> 32);
             if constexpr (G.va >= 0 && G.va_add)
-              pcg_draw_pair_a(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua],
-                              ak[G.va]);
+              pcg_draw_pair_a(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua], ak[G.va]);
             else if constexpr (G.va >= 0)
-              pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua],
-                            ak[G.va]);
+              pcg_draw_pair(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua], ak[G.va]);
             else
-              pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua]);
+              pcg_draw_one(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua]);
+            sa.p01 = ((uint64_t)s1 << 32) | s0;
           } else {
-            uint32_t* sb = st[G.qb];
-#define SA_DRAW2_PAIR(fn)                                                                                     \
-  fn<G.F>(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia, m[0], ib, m[1], \
-          zmin, ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb], bua, bva, bub, bvb)
+            State& sb = st[G.qb];
+#define SA_DRAW2_PAIR(fn)                                                                                 \
+  fn<G.F>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], ib, m[1], zmin, \
+          ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb], bua, bva, bub, bvb)
             if constexpr (G.va >= 0 && G.va_add && G.vb_add)
               SA_DRAW2_PAIR(pcg_draw2_pair_aa);
             else if constexpr (G.va >= 0 && G.va_add)
@@ -765,11 +770,11 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
               SA_DRAW2_PAIR(pcg_draw2_pair_ss);
 #undef SA_DRAW2_PAIR
             else if constexpr (G.ua == G.ub)
-              pcg_draw2_one_same<G.F>(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2],
-                                      mk[3], ia, m[0], ib, m[1], zmin, ak[G.ua], bua);
+              pcg_draw2_one_same<G.F>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia,
+                                      m[0], ib, m[1], zmin, ak[G.ua], bua);
             else
-              pcg_draw2_one<G.F>(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3],
-                                 ia, m[0], ib, m[1], zmin, ak[G.ua], ak[G.ub], bua, bub);
+              pcg_draw2_one<G.F>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0],
+                                 ib, m[1], zmin, ak[G.ua], ak[G.ub], bua, bub);
           }
           if (k == 0 && g + 1 < SO::value.n && !(SA_ABLATE & 128)) fetch(g + 1);
         }

@@ -113,3 +113,24 @@ def test_limb_equations_equal_numpy_pcg64():
         x, r = hi ^ lo, hi >> 58
         out = ((x >> r) | (x << (64 - r))) & ((1 << 64) - 1)
         assert out == int(gen.random_raw())
+
+
+def test_pair01_isa_check_flags_a_broken_alias(tmp_path):
+    """tools/check_pair01.py (run by the Makefile on every build of the
+    masking kernels) accepts a draw block whose state pair is written in
+    place and rejects one where the compiler put limb 0 / limb 1 elsewhere."""
+    good = """;;#ASMSTART
+\tv_mad_u64_u32 v[2:3], s[40:41], v30, v41, s[4:5]
+\tv_mad_u64_u32 v[30:31], s[42:43], v30, v40, s[6:7]
+\tv_add_co_u32_e64 v31, s[44:45], v31, v2
+;;#ASMEND
+"""
+    bad_src = good.replace("v[30:31], s[42:43], v30", "v[30:31], s[42:43], v28")
+    bad_add = good.replace("v_add_co_u32_e64 v31, s[44:45], v31", "v_add_co_u32_e64 v29, s[44:45], v29")
+    tool = os.path.join(ROOT, "tools", "check_pair01.py")
+    rcs = []
+    for i, text in enumerate((good, bad_src, bad_add)):
+        p = tmp_path / f"k{i}.s"
+        p.write_text(text)
+        rcs.append(subprocess.run([sys.executable, tool, str(p)], capture_output=True).returncode)
+    assert rcs == [0, 1, 1]

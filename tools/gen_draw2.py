@@ -5,7 +5,10 @@ instruction streams interleaved so every dependent pair of one stream sits at
 least two issue slots apart (the other stream's instruction fills the gap).
 
 The single-draw schedule is SA_PCG_DRAW_ASM in sa_clients_impl.h; this script
-keeps its instructions, renames stream B onto its own scratch VGPRs
+keeps its instructions except one -- limbs 0-1 of a state are one VGPR pair
+that the first column's mad (moved after the last read of limbs 0-1)
+writes in place, so the single draw's v_mov of the new limb 0 is gone --
+renames stream B onto its own scratch VGPRs
 (v10-v19), carry SGPR pairs and a swap mask in an SGPR pair instead of VCC,
 merges the two raw==0 running minimums into one v_min3, and checks the gfx950
 rule the single draw already follows: a VALU-written SGPR (carry, VCC) is
@@ -34,6 +37,17 @@ usage: python tools/gen_draw2.py > sfl_amd/csrc/sa_draw2.h
 """
 
 import re
+import sys
+
+# Limbs 0-1 of each state live in one 64-bit VGPR pair (operand p01, "+v");
+# the first column's mad writes that pair directly (its low word IS the new
+# limb 0, its high word the partial limb 1 that the add then completes in
+# place), so the draw needs no v_mov.  The 32-bit operands s0 / s1 are
+# inputs the compiler places in the pair's two halves (reads of limbs 0-1
+# all come before the pair is written) -- build-checked by
+# tools/check_pair01.py on the ISA.  --no-pair01 emits the earlier form
+# (limbs in four 32-bit operands, the new limb 0 moved in from scratch).
+PAIR01 = "--no-pair01" not in sys.argv
 
 # one draw: (asm, sgpr_writes, sgpr_reads); {..} fields are renamed per stream
 DRAW = [
@@ -85,7 +99,23 @@ def stream(tag, base, vmode, acc_u, acc_v):
         f["cnd_lo"] = f"v_cndmask_b32_e64 v{base + 6}, v{base + 4}, v{base + 5}, %[swb]"
         f["cnd_hi"] = f"v_cndmask_b32_e64 v{base + 7}, v{base + 5}, v{base + 4}, %[swb]"
     out = []
-    for asm, w, r in DRAW:
+    draw = DRAW
+    if PAIR01:
+        f["p01"] = f"p01{tag}"
+        e0 = None
+        draw = []
+        for asm, w, r in DRAW:
+            if asm.startswith("v_mad_u64_u32 v[{v0}:{v1}]"):
+                e0 = (asm.replace("v[{v0}:{v1}]", "%[{p01}]"), w, r)
+                continue
+            if asm.startswith("v_mov_b32_e32 %[{s0}]"):
+                continue
+            asm = asm.replace("v_add_co_u32_e64 %[{s1}], %[{k3}], v{v1}, v{v2}",
+                              "v_add_co_u32_e64 %[{s1}], %[{k3}], %[{s1}], v{v2}")
+            draw.append((asm, w, r))
+            if asm.startswith("v_mad_u64_u32 v[{v6}:{v7}], %[{k3}], %[{s1}], %[a2]"):
+                draw.append(e0)  # after the last read of limbs 0 and 1
+    for asm, w, r in draw:
         if asm == "VADD":
             if vmode != "a":
                 continue
@@ -167,6 +197,9 @@ def block(vma, vmb, same_acc, f):
     accs = ["ua"] + (["va"] if vma else []) + ([] if same_acc else ["ub"] + (["vb"] if vmb else []))
     outs = ['[s0a] "+v"(s0a)', '[s1a] "+v"(s1a)', '[s2a] "+v"(s2a)', '[s3a] "+v"(s3a)',
             '[s0b] "+v"(s0b)', '[s1b] "+v"(s1b)', '[s2b] "+v"(s2b)', '[s3b] "+v"(s3b)', '[zmin] "+v"(zmin)']
+    if PAIR01:
+        outs = ['[p01a] "+v"(p01a)', '[s2a] "+v"(s2a)', '[s3a] "+v"(s3a)',
+                '[p01b] "+v"(p01b)', '[s2b] "+v"(s2b)', '[s3b] "+v"(s3b)', '[zmin] "+v"(zmin)']
     outs += [f'[{x}] "=&v"({x})' if first[x] else f'[{x}] "+v"({x})' for x in accs if x in u64]
     outs += [f'[{x}{h}] "+v"({x}{h})' for x in split for h in ("lo", "hi")]
     outs += [f'[{k}] "=&s"({k})' for k in ("k1a", "k2a", "k3a", "k1b", "k2b", "k3b", "swb")]
@@ -174,6 +207,8 @@ def block(vma, vmb, same_acc, f):
            '[c0a] "s"(ia.w0)', '[c1a] "s"(ia.w1)', '[c23a] "s"(ia.hi)', '[ma] "s"(ma)',
            '[c0b] "s"(ib.w0)', '[c1b] "s"(ib.w1)', '[c23b] "s"(ib.hi)', '[mb] "s"(mb)']
     ins += [f'[b{x}] "s"(b{x})' for x in accs if x in u64 and first[x]]
+    if PAIR01:
+        ins += ['[s0a] "v"(s0a)', '[s1a] "v"(s1a)', '[s0b] "v"(s0b)', '[s1b] "v"(s1b)']
     return lines, outs, ins, seq, split, accs
 
 
@@ -184,8 +219,11 @@ def emit(name, vma, vmb, same_acc):
     n_nop = sum(1 for s in seq if s[0].startswith("s_nop"))
     lines = []
     lines.append(f"// {name}: {n_valu} VALU + {n_nop} s_nop for two draws; first-touch sets F in {{{', '.join(map(str, flags))}}}")
-    params = ["uint32_t& s0a", "uint32_t& s1a", "uint32_t& s2a", "uint32_t& s3a",
-              "uint32_t& s0b", "uint32_t& s1b", "uint32_t& s2b", "uint32_t& s3b",
+    st_params = (["uint64_t& p01a", "uint32_t& s2a", "uint32_t& s3a", "uint64_t& p01b", "uint32_t& s2b", "uint32_t& s3b"]
+                 if PAIR01 else
+                 ["uint32_t& s0a", "uint32_t& s1a", "uint32_t& s2a", "uint32_t& s3a",
+                  "uint32_t& s0b", "uint32_t& s1b", "uint32_t& s2b", "uint32_t& s3b"])
+    params = st_params + [
               "uint32_t a0", "uint32_t a1", "uint32_t a2", "uint32_t a3",
               "const Inc& ia", "uint32_t ma", "const Inc& ib", "uint32_t mb",
               "uint32_t& zmin"] + [f"uint64_t& {x}" for x in accs] + [f"uint64_t b{x}" for x in accs]
@@ -196,6 +234,10 @@ def emit(name, vma, vmb, same_acc):
         lines.append(f"  uint32_t {x}lo = (uint32_t){x}, {x}hi = (uint32_t)({x} >> 32);")
     for x in accs:
         lines.append(f"  (void)b{x};")
+    if PAIR01:
+        lines.append("  // limbs 0 / 1 as 32-bit inputs: the halves of p01 (aliasing build-checked)")
+        for t in "ab":
+            lines.append(f"  const uint32_t s0{t} = (uint32_t)p01{t}, s1{t} = (uint32_t)(p01{t} >> 32);")
     for i, f in enumerate(flags):
         body, outs, ins, _, _, _ = block(vma, vmb, same_acc, f)
         lines.append(f"  {'if' if i == 0 else '} else if'} constexpr (F == {f}) {{")
