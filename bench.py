@@ -306,12 +306,26 @@ def main():
                     help="also fold every client's masked values into an XOR digest (test checksum)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher rehearsal without a GPU: ranks join a gloo group, rank 0 prints one line")
+    ap.add_argument("--watchdog-seconds", type=float, default=900.0,
+                    help="a rank still running after this long exits with status 3 (a hung collective "
+                         "cannot be interrupted from Python; torchrun then stops the other ranks); 0 disables")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dist):
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.watchdog_seconds > 0:
+        import threading
+
+        def _expire():
+            print(f"bench.py rank {rank}: still running after {args.watchdog_seconds:.0f} s, exiting",
+                  file=sys.stderr, flush=True)
+            os._exit(3)
+
+        wd = threading.Timer(args.watchdog_seconds, _expire)
+        wd.daemon = True
+        wd.start()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # CPU baseline first: its per-client worker processes are forked, which
