@@ -224,7 +224,6 @@ __device__ __forceinline__ bool fast_products(const Vec2<XT> (&xv)[L], const Vec
                                               const QScale& qs, float (&p)[L][kE]) {
   if constexpr (std::is_same<CT, float>::value) {
     typedef float f2 __attribute__((ext_vector_type(2)));
-    bool ok = true;
 #pragma unroll
     for (int c = 0; c < L; c++) {
       const bool has_wv = kGeneral && ka->c[c].wvec;
@@ -241,9 +240,19 @@ __device__ __forceinline__ bool fast_products(const Vec2<XT> (&xv)[L], const Vec
         p[c][0] = p2[0];
         p[c][1] = p2[1];
       }
-#pragma unroll
-      for (int k = 0; k < kE; k++) ok = ok && (__builtin_fabsf(p[c][k]) < 0x1p31f);
     }
+    // The vote: the largest |p| of the lane through gfx950's NaN-propagating
+    // v_maximum3_f32 (IEEE 754-2019 maximum: a NaN operand yields NaN, which
+    // then fails the < 2^31 test like an infinity), one instruction per two
+    // products instead of one compare each.
+    const float* q = &p[0][0];
+    constexpr int kN = L * kE;
+    float mx;
+    asm("v_maximum3_f32 %0, |%1|, |%2|, |%3|" : "=v"(mx) : "v"(q[0]), "v"(q[1 % kN]), "v"(q[2 % kN]));
+#pragma unroll
+    for (int i = 3; i < kN; i += 2)
+      asm("v_maximum3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(q[i]), "v"(q[i + 1 < kN ? i + 1 : i]));
+    const bool ok = mx < 0x1p31f;
     return !__any(!ok) || (SA_ABLATE & 2);
   } else {
     return false;
