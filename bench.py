@@ -378,8 +378,12 @@ def main():
     kev = []  # (start, end) events around every masking launch of the timed steps (compute stream)
 
     def step(i, timed_idx=None):
+        # join=False: a round's exchange tail overlaps the next round's first
+        # launches (each chunk's launch still waits for that chunk's previous
+        # reduce); the timed region ends with a device synchronise
         pipe.run(xs, [1.0] * Lc, gens[i], plan.n_cross, sum_buf, None, fxp_bits=args.fxp_bits,
-                 digests=digests, flags=flags, kernel_events=kev if timed_idx is not None else None)
+                 digests=digests, flags=flags, kernel_events=kev if timed_idx is not None else None,
+                 join=False)
 
     for i in range(args.warmup):
         step(i)

@@ -147,12 +147,21 @@ class PipelinedMaskedSum:
         self.bounds = chunk_bounds(n, chunks)
         self.comm_stream = torch.cuda.Stream(device) if comm is not None else None
         self.events = [torch.cuda.Event() for _ in self.bounds]
+        # reduce of chunk j done (comm stream): the next round's chunk-j launch
+        # waits for it, and for nothing else of the previous round
+        self.reduced = [torch.cuda.Event() for _ in self.bounds]
+        self._pending = [False] * len(self.bounds)
 
     def run(self, xs, weights, chunk_gens, n_cross: int, sum_buf, recv=None, *, root: int = 0,
-            fxp_bits: int = 18, digests=None, flags=None, kernel_events: list | None = None):
+            fxp_bits: int = 18, digests=None, flags=None, kernel_events: list | None = None,
+            join: bool = True):
         """``kernel_events``: if given, a timing-event pair recorded around
         each chunk's masking launch is appended (kernel time without the
-        exchange)."""
+        exchange).  ``join=False`` leaves the last reduces running on the
+        comm stream (the caller synchronises the device before reading the
+        result); a following run() still orders each chunk's launch after
+        that chunk's previous reduce, so back-to-back rounds overlap one
+        round's exchange tail with the next round's first launches."""
         import torch
 
         from . import kernels as K
@@ -162,6 +171,9 @@ class PipelinedMaskedSum:
         compute = torch.cuda.current_stream(self.device)
         for j, (lo, hi) in enumerate(self.bounds):
             pg, ps, cross = chunk_gens[j]
+            if self._pending[j]:  # the previous round's reduce of this chunk still reads sum_buf
+                compute.wait_event(self.reduced[j])
+                self._pending[j] = False
             if kernel_events is not None:
                 kernel_events.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
                 kernel_events[-1][0].record(compute)
@@ -174,6 +186,9 @@ class PipelinedMaskedSum:
                 self.comm_stream.wait_event(self.events[j])
                 with torch.cuda.stream(self.comm_stream):
                     self.comm.reduce_u64(sum_buf[lo:hi], recv[lo:hi] if recv is not None else None, root=root)
-        if self.comm is not None:
+                    self.reduced[j].record(self.comm_stream)
+                self._pending[j] = True
+        if self.comm is not None and join:
             compute.wait_stream(self.comm_stream)
+            self._pending = [False] * len(self.bounds)
         return recv if recv is not None else sum_buf

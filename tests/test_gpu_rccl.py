@@ -76,3 +76,37 @@ def test_pipelined_masked_sum_matches_oracle(comm, chunks):
     assert len(kev) == len(pipe.bounds)
     assert np.array_equal(recv.cpu().numpy().view(np.uint64), exp)
     assert [int(v) for v in dig.cpu().numpy().view(np.uint64)] == [o.digest(masked[c]) for c in plan.clients]
+
+
+def test_back_to_back_rounds_without_join(comm):
+    """bench.py's form: rounds run back to back with join=False, so a round's
+    reduces may still be reading the shared partial-sum buffer when the next
+    round's launches start; each chunk's launch waits for that chunk's
+    previous reduce, so every round's received sum equals the oracle's."""
+    from oracle import secagg as o
+    from sfl_amd.parallel_sum import PipelinedMaskedSum, plan_generators, plan_rank
+
+    C, W, n, chunks = 8, 2, 40_003, 5
+    names = [f"client{c}" for c in range(C)]
+    seeds = o.seeds_for(names)
+    plan = plan_rank(names, W, 0)
+    dev = torch.device("cuda", 0)
+    pipe = PipelinedMaskedSum(comm, dev, n, chunks)
+    seed_of = lambda u, v: seeds[names[u]][names[v]]  # noqa: E731
+    s = torch.empty(n, dtype=torch.int64, device=dev)
+    exps, recvs = [], []
+    for r in range(3):
+        rng = np.random.default_rng(100 + r)
+        xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
+        masked = o.secure_masked(xs, names, seeds=seeds, offset=r * n)
+        exp = np.zeros(n, dtype=np.uint64)
+        for c in plan.clients:
+            exp += masked[c]
+        exps.append(exp)
+        gens = [plan_generators(plan, seed_of, offset=r * n + lo) for lo, _ in pipe.bounds]
+        recvs.append(torch.empty(n, dtype=torch.int64, device=dev))
+        pipe.run([torch.from_numpy(xs[c]).to(dev) for c in plan.clients], [1.0] * len(plan.clients), gens,
+                 plan.n_cross, s, recvs[-1], join=False)
+    torch.cuda.synchronize()
+    for r in range(3):
+        assert np.array_equal(recvs[r].cpu().numpy().view(np.uint64), exps[r]), r
