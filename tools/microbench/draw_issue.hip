@@ -8,6 +8,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
 
 #include "../../sfl_amd/csrc/sa_clients_impl.h"
 
@@ -26,6 +30,13 @@ struct StreamLds {
   uint64_t inc_lo, inc_hi, cj_lo, cj_hi, smask, pad;
 };
 typedef __attribute__((address_space(3))) const StreamLds* lds_ptr;
+
+// a draw state as the product kernel holds it: limbs 0-1 as one VGPR pair
+// (written in place by the paired draws, sa_draw2.h), limbs 2 and 3
+struct MbState {
+  uint64_t p01;
+  uint32_t s2, s3;
+};
 
 // Same asm as pcg_draw_pair/one, but the stream constants are SGPR operands
 // (scalar-loaded) and the multiplier limbs VGPR operands (gfx9 constant bus: one
@@ -142,14 +153,13 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
   constexpr int P = Sched<L, X>::P;
   extern __shared__ char dyn[];
   if (dyn[0] == 123 && seed == 77) out[0] = 1;
-  uint32_t st[P][4];
+  MbState st[P];
   const uint32_t tid = threadIdx.x + blockIdx.x * blockDim.x;
 #pragma unroll
   for (int j = 0; j < P; j++) {
-    st[j][0] = tid * 0x9E3779B9u + j;
-    st[j][1] = seed ^ (j * 77u);
-    st[j][2] = tid + 13u * j;
-    st[j][3] = ~tid;
+    st[j].p01 = ((uint64_t)(seed ^ (j * 77u)) << 32) | (tid * 0x9E3779B9u + j);
+    st[j].s2 = tid + 13u * j;
+    st[j].s3 = ~tid;
   }
   const uint32_t mk[4] = {vreg(A0 + seed), vreg(A1), vreg(A2), vreg(A3)};
   uint64_t acc2[2][L];
@@ -180,23 +190,23 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
       const uint32_t ma = (uint32_t)nm[0], mb = (uint32_t)nm[1];
 #pragma unroll
       for (int k = 0; k < 2; k++) {
-        uint32_t* sa = st[G.qa];
+        MbState& sa = st[G.qa];
         uint64_t* ak = acc2[k];
         const uint32_t fma_ = ma ^ (G.fa ? 0xFFFFFFFFu : 0u), fmb_ = mb ^ (G.fb ? 0xFFFFFFFFu : 0u);
         if (G.qb < 0) {
+          uint32_t s0 = (uint32_t)sa.p01, s1 = (uint32_t)(sa.p01 >> 32);
           if (G.va >= 0 && G.va_add)
-            pcg_draw_pair_a(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua],
-                            ak[G.va]);
+            pcg_draw_pair_a(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua], ak[G.va]);
           else if (G.va >= 0)
-            pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua],
-                          ak[G.va]);
+            pcg_draw_pair(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua], ak[G.va]);
           else
-            pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua]);
+            pcg_draw_one(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua]);
+          sa.p01 = ((uint64_t)s1 << 32) | s0;
         } else {
-          uint32_t* sb = st[G.qb];
-#define DRAW2(fn)                                                                                              \
-  fn(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_,         \
-     zmin, ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb])
+          MbState& sb = st[G.qb];
+#define DRAW2(fn)                                                                                         \
+  fn<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_, zmin,     \
+        ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb], 0, 0, 0, 0)
           if (G.va >= 0 && G.va_add && G.vb_add)
             DRAW2(pcg_draw2_pair_aa);
           else if (G.va >= 0 && G.va_add)
@@ -207,11 +217,11 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
             DRAW2(pcg_draw2_pair_ss);
 #undef DRAW2
           else if (G.ua == G.ub)
-            pcg_draw2_one_same(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia,
-                               fma_, ib, fmb_, zmin, ak[G.ua]);
+            pcg_draw2_one_same<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib,
+                                  fmb_, zmin, ak[G.ua], 0);
           else
-            pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia,
-                          fma_, ib, fmb_, zmin, ak[G.ua], ak[G.ub]);
+            pcg_draw2_one<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_,
+                             zmin, ak[G.ua], ak[G.ub], 0, 0);
         }
         if (k == 0 && g + 1 < S.n) fetch(g + 1);
       }
@@ -223,7 +233,7 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
 #pragma unroll
     for (int c = 0; c < L; c++) acc += acc2[k][c];
 #pragma unroll
-  for (int j = 0; j < P; j++) acc ^= st[j][0] ^ st[j][3];
+  for (int j = 0; j < P; j++) acc ^= st[j].p01 ^ st[j].s3;
   out[tid] = acc;
 }
 
@@ -235,14 +245,13 @@ __global__ void __launch_bounds__(256, W) k_dualE(uint64_t* out, int iters, uint
   constexpr int P = Sched<L, X>::P;
   extern __shared__ char dyn[];
   if (dyn[0] == 123 && seed == 77) out[0] = 1;
-  uint32_t st[P][4];
+  MbState st[P];
   const uint32_t tid = threadIdx.x + blockIdx.x * blockDim.x;
 #pragma unroll
   for (int j = 0; j < P; j++) {
-    st[j][0] = tid * 0x9E3779B9u + j;
-    st[j][1] = seed ^ (j * 77u);
-    st[j][2] = tid + 13u * j;
-    st[j][3] = ~tid;
+    st[j].p01 = ((uint64_t)(seed ^ (j * 77u)) << 32) | (tid * 0x9E3779B9u + j);
+    st[j].s2 = tid + 13u * j;
+    st[j].s3 = ~tid;
   }
   const uint32_t mk[4] = {vreg(A0 + seed), vreg(A1), vreg(A2), vreg(A3)};  // E = 1: the tile-jump limbs only
   uint64_t acc2[E][L];
@@ -273,23 +282,23 @@ __global__ void __launch_bounds__(256, W) k_dualE(uint64_t* out, int iters, uint
       const uint32_t ma = (uint32_t)nm[0], mb = (uint32_t)nm[1];
 #pragma unroll
       for (int k = 0; k < E; k++) {
-        uint32_t* sa = st[G.qa];
+        MbState& sa = st[G.qa];
         uint64_t* ak = acc2[k];
         const uint32_t fma_ = ma ^ (G.fa ? 0xFFFFFFFFu : 0u), fmb_ = mb ^ (G.fb ? 0xFFFFFFFFu : 0u);
         if (G.qb < 0) {
+          uint32_t s0 = (uint32_t)sa.p01, s1 = (uint32_t)(sa.p01 >> 32);
           if (G.va >= 0 && G.va_add)
-            pcg_draw_pair_a(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua],
-                            ak[G.va]);
+            pcg_draw_pair_a(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua], ak[G.va]);
           else if (G.va >= 0)
-            pcg_draw_pair(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua],
-                          ak[G.va]);
+            pcg_draw_pair(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua], ak[G.va]);
           else
-            pcg_draw_one(sa[0], sa[1], sa[2], sa[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua]);
+            pcg_draw_one(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua]);
+          sa.p01 = ((uint64_t)s1 << 32) | s0;
         } else {
-          uint32_t* sb = st[G.qb];
-#define DRAW2(fn)                                                                                              \
-  fn(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_,         \
-     zmin, ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb])
+          MbState& sb = st[G.qb];
+#define DRAW2(fn)                                                                                         \
+  fn<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_, zmin,     \
+        ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb], 0, 0, 0, 0)
           if (G.va >= 0 && G.va_add && G.vb_add)
             DRAW2(pcg_draw2_pair_aa);
           else if (G.va >= 0 && G.va_add)
@@ -300,11 +309,11 @@ __global__ void __launch_bounds__(256, W) k_dualE(uint64_t* out, int iters, uint
             DRAW2(pcg_draw2_pair_ss);
 #undef DRAW2
           else if (G.ua == G.ub)
-            pcg_draw2_one_same(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia,
-                               fma_, ib, fmb_, zmin, ak[G.ua]);
+            pcg_draw2_one_same<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib,
+                                  fmb_, zmin, ak[G.ua], 0);
           else
-            pcg_draw2_one(sa[0], sa[1], sa[2], sa[3], sb[0], sb[1], sb[2], sb[3], mk[0], mk[1], mk[2], mk[3], ia,
-                          fma_, ib, fmb_, zmin, ak[G.ua], ak[G.ub]);
+            pcg_draw2_one<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_,
+                             zmin, ak[G.ua], ak[G.ub], 0, 0);
         }
         if (k == 0 && g + 1 < S.n) fetch(g + 1);
       }
@@ -316,7 +325,7 @@ __global__ void __launch_bounds__(256, W) k_dualE(uint64_t* out, int iters, uint
 #pragma unroll
     for (int c = 0; c < L; c++) acc += acc2[k][c];
 #pragma unroll
-  for (int j = 0; j < P; j++) acc ^= st[j][0] ^ st[j][3];
+  for (int j = 0; j < P; j++) acc ^= st[j].p01 ^ st[j].s3;
   out[tid] = acc;
 }
 
@@ -451,7 +460,14 @@ __global__ void __launch_bounds__(256) k_draws(uint64_t* out, int iters, uint32_
   out[tid] = acc;
 }
 
-int main() {
+// usage: draw_issue                     all cases, every occupancy
+//        draw_issue CASE WAVES         one case at one occupancy: the median
+//                                      of 15 launches after 40 warm-up ones, as
+//                                      one JSON line (bench.py measures the
+//                                      same-box draw-loop ceiling)
+int main(int argc, char** argv) {
+  const char* only = argc > 1 ? argv[1] : nullptr;
+  const int only_w = argc > 2 ? atoi(argv[2]) : 0;
   int ncu = 0;
   CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
   uint64_t* d_out;
@@ -474,7 +490,9 @@ int main() {
     CHECK(hipMemcpy(gconst, h, sizeof(h), hipMemcpyHostToDevice));
   }
   auto run = [&](auto kern, int P, const char* name, int iters, auto... extra) -> int {
+    if (only && strcmp(only, name) != 0) return 0;
     for (int w : {1, 2, 3, 4, 5, 6, 8}) {
+      if (only_w && w != only_w) continue;
       // w blocks of 4 waves per CU -> w waves per SIMD (if registers allow)
       const size_t dyn = (160 * 1024) / w - 4096;
       int nb = 0;
@@ -485,14 +503,27 @@ int main() {
       }
       const int blocks = ncu * w;
       float ms = 0;
-      for (int rep = 0; rep < 2; rep++) {
+      // one case: 40 untimed launches first (clocks ramp up from idle over
+      // the first ~10 ms), then the median of 15
+      const int reps = only ? 15 : 2;
+      float t[15];
+      for (int rep = 0; only && rep < 40; rep++)
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), dyn, 0, d_out, iters, 5u, extra...);
+      for (int rep = 0; rep < reps; rep++) {
         CHECK(hipEventRecord(e0));
         hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), dyn, 0, d_out, iters, 5u, extra...);
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
-        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        CHECK(hipEventElapsedTime(&t[rep], e0, e1));
       }
+      if (only) std::sort(t, t + reps);
+      ms = only ? t[reps / 2] : t[reps - 1];  // one case: the median; the sweep: the second launch
       const double draws = (double)blocks * 256 * iters * P;
+      if (only) {
+        printf("{\"case\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.4f, \"draws_per_s\": %.6e}\n", name, w, ms,
+               draws / (ms * 1e-3));
+        continue;
+      }
       printf("%-22s waves/SIMD=%d  %8.3f ms  %7.1f G draws/s\n", name, w, ms, draws / (ms * 1e-3) / 1e9);
       fflush(stdout);
     }
