@@ -288,7 +288,9 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
 //   the four limb-3 products summed by one v_mul_lo_u32 and three
 //   v_mad_u64_u32 (only the low word is kept), joined by carry adds whose
 //   carry-ins are the mads' own carry-outs -- 9 mads + 1 mul_lo + 4 adds +
-//   1 mov, no register shuffling.  Then t = rotr(hi^lo^m,
+//   1 mov (the paired draws of sa_draw2.h, which do nearly all the work,
+//   keep limbs 0-1 in one VGPR pair written in place and need no mov).
+//   Then t = rotr(hi^lo^m,
 //   hi>>58) in 32-bit halves (v_bitop3 + v_alignbit + swap), the raw==0 test
 //   (hi == lo <=> xl == xh == m) folded into a running minimum, and the
 //   accumulation (below).
@@ -297,7 +299,8 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
 // carry-out; k2: kO, c2, then the acc_v borrow; k3: discarded carry-outs, c1).
 // Every VALU-written SGPR (carries, VCC) is read >= 2 instructions later
 // (gfx950 VALU-SGPR-write -> VALU-read hazard).  v0-v9 are fixed scratch (low
-// registers, so the kernel's VGPR budget is not raised).
+// registers, so the kernel's VGPR budget is not raised).  Single draws only
+// serve schedules with an odd leftover stream.
 #define SA_PCG_DRAW_ASM                                                                  \
   "v_mad_u64_u32 v[0:1], %[k1], %[s0], %[a0], %[c0]\n\t"    /* E0 = s0a0 + c0 < 2^64 */  \
   "v_mad_u64_u32 v[2:3], %[k3], %[s0], %[a1], %[c1]\n\t"    /* O1 = s0a1 + c1 < 2^64 */  \
