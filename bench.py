@@ -298,6 +298,10 @@ def workload(args, world: int) -> str:
     X = C - L
     pairs = L * (L - 1) // 2
     if world == 1:
+        if L > 8 or pairs + L * X > 32:  # beyond sa_fused_clients' shapes: client by client
+            return (f"{C} clients x {N} fp32 grad elems on 1 GPU, fxp {args.fxp_bits}, ring 2^64: per-client "
+                    f"sa_mask passes of <= 16 streams accumulating into the sum ({C - 1} streams per client, "
+                    f"no pair sharing)")
         return (f"{C} clients x {N} fp32 grad elems on 1 GPU, fxp {args.fxp_bits}, ring 2^64: one fused launch "
                 f"k_clients<float,float,{L},{X}> ({pairs} pair streams)")
     return (f"{C} clients x {N} fp32 grad elems over {world} GPUs, fxp {args.fxp_bits}, ring 2^64; per rank: "
@@ -439,6 +443,10 @@ def main():
     launches = len(pipe.bounds)
     achieved = bytes_alg / (kern_ms / 1e3) / 1e9
     kname = f"k_clients<float, float, {Lc}, {plan.n_cross}>"  # the launch's kernel
+    n_streams = len(plan.pairs) + len(plan.cross)
+    fused = Lc <= 8 and n_streams <= 32  # sa_fused_clients' limits (kMaxLocal, kMaxStreams)
+    if not fused:  # sa_fused_clients masks client by client (sa_mask passes of <= 16 streams)
+        kname = f"k_clients<float, float, 1, X<=16> per client and pass (fallback for {Lc} local clients)"
     pmc = pmc_traffic(f"void sa::{kname}", N // launches)
     draws_s = draws / (kern_ms / 1e3)
     peak_draws = ceiling["draws_per_s"] if ceiling else PCG_PAIR_DRAWS_2WAVE
@@ -464,7 +472,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": pmc["bytes"] if pmc else None, "traffic_detail": pmc,
-                     "kernel": f"{kname} (sa_fused_clients)", "kernel_ms_per_step": kern_ms,
+                     "kernel": f"{kname} (sa_fused_clients)" if fused else kname, "kernel_ms_per_step": kern_ms,
                      "launches_per_step": launches,
                      "algorithmic_bytes_per_launch": bytes_alg / launches,
                      "kernel_ms_per_launch": kern_ms / launches,
