@@ -200,6 +200,52 @@ def test_fused_clients_bit_exact(C, n):
     assert np.array_equal(_u64(s2), s_exp + s_exp)
 
 
+@pytest.mark.parametrize("fxp", [0, 1, 7, 24, 31, 32, 40, 52, 62])
+def test_fxp_bits_range(fxp):
+    """Every fixed-point width the C-ABI accepts (0..62), not just the
+    reference default 18: fused launch (pair sharing, digests, wire images,
+    sum-only finish), per-client masking of f32 / f64 / int64 payloads with
+    scalar weights, and the decode -- bit-exact vs the oracle.  Wide fxp
+    sends every tile down the exact int64 path (|x*w*2^fxp| >= 2^31) and, at
+    52+, past 2^63 (INT64_MIN, numpy's x86 astype); fxp 0 truncates most
+    gradients to 0."""
+    K = _K()
+    C, n, off = 5, 4099, 7
+    names, xs, seeds, pg, ps = _fused_setup(C, n, off, seed=fxp)
+    xs = [x * np.float32(1 + 30 * c) for c, x in enumerate(xs)]  # magnitudes 1e-2 .. 1.2
+    ws = [1.0, 0.5, 3.0, 0.1, 2.0]
+    masked = o.secure_masked(xs, names, weights=ws, fxp_bits=fxp, seeds=seeds, offset=off)
+    s_exp = o.server_sum(masked)
+    s = torch.empty(n, dtype=torch.int64, device=DEV)
+    dig = torch.zeros(C, dtype=torch.int64, device=DEV)
+    mo = [torch.empty(n, dtype=torch.int64, device=DEV) for _ in range(C)]
+    xt = [torch.from_numpy(x).to(DEV) for x in xs]
+    K.fused_clients(xt, ws, pg, ps, [], 0, s, fxp_bits=fxp, digests=dig, masked_outs=mo)
+    s2 = torch.empty(n, dtype=torch.int64, device=DEV)
+    K.fused_clients(xt, ws, pg, ps, [], 0, s2, fxp_bits=fxp)
+    dec = K.decode(s, torch.empty(n, dtype=torch.float64, device=DEV), fxp_bits=fxp, divisor=sum(ws))
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(s), s_exp)
+    assert np.array_equal(_u64(s2), s_exp)
+    for c in range(C):
+        assert np.array_equal(_u64(mo[c]), masked[c]), c
+    assert [int(v) for v in _u64(dig)] == [o.digest(m) for m in masked]
+    assert np.array_equal(dec.cpu().numpy(), o.decode(s_exp, fxp, sum(ws)))
+    # per-client masking of the other payload types at this width
+    rng = np.random.default_rng(fxp)
+    seeds1 = [o.pair_seed(2, j) for j in (0, 1, 3)]
+    signs1 = [1, -1, 1]
+    for x, w, ct in (((rng.standard_normal(n) * 50).astype(np.float64), 0.75, torch.float64),
+                     (rng.integers(-(1 << 20), 1 << 20, n), 3, torch.int64),
+                     ((rng.standard_normal(n) * 4).astype(np.float32), 0.3, torch.float32)):
+        exp = _oracle_masked(o.quantize(x, w, fxp), seeds1, signs1, 99)
+        out = torch.empty(n, dtype=torch.int64, device=DEV)
+        K.mask(torch.from_numpy(x).to(DEV), out, _streams(seeds1, signs1, 99), weight=w, compute_dtype=ct,
+               fxp_bits=fxp)
+        torch.cuda.synchronize()
+        assert np.array_equal(_u64(out), exp), ct
+
+
 @pytest.mark.parametrize("C", [4, 8])
 def test_fused_mixed_fast_and_exact_tiles(C):
     """A few scattered values that leave the int32 conversion (|x*w*2^fxp| >=
