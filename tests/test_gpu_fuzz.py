@@ -115,3 +115,69 @@ def test_plugin_random_cases_match_oracle(seed):
                     mv = agg.last_masked[li][c].cpu().numpy().view(np.uint64)
                     assert np.array_equal(mv, masked[c].reshape(-1)), (seed, rnd, li, c)
             offset += int(np.prod(sh))
+
+
+N_KERNEL_CASES = 60
+
+
+@pytest.mark.parametrize("seed", range(N_KERNEL_CASES))
+def test_fused_launch_random_shapes_match_oracle(seed):
+    """``sa_fused_clients`` at random per-rank shapes: L local clients of T
+    (L = 1..8, the other T - L as cross streams of every local client, fused
+    or the per-client fallback), random n, stream offset up to 2^60, python
+    float / int weights, gradients at random scales with a few values that
+    force the exact int64 quantize path; digests, wire images and accumulate
+    on or off.  The partial sum is the sum of the local clients' masked
+    vectors of the oracle, bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd import _lib as L
+    from sfl_amd import kernels as K
+
+    rng = np.random.default_rng(5000 + seed)
+    T = int(rng.integers(2, 13))
+    Lc = int(rng.integers(1, min(8, T) + 1))
+    n = int(rng.choice([1, 2, 63, 64, 65, 1000, 4097, int(rng.integers(1, 200_000))]))
+    offset = int(rng.integers(0, 1 << 60))
+    names = [f"q{int(v):02d}" for v in rng.permutation(40)[:T]]
+    seeds = o.seeds_for(names)
+    scale = float(10.0 ** rng.integers(-4, 3))
+    xs = [(rng.standard_normal(n) * scale).astype(np.float32) for _ in names]
+    if n > 100 and rng.random() < 0.4:
+        idx = rng.choice(n, 5, replace=False)
+        xs[0][idx] = np.float32([3e9, -np.inf, np.nan, 1e30, -2.5e9])
+    ws = ([float(v) for v in rng.random(T) * 3 + 0.05] if rng.random() < 0.5
+          else [int(v) for v in rng.integers(1, 60, T)])
+    masked = o.secure_masked(xs, names, weights=ws, seeds=seeds, offset=offset)
+    local = list(range(Lc))
+    remote = list(range(Lc, T))
+    pg, ps = [], []
+    for u in local:
+        for v in local[u + 1:]:
+            pg.append(L.pcg64_advance(L.pcg64_from_seed(seeds[names[u]][names[v]]), offset))
+            ps.append(1 if names[v] > names[u] else -1)
+    cross = []
+    for u in local:
+        for v in remote:
+            cross.append((L.pcg64_advance(L.pcg64_from_seed(seeds[names[u]][names[v]]), offset),
+                          1 if names[v] > names[u] else -1, v))
+    want_dig, want_mo, acc = (bool(rng.random() < 0.5) for _ in range(3))
+    base = rng.integers(0, 2**63, n).astype(np.uint64) if acc else np.zeros(n, np.uint64)
+    s = torch.from_numpy(base.view(np.int64).copy()).to("cuda:0")
+    dig = torch.zeros(Lc, dtype=torch.int64, device="cuda:0") if want_dig else None
+    mo = [torch.empty(n, dtype=torch.int64, device="cuda:0") for _ in local] if want_mo else None
+    flags = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    K.fused_clients([torch.from_numpy(xs[u]).to("cuda:0") for u in local], [ws[u] for u in local], pg, ps,
+                    cross, len(remote), s, accumulate=acc, digests=dig, flags=flags, masked_outs=mo)
+    torch.cuda.synchronize()
+    exp = base.copy()
+    for u in local:
+        exp = exp + masked[u]
+    ctx = (seed, T, Lc, n, want_dig, want_mo, acc)
+    assert np.array_equal(K.as_u64(s), exp), ctx
+    if want_mo:
+        for u in local:
+            assert np.array_equal(K.as_u64(mo[u]), masked[u]), ctx + (u,)
+    if want_dig:
+        assert [int(v) for v in K.as_u64(dig)] == [o.digest(masked[u]) for u in local], ctx
+    assert int(flags.item()) == 0
