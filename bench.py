@@ -405,6 +405,7 @@ def main():
     digests = torch.zeros(Lc, dtype=torch.int64, device=dev) if args.digests else None
     flags = torch.zeros(1, dtype=torch.int32, device=dev)
     kev = []  # (start, end) events around every masking launch of the timed steps (compute stream)
+    xev = []  # (start, end) events around every reduce of the timed steps (comm stream)
 
     def step(i, timed_idx=None):
         # join=False: a round's exchange tail overlaps the next round's first
@@ -412,7 +413,7 @@ def main():
         # reduce); the timed region ends with a device synchronise
         pipe.run(xs, [1.0] * Lc, gens[i], plan.n_cross, sum_buf, None, fxp_bits=args.fxp_bits,
                  digests=digests, flags=flags, kernel_events=kev if timed_idx is not None else None,
-                 join=False)
+                 exchange_events=xev if timed_idx is not None else None, join=False)
 
     for i in range(args.warmup):
         step(i)
@@ -429,10 +430,11 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in kev) / args.steps  # masking kernel time per step
+    xchg_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps  # reduce time per step (comm stream)
     if multi:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms, xchg_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, kern_ms, xchg_ms = float(t[0]), float(t[1]), float(t[2])
     if int(flags.item()):
         print("warning: PRG zero-draw flag raised", file=sys.stderr)
 
@@ -487,6 +489,21 @@ def main():
                               "frac": draws_s / peak_draws,
                               "frac_vs_one_sided_8wave": draws_s / PCG_ONE_DRAWS_8WAVE}},
     }
+    if multi:
+        # the exchange step: every rank's uint64 partial sum
+        # reduced in place to rank 0, one ncclReduce per pipeline chunk on a
+        # comm stream beside the masking launches; time from each chunk's
+        # launch end on this rank to its reduce end, summed per step, max over
+        # ranks.  nccl-tests' convention: reduce bus bandwidth = algbw.
+        xb = 8 * N
+        out["exchange"] = {"collective": "ncclReduce(uint64, sum) in place to rank 0",
+                           "chunks": launches, "bytes_per_rank_per_step": xb,
+                           "ms_per_step": xchg_ms,
+                           "algbw_GBps": xb / (xchg_ms / 1e3) / 1e9 if xchg_ms > 0 and world > 1 else None,
+                           "overlap": "chunk j's reduce runs while chunk j+1 is masked; "
+                                      "ms_per_step ~ max(kernel, exchange) + one chunk of fill/drain"}
+        if world == 1:
+            out["exchange"]["note"] = "world 1 (--dist rehearsal): the in-place reduce moves no data"
     if args.extra and world == 1:
         out["extra"] = extra_measurements(args, xs, plan, gens, K, torch, dev)
     if rank == 0:

@@ -154,10 +154,12 @@ class PipelinedMaskedSum:
 
     def run(self, xs, weights, chunk_gens, n_cross: int, sum_buf, recv=None, *, root: int = 0,
             fxp_bits: int = 18, digests=None, flags=None, kernel_events: list | None = None,
-            join: bool = True):
+            exchange_events: list | None = None, join: bool = True):
         """``kernel_events``: if given, a timing-event pair recorded around
         each chunk's masking launch is appended (kernel time without the
-        exchange).  ``join=False`` leaves the last reduces running on the
+        exchange); ``exchange_events`` likewise around each chunk's reduce on
+        the comm stream (from the moment that chunk's launch has finished
+        here, so the wait for slower peers counts).  ``join=False`` leaves the last reduces running on the
         comm stream (the caller synchronises the device before reading the
         result); a following run() still orders each chunk's launch after
         that chunk's previous reduce, so back-to-back rounds overlap one
@@ -185,7 +187,13 @@ class PipelinedMaskedSum:
                 self.events[j].record(compute)
                 self.comm_stream.wait_event(self.events[j])
                 with torch.cuda.stream(self.comm_stream):
+                    if exchange_events is not None:
+                        exchange_events.append((torch.cuda.Event(enable_timing=True),
+                                                torch.cuda.Event(enable_timing=True)))
+                        exchange_events[-1][0].record(self.comm_stream)
                     self.comm.reduce_u64(sum_buf[lo:hi], recv[lo:hi] if recv is not None else None, root=root)
+                    if exchange_events is not None:
+                        exchange_events[-1][1].record(self.comm_stream)
                     self.reduced[j].record(self.comm_stream)
                 self._pending[j] = True
         if self.comm is not None and join:
