@@ -182,6 +182,8 @@ class LoopbackServer:
                     errors.append(e)
                     cond.notify_all()
 
+        out = np.empty(n, dtype=np.float64)  # the caller's copy, filled chunk by chunk below
+        res_np = res_host.numpy()
         rx = [threading.Thread(target=receive, args=(i,), daemon=True) for i in range(C)]
         tx = [threading.Thread(target=send, args=(i,), daemon=True) for i in range(C)]
         for t in rx + tx:
@@ -213,6 +215,9 @@ class LoopbackServer:
                     e.record(agg)
                 e.synchronize()
                 ready[j].set()
+                # copy the chunk out of the pinned buffer while it is broadcast
+                # and later chunks arrive (no 8n-byte copy after the round)
+                out[lo:hi] = res_np[lo:hi]
             stamps["recv_done"] = time.perf_counter()
             for t in rx + tx:
                 t.join(timeout)
@@ -229,7 +234,6 @@ class LoopbackServer:
             for r in ready:  # release senders (on an error they stop before sending)
                 r.set()
         t_end = time.perf_counter()
-        out = res_host.numpy()[:n].copy()
         if keep_masked:
             for st in streams:
                 st.synchronize()
@@ -369,11 +373,23 @@ class LoopbackClient:
         t2 = time.perf_counter()
         return {"h2d_mask_s": t1 - t0, "d2h_send_s": t2 - t1}
 
-    def result(self, n: int | None = None) -> np.ndarray:
+    def result(self, n: int | None = None, into: np.ndarray | None = None) -> np.ndarray:
         """The server's float64 aggregate (``n`` elements when given: a larger
-        announced frame is refused before anything is allocated)."""
-        h, mv = W.recv_frame(self.sock, expect_kind=W.RESULT, max_bytes=None if n is None else 8 * int(n))
-        return W.as_array(h, mv).copy()
+        announced frame is refused before anything is allocated).  The
+        payload is received straight into the returned array -- ``into``
+        (float64, reused across rounds by a caller that consumes each result
+        before the next) or a fresh one -- with no intermediate copy."""
+        if into is None and n is not None:
+            into = np.empty(int(n), dtype=np.float64)
+        if into is None:
+            h, mv = W.recv_frame(self.sock, expect_kind=W.RESULT)
+            return W.as_array(h, mv).copy()
+        if into.dtype != np.float64 or not into.flags.c_contiguous:
+            raise ValueError("result buffer must be a contiguous float64 array")
+        h, _ = W.recv_frame(self.sock, into, expect_kind=W.RESULT)
+        if h.dtype != W.F64 or (n is not None and h.count != int(n)):
+            raise W.WireError(f"RESULT frame of {h.count} elements (dtype {h.dtype}), want {n} float64")
+        return into[:h.count]
 
     def close(self):
         try:
@@ -403,11 +419,15 @@ def client_process(parties: list, port: int, n: int, rounds: int, gpu: int, fxp_
             cl = LoopbackClient(party, index, port, gpu=gpu, fxp_bits=fxp_bits, seeds=seeds)
             cl.handshake()
             stats = []
+            res = np.empty(n, dtype=np.float64)  # one receive buffer for every round
             for r in range(rounds):
                 st = cl.submit(xs[r], r, weight)
-                res = cl.result(n)
-                st["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))
+                if r:  # the previous result's checksum, after this round's submit
+                    stats[-1]["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))
+                cl.result(n, into=res)
                 stats.append(st)
+            if stats:
+                stats[-1]["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))
             W.recv_header(cl.sock, expect_kind=W.BYE)
             cl.close()
             out_q.put((index, "ok", stats))
@@ -446,7 +466,9 @@ def run_loopback(names: list[str], n: int, rounds: int = 1, *, seeds: dict | Non
     try:
         srv.accept(timeout=timeout)
         for r in range(rounds):
+            t_start = time.perf_counter()
             out, t = srv.round(n, r, average=average, keep_masked=keep_masked, verify_digest=verify_digest)
+            t["t_start"] = t_start  # successive starts give the steady-state period (copy-out included)
             results.append(out)
             timings.append(t)
             if keep_masked:

@@ -21,7 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--elems", type=int, default=100_000_000)
-    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--parties-per-process", type=int, default=1,
                     help="client parties hosted per OS process (config 5: 32 clients as 8 x 4)")
     args = ap.parse_args()
@@ -36,12 +36,21 @@ def main():
                                           parties_per_process=args.parties_per_process)
     steady = timings[1:] if len(timings) > 1 else timings
     rs = float(np.median([t["round_s"] for t in steady]))
+    # the rate: wall time from the start of round 1 (round 0 warms up) to the
+    # end of the last round, per round -- it counts the parties' turnaround
+    # between rounds as well as the server's rounds; one round: its time
+    if len(timings) > 1:
+        span = timings[-1]["t_start"] + timings[-1]["round_s"] - timings[1]["t_start"]
+        period = span / (len(timings) - 1)
+    else:
+        period = rs
     cl = [s for per in stats.values() for s in per[1:] or per]
     out = {
         "metric": "host-resident grad elems/s (loopback sockets, H2D/D2H inclusive)",
         "clients": args.clients, "elems_per_client": args.elems, "rounds": args.rounds,
-        "round_s_median": rs, "grad_elems_per_s": args.clients * args.elems / rs,
-        "server": {k: float(np.median([t[k] for t in steady])) for k in steady[0]},
+        "period_s": period, "grad_elems_per_s": args.clients * args.elems / period,
+        "round_s_median": rs,
+        "server": {k: float(np.median([t[k] for t in steady])) for k in steady[0] if k != "t_start"},
         "client_h2d_mask_s_median": float(np.median([s["h2d_mask_s"] for s in cl])),
         "client_d2h_send_s_median": float(np.median([s["d2h_send_s"] for s in cl])),
         "parties_per_process": args.parties_per_process,
