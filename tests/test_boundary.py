@@ -77,6 +77,38 @@ def test_errors_cross_the_abi_as_codes():
     assert lib.sa_pcg64_from_seed(arr, -1, None) == L.SA_ERR_ARG
 
 
+def test_every_entry_point_validates_before_touching_the_gpu():
+    """Each export refuses bad arguments with SA_ERR_ARG and a message,
+    before any HIP call (so this runs on a machine without a GPU); the
+    reference's equivalent is a Python assert with a message
+    (sparse_plain_aggregator.py:85).  n == 0 with valid sizes is a no-op."""
+    from sfl_amd import _lib as L
+
+    lib = L.lib()
+    calls = {
+        "sa_fused_clients": lambda: lib.sa_fused_clients(None, 0, 0, 10, 18, None, None, None, 0, None, 0, None,
+                                                         None, None),
+        "sa_decode": lambda: lib.sa_decode(None, 10, 63, 1.0, None, None, None),
+        "sa_sum_f64": lambda: lib.sa_sum_f64(None, 0, 10, None, None),
+        "sa_pcg64_find_zero": lambda: lib.sa_pcg64_find_zero(None, 1, 10, None, None),
+        "sa_stream_shift": lambda: lib.sa_stream_shift(None, 10, None, 1, 0, 1, None),
+        "sa_xor_u64": lambda: lib.sa_xor_u64(None, 10, None, None),
+        "sa_sumsq_f32": lambda: lib.sa_sumsq_f32(None, 10, None, None, 0, None),
+        "sa_dp_perturb_f32": lambda: lib.sa_dp_perturb_f32(None, 10, None, None, None),
+        "sa_mask_dp": lambda: lib.sa_mask_dp(None, 10, 1.0, 18, None, 0, None, None, None, None, None, None),
+        "sa_mask": lambda: lib.sa_mask(None, 0, 0, 10, 1.0, None, 63, None, 0, None, None, None, None, None),
+        "sa_comm_unique_id": lambda: lib.sa_comm_unique_id(None, 0),
+        "sa_comm_init": lambda: lib.sa_comm_init(None, None, 0, 0, 0),
+        "sa_comm_reduce_u64": lambda: lib.sa_comm_reduce_u64(None, None, None, 10, 0, None),
+        "sa_comm_allreduce_u64": lambda: lib.sa_comm_allreduce_u64(None, None, None, 10, None),
+        "sa_pcg64_raw_host": lambda: lib.sa_pcg64_raw_host(None, None, 5),
+    }
+    for name, call in calls.items():
+        assert call() == L.SA_ERR_ARG, name
+        assert lib.sa_last_error(), name
+    assert lib.sa_mask(None, 0, 0, 0, 1.0, None, 18, None, 0, None, None, None, None, None) == L.SA_OK
+
+
 def test_kernels_refuse_host_tensors():
     import torch
 
