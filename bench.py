@@ -14,7 +14,9 @@ N>1: one process per GPU, clients sharded in contiguous blocks (8/N per
 GPU, config 3 at N=8); each rank runs the fused masking over its clients
 (internal pairs + cross streams), pipelined in chunks against ncclReduce of
 the uint64 partial sums to rank 0 (the server) over xGMI.  Total work is
-fixed as N grows: "scaling": "strong".  `python bench.py --gpus N` starts
+fixed as N grows: "scaling": "strong".  `--exchange sharded` replaces the
+reduce with the sharded server of SURVEY.md §8(e) (ncclReduceScatter, every
+rank decodes its shard; `--gather` also gathers the float64 shards to rank 0).  `python bench.py --gpus N` starts
 its N rank processes itself (torch.distributed.run as a child process,
 before this process touches the GPU); under an outer torchrun (WORLD_SIZE
 set) it runs as one rank.
@@ -306,7 +308,10 @@ def workload(args, world: int) -> str:
                 f"k_clients<float,float,{L},{X}> ({pairs} pair streams)")
     return (f"{C} clients x {N} fp32 grad elems over {world} GPUs, fxp {args.fxp_bits}, ring 2^64; per rank: "
             f"{L} local client(s), {pairs} internal pair + {L * X} cross streams "
-            f"(k_clients<float,float,{L},{X}>), pipelined ncclReduce(uint64) of the partial sum to rank 0")
+            f"(k_clients<float,float,{L},{X}>), pipelined " +
+            ("ncclReduceScatter(uint64) of the partial sum, each rank decoding its shard (sharded server)"
+             + (" and gathering the float64 shards to rank 0" if args.gather else "")
+             if args.exchange == "sharded" else "ncclReduce(uint64) of the partial sum to rank 0"))
 
 
 def main():
@@ -328,6 +333,11 @@ def main():
                          "(rehearsal of the N>1 path on one GPU)")
     ap.add_argument("--chunks", type=int, default=None,
                     help="masking/reduce pipeline depth (default 8 for N>1, 1 at N=1)")
+    ap.add_argument("--exchange", choices=("reduce", "sharded"), default="reduce",
+                    help="N>1 exchange: ncclReduce of the partial sums to rank 0 (default), or the sharded "
+                         "server of SURVEY.md 8(e): ncclReduceScatter, every rank decodes its shard")
+    ap.add_argument("--gather", action="store_true",
+                    help="with --exchange sharded: also gather the decoded float64 shards to rank 0")
     ap.add_argument("--digests", action="store_true",
                     help="also fold every client's masked values into an XOR digest (test checksum)")
     ap.add_argument("--dry-run", action="store_true",
@@ -391,13 +401,17 @@ def main():
         xs.append(torch.randn(N, generator=g, device=dev, dtype=torch.float32) * 1e-2)
     total_steps = args.warmup + args.steps
     chunks = args.chunks if args.chunks is not None else (8 if world > 1 else 1)
-    pipe = PipelinedMaskedSum(comm, dev, N, chunks)
+    sharded = multi and args.exchange == "sharded"
+    pipe = PipelinedMaskedSum(comm, dev, N, chunks, exchange="sharded" if sharded else "reduce")
     # every step is a new round: streams start i*N draws in, chunk j at +lo_j
     gens = [[plan_generators(plan, pair_seed, offset=i * N + lo) for lo, _ in pipe.bounds]
             for i in range(total_steps)]
     # the partial sum is reduced IN PLACE (rank 0, the server, receives the
     # masked sum in sum_buf; at N=1 the reduce is a no-op)
-    sum_buf = torch.empty(N, dtype=torch.int64, device=dev)
+    # (sharded server: padded to whole shards, the padding zeroed once; every
+    # rank decodes its shard of each chunk into dec on the comm stream)
+    sum_buf = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
+    dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev) if sharded else None
     # no per-client digests: an XOR checksum the tests use to pin every
     # client's masked vector, not part of the reference's arithmetic; the
     # kernel forms each client's masked value and adds it to the sum either
@@ -413,7 +427,8 @@ def main():
         # reduce); the timed region ends with a device synchronise
         pipe.run(xs, [1.0] * Lc, gens[i], plan.n_cross, sum_buf, None, fxp_bits=args.fxp_bits,
                  digests=digests, flags=flags, kernel_events=kev if timed_idx is not None else None,
-                 exchange_events=xev if timed_idx is not None else None, join=False)
+                 exchange_events=xev if timed_idx is not None else None, join=False,
+                 dec=dec, gather=args.gather)
 
     for i in range(args.warmup):
         step(i)
@@ -496,7 +511,12 @@ def main():
         # launch end on this rank to its reduce end, summed per step, max over
         # ranks.  nccl-tests' convention: reduce bus bandwidth = algbw.
         xb = 8 * N
-        out["exchange"] = {"collective": "ncclReduce(uint64, sum) in place to rank 0",
+        coll = "ncclReduce(uint64, sum) in place to rank 0"
+        if sharded:
+            coll = ("sharded server: ncclReduceScatter(uint64, sum) in place, every rank decodes its shard "
+                    "(k_decode on the comm stream)" + (", float64 shards gathered to rank 0 (ncclSend/Recv)"
+                                                       if args.gather else ""))
+        out["exchange"] = {"collective": coll,
                            "chunks": launches, "bytes_per_rank_per_step": xb,
                            "ms_per_step": xchg_ms,
                            "algbw_GBps": xb / (xchg_ms / 1e3) / 1e9 if xchg_ms > 0 and world > 1 else None,

@@ -251,6 +251,18 @@ int sa_comm_reduce_u64(void* comm, const uint64_t* send, uint64_t* recv, uint64_
                        void* stream);
 int sa_comm_allreduce_u64(void* comm, const uint64_t* send, uint64_t* recv, uint64_t n,
                           void* stream);
+/* The sharded server (SURVEY.md §8(e) "ReduceScatter, then decode the shards
+ * in parallel, then Gather float64"): ncclReduceScatter(ncclUint64, ncclSum),
+ * rank r's recv (count elements) = sum over ranks of send[r*count, (r+1)*count);
+ * in place when recv == send + r*count.  Same exchange as sa_comm_reduce_u64
+ * (the server's np.sum, sparse_plain_aggregator.py:88-94), the server split
+ * over the ranks. */
+int sa_comm_reduce_scatter_u64(void* comm, const uint64_t* send, uint64_t* recv, uint64_t count,
+                               void* stream);
+/* The decoded float64 shards to the server: on root, recv[r*count, (r+1)*count)
+ * = rank r's send (grouped ncclSend/ncclRecv); recv may be NULL off root. */
+int sa_comm_gather_f64(void* comm, const double* send, double* recv, uint64_t count, int root,
+                       void* stream);
 int sa_comm_destroy(void* comm);
 
 #ifdef __cplusplus

@@ -73,6 +73,60 @@ extern "C" int sa_comm_allreduce_u64(void* comm, const uint64_t* send, uint64_t*
   return SA_OK;
 }
 
+// The sharded server (ReduceScatter, decode the shards in
+// parallel, Gather float64): rank r receives the masked sum of elements
+// [r*count, (r+1)*count) of send.  In place when recv == send + r*count.
+extern "C" int sa_comm_reduce_scatter_u64(void* comm, const uint64_t* send, uint64_t* recv,
+                                          uint64_t count, void* stream) {
+  if (!comm || !send || !recv) {
+    sa_set_error("sa_comm_reduce_scatter_u64: bad arguments");
+    return SA_ERR_ARG;
+  }
+  SA_NCCL_CHECK(ncclReduceScatter(send, recv, (size_t)count, ncclUint64, ncclSum, (ncclComm_t)comm,
+                                  (hipStream_t)stream));
+  return SA_OK;
+}
+
+// float64 shards to the server: root's recv[r*count, (r+1)*count) = rank r's
+// send (one grouped ncclSend/ncclRecv round; root's own shard is a device copy
+// unless it is already in place).  recv is only read on root (may be NULL
+// elsewhere).
+extern "C" int sa_comm_gather_f64(void* comm, const double* send, double* recv, uint64_t count,
+                                  int root, void* stream) {
+  if (!comm || !send) {
+    sa_set_error("sa_comm_gather_f64: bad arguments");
+    return SA_ERR_ARG;
+  }
+  ncclComm_t c = (ncclComm_t)comm;
+  int rank = 0, nranks = 0;
+  SA_NCCL_CHECK(ncclCommUserRank(c, &rank));
+  SA_NCCL_CHECK(ncclCommCount(c, &nranks));
+  if (root < 0 || root >= nranks || (rank == root && !recv)) {
+    sa_set_error("sa_comm_gather_f64: bad root %d or missing receive buffer (world %d)", root, nranks);
+    return SA_ERR_ARG;
+  }
+  if (count == 0) return SA_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (rank != root) {
+    SA_NCCL_CHECK(ncclSend(send, (size_t)count, ncclFloat64, root, c, s));
+    return SA_OK;
+  }
+  double* own = recv + (size_t)root * count;
+  if (own != send) SA_HIP_CHECK(hipMemcpyAsync(own, send, count * sizeof(double), hipMemcpyDeviceToDevice, s));
+  SA_NCCL_CHECK(ncclGroupStart());
+  for (int r = 0; r < nranks; ++r) {
+    if (r == root) continue;
+    ncclResult_t e = ncclRecv(recv + (size_t)r * count, (size_t)count, ncclFloat64, r, c, s);
+    if (e != ncclSuccess) {
+      ncclGroupEnd();
+      sa_set_error("ncclRecv from rank %d failed: %s", r, ncclGetErrorString(e));
+      return SA_ERR_RCCL;
+    }
+  }
+  SA_NCCL_CHECK(ncclGroupEnd());
+  return SA_OK;
+}
+
 extern "C" int sa_comm_destroy(void* comm) {
   if (!comm) return SA_OK;
   SA_NCCL_CHECK(ncclCommDestroy((ncclComm_t)comm));

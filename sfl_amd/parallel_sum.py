@@ -109,6 +109,30 @@ class RcclComm:
                                               send.numel(), C.c_void_p(stream)), "sa_comm_allreduce_u64")
         return recv
 
+    def reduce_scatter_u64(self, send, recv):
+        """``recv`` (rank r) = the masked sum of ``send``'s r-th of ``world``
+        equal shards (in place when ``recv`` is that shard of ``send``)."""
+        import torch
+
+        if send.numel() != recv.numel() * self.world:
+            raise ValueError(f"reduce_scatter: {send.numel()} elements do not split into {self.world} x {recv.numel()}")
+        stream = torch.cuda.current_stream(send.device).cuda_stream
+        L.check(L.lib().sa_comm_reduce_scatter_u64(self._h, C.c_void_p(send.data_ptr()), C.c_void_p(recv.data_ptr()),
+                                                   recv.numel(), C.c_void_p(stream)), "sa_comm_reduce_scatter_u64")
+        return recv
+
+    def gather_f64(self, send, recv, root: int = 0):
+        """Root's ``recv`` (``world`` x ``send.numel()``) = every rank's float64 shard in rank order."""
+        import torch
+
+        if self.rank == root and (recv is None or recv.numel() != send.numel() * self.world):
+            raise ValueError("gather: the root needs a receive buffer of world x shard elements")
+        stream = torch.cuda.current_stream(send.device).cuda_stream
+        L.check(L.lib().sa_comm_gather_f64(self._h, C.c_void_p(send.data_ptr()),
+                                           C.c_void_p(recv.data_ptr()) if recv is not None else None,
+                                           send.numel(), root, C.c_void_p(stream)), "sa_comm_gather_f64")
+        return recv
+
     def close(self):
         if self._h:
             L.check(L.lib().sa_comm_destroy(self._h), "sa_comm_destroy")
@@ -129,6 +153,32 @@ def chunk_bounds(n: int, chunks: int, align: int = 1024) -> list[tuple[int, int]
     return out or [(0, 0)]
 
 
+def shard_layout(bounds: list[tuple[int, int]], world: int) -> list[tuple[int, int]]:
+    """The sharded server's split of every pipeline chunk:
+    chunk [lo, hi) is reduce-scattered as ``world`` equal shards of ``k``
+    elements (``(hi - lo) / world`` rounded up to a multiple of 128, so every
+    shard starts 1 KiB aligned), rank r's shard starting at ``lo + r*k``.
+    Returns [(lo, k)] per chunk.  Only the last chunk may need padding (the
+    pipeline's chunk starts are multiples of ``1024 * world``), so its shards
+    may run past n: buffers hold ``padded_len`` elements."""
+    return [(lo, -(-(hi - lo) // (world * 128)) * 128) for lo, hi in bounds]
+
+
+def padded_len(bounds: list[tuple[int, int]], world: int) -> int:
+    """Elements a sharded-server buffer must hold (n plus < world of padding)."""
+    return max((lo + world * k for lo, k in shard_layout(bounds, world)), default=0)
+
+
+def rank_shards(bounds: list[tuple[int, int]], world: int, rank: int, n: int) -> list[tuple[int, int]]:
+    """The element ranges [a, b) of [0, n) whose masked sum rank ``rank``
+    receives (and decodes) as the sharded server, one per chunk."""
+    out = []
+    for lo, k in shard_layout(bounds, world):
+        a = min(n, lo + rank * k)
+        out.append((a, min(n, a + k)))
+    return out
+
+
 class PipelinedMaskedSum:
     """One rank's share of a secure-aggregation round with the exchange
     overlapped: the fused masking launch of chunk j (compute stream) runs
@@ -137,14 +187,34 @@ class PipelinedMaskedSum:
     chunk).  Chunk j's streams start ``lo_j`` draws into the round, so the
     result is bit-identical to one launch over the whole vector.
 
-    ``chunk_gens[j]`` = ``plan_generators(plan, seed_of, offset=round_offset + lo_j)``."""
+    ``chunk_gens[j]`` = ``plan_generators(plan, seed_of, offset=round_offset + lo_j)``.
 
-    def __init__(self, comm: RcclComm | None, device, n: int, chunks: int):
+    ``exchange="sharded"``: the sharded server of SURVEY.md §8(e) instead of
+    the reduce to one rank -- each chunk's partial sum is reduce-scattered in
+    place (rank r receives the masked sum of its shard, ``shard_layout``),
+    every rank decodes its shard into ``dec`` on the comm stream, and with
+    ``gather=True`` the float64 shards are gathered into the root's ``dec``.
+    Partial-sum and ``dec`` buffers hold ``self.buffer_len`` elements (n plus
+    < world of padding that is reduced and decoded but never read)."""
+
+    def __init__(self, comm: RcclComm | None, device, n: int, chunks: int, exchange: str = "reduce"):
         import torch
 
+        if exchange not in ("reduce", "sharded"):
+            raise ValueError(f"exchange must be 'reduce' or 'sharded', not {exchange!r}")
+        if exchange == "sharded" and comm is None:
+            raise ValueError("the sharded server needs a communicator")
         self.comm = comm
         self.device = device
-        self.bounds = chunk_bounds(n, chunks)
+        self.n = n
+        self.exchange = exchange
+        world = comm.world if comm is not None else 1
+        # sharded: chunk starts on multiples of 1024 * world, so only the last
+        # chunk's shards can run past its end (into padding, never into the
+        # next chunk that the compute stream may be masking)
+        self.bounds = chunk_bounds(n, chunks, align=1024 * world if exchange == "sharded" else 1024)
+        self.shards = shard_layout(self.bounds, world) if exchange == "sharded" else None
+        self.buffer_len = padded_len(self.bounds, world) if exchange == "sharded" else n
         self.comm_stream = torch.cuda.Stream(device) if comm is not None else None
         self.events = [torch.cuda.Event() for _ in self.bounds]
         # reduce of chunk j done (comm stream): the next round's chunk-j launch
@@ -154,7 +224,8 @@ class PipelinedMaskedSum:
 
     def run(self, xs, weights, chunk_gens, n_cross: int, sum_buf, recv=None, *, root: int = 0,
             fxp_bits: int = 18, digests=None, flags=None, kernel_events: list | None = None,
-            exchange_events: list | None = None, join: bool = True):
+            exchange_events: list | None = None, join: bool = True, dec=None, divisor: float = 1.0,
+            gather: bool = False):
         """``kernel_events``: if given, a timing-event pair recorded around
         each chunk's masking launch is appended (kernel time without the
         exchange); ``exchange_events`` likewise around each chunk's reduce on
@@ -170,6 +241,12 @@ class PipelinedMaskedSum:
 
         if len(chunk_gens) != len(self.bounds):
             raise ValueError(f"{len(chunk_gens)} generator sets for {len(self.bounds)} chunks")
+        sharded = self.exchange == "sharded"
+        if sharded:
+            if recv is not None:
+                raise ValueError("the sharded server reduces in place (recv=None)")
+            if dec is None or dec.numel() < self.buffer_len or sum_buf.numel() < self.buffer_len:
+                raise ValueError(f"sharded server: sum_buf and dec need {self.buffer_len} elements")
         compute = torch.cuda.current_stream(self.device)
         for j, (lo, hi) in enumerate(self.bounds):
             pg, ps, cross = chunk_gens[j]
@@ -191,7 +268,18 @@ class PipelinedMaskedSum:
                         exchange_events.append((torch.cuda.Event(enable_timing=True),
                                                 torch.cuda.Event(enable_timing=True)))
                         exchange_events[-1][0].record(self.comm_stream)
-                    self.comm.reduce_u64(sum_buf[lo:hi], recv[lo:hi] if recv is not None else None, root=root)
+                    if sharded:
+                        lo_s, k = self.shards[j]
+                        mine = lo_s + self.comm.rank * k
+                        shard = self.comm.reduce_scatter_u64(sum_buf[lo_s:lo_s + k * self.comm.world],
+                                                             sum_buf[mine:mine + k])
+                        K.decode(shard, dec[mine:mine + k], fxp_bits=fxp_bits, divisor=divisor)
+                        if gather:
+                            self.comm.gather_f64(dec[mine:mine + k], dec[lo_s:lo_s + k * self.comm.world]
+                                                 if self.comm.rank == root else None, root=root)
+                    else:
+                        self.comm.reduce_u64(sum_buf[lo:hi], recv[lo:hi] if recv is not None else None,
+                                             root=root)
                     if exchange_events is not None:
                         exchange_events[-1][1].record(self.comm_stream)
                     self.reduced[j].record(self.comm_stream)
@@ -199,4 +287,6 @@ class PipelinedMaskedSum:
         if self.comm is not None and join:
             compute.wait_stream(self.comm_stream)
             self._pending = [False] * len(self.bounds)
+        if sharded:
+            return dec
         return recv if recv is not None else sum_buf

@@ -101,6 +101,8 @@ def test_every_entry_point_validates_before_touching_the_gpu():
         "sa_comm_init": lambda: lib.sa_comm_init(None, None, 0, 0, 0),
         "sa_comm_reduce_u64": lambda: lib.sa_comm_reduce_u64(None, None, None, 10, 0, None),
         "sa_comm_allreduce_u64": lambda: lib.sa_comm_allreduce_u64(None, None, None, 10, None),
+        "sa_comm_reduce_scatter_u64": lambda: lib.sa_comm_reduce_scatter_u64(None, None, None, 10, None),
+        "sa_comm_gather_f64": lambda: lib.sa_comm_gather_f64(None, None, None, 10, 0, None),
         "sa_pcg64_raw_host": lambda: lib.sa_pcg64_raw_host(None, None, 5),
     }
     for name, call in calls.items():

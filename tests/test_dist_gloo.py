@@ -103,3 +103,37 @@ def test_chunk_bounds_cover_and_align(n, chunks):
     assert all(lo % 1024 == 0 for lo, _ in b)
     assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
     assert len(b) <= max(1, chunks)
+
+
+@pytest.mark.parametrize("n", [1, 1023, 50_003, 10**6 + 7, 10**8])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("chunks", [1, 3, 8])
+def test_sharded_server_layout(n, world, chunks):
+    """The sharded server's split: per chunk, ``world``
+    equal shards tile the chunk exactly (only the last chunk is padded, and
+    by less than world x 128 elements), shard starts are 1 KiB aligned, and
+    the ranks' decoded ranges cover [0, n) once."""
+    from sfl_amd.parallel_sum import chunk_bounds, padded_len, rank_shards, shard_layout
+
+    b = chunk_bounds(n, chunks, align=1024 * world)  # PipelinedMaskedSum's sharded bounds
+    lay = shard_layout(b, world)
+    for j, ((lo, hi), (lo2, k)) in enumerate(zip(b, lay)):
+        assert lo == lo2 and k % 128 == 0
+        if j < len(b) - 1:
+            assert world * k == hi - lo
+        else:
+            assert 0 <= world * k - (hi - lo) < world * 128
+    assert n <= padded_len(b, world) < n + world * 128
+    covered = []
+    for r in range(world):
+        for a, e in rank_shards(b, world, r, n):
+            assert 0 <= a <= e <= n
+            covered.append((a, e))
+    covered.sort()
+    pos = 0
+    for a, e in covered:
+        if a == e:
+            continue
+        assert a == pos
+        pos = e
+    assert pos == n

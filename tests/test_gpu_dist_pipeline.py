@@ -101,3 +101,93 @@ def test_ranks_pipeline_and_in_place_reduce(world, chunks):
         assert dig_ok is True, (rank, dig_ok)
         assert sum_ok, f"rank {rank}: root's in-place reduced sum differs from the oracle"
         assert fl == 0
+
+
+class GlooShardedServer:
+    """RcclComm's sharded-server contract (reduce_scatter_u64 / gather_f64)
+    through gloo host round trips, for W ranks on the one test GPU."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+
+    def reduce_scatter_u64(self, send, recv):
+        import torch.distributed as dist
+
+        host = send.cpu()  # on the comm stream: waits for the chunk's launch
+        dist.all_reduce(host, op=dist.ReduceOp.SUM)  # int64 addition wraps like uint64
+        k = recv.numel()
+        recv.copy_(host[self.rank * k:(self.rank + 1) * k], non_blocking=False)
+        return recv
+
+    def gather_f64(self, send, recv, root: int = 0):
+        import torch
+        import torch.distributed as dist
+
+        host = send.cpu()
+        parts = [torch.empty_like(host) for _ in range(self.world)] if self.rank == root else None
+        dist.gather(host, parts, dst=root)
+        if self.rank == root:
+            recv.copy_(torch.cat(parts), non_blocking=False)
+        return recv
+
+
+def _worker_sharded(rank, world, port, n, chunks, offset, q):
+    import torch
+    import torch.distributed as dist
+
+    from oracle import secagg as o
+    from sfl_amd.parallel_sum import PipelinedMaskedSum, plan_generators, plan_rank, rank_shards
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        C = 8
+        names = [f"client{c}" for c in range(C)]
+        seeds = o.seeds_for(names)
+        seed_of = lambda u, v: seeds[names[u]][names[v]]  # noqa: E731
+        rng = np.random.default_rng(78)
+        xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
+        dev = torch.device("cuda", 0)
+        plan = plan_rank(names, world, rank)
+        pipe = PipelinedMaskedSum(GlooShardedServer(rank, world), dev, n, chunks, exchange="sharded")
+        gens = [plan_generators(plan, seed_of, offset=offset + lo) for lo, _ in pipe.bounds]
+        part = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
+        dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev)
+        pipe.run([torch.from_numpy(xs[c]).to(dev) for c in plan.clients], [1.0] * len(plan.clients), gens,
+                 plan.n_cross, part, None, dec=dec, gather=True)
+        torch.cuda.synchronize()
+        ssum = o.server_sum(o.secure_masked(xs, names, seeds=seeds, offset=offset))
+        want = o.decode(ssum)
+        got_s, got_d = part.cpu().numpy().view(np.uint64), dec.cpu().numpy()
+        shard_ok = all(np.array_equal(got_s[a:b], ssum[a:b]) and np.array_equal(got_d[a:b], want[a:b])
+                       for a, b in rank_shards(pipe.bounds, world, rank, n))
+        full_ok = bool(np.array_equal(got_d[:n], want)) if rank == 0 else True
+        q.put((rank, shard_ok, full_ok))
+        dist.destroy_process_group()
+    except BaseException as e:  # noqa: BLE001 - reported to the parent
+        q.put((rank, repr(e), False))
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 3), (4, 2), (8, 8)])
+def test_ranks_sharded_server(world, chunks):
+    """exchange="sharded" with W real ranks: every rank's shard of the masked
+    sum and its float64 decode equal the oracle's on that range, and the
+    root's gathered decode equals the oracle's whole decoded sum."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    n = 70_001
+    procs = [ctx.Process(target=_worker_sharded, args=(r, world, port, n, chunks, 3 * 10**9 + 1, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for rank, shard_ok, full_ok in res:
+        assert shard_ok is True, (rank, shard_ok)
+        assert full_ok, f"rank {rank}: gathered decode differs from the oracle"

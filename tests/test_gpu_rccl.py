@@ -110,3 +110,52 @@ def test_back_to_back_rounds_without_join(comm):
     torch.cuda.synchronize()
     for r in range(3):
         assert np.array_equal(recvs[r].cpu().numpy().view(np.uint64), exps[r]), r
+
+
+def test_rccl_world1_reduce_scatter_and_gather(comm):
+    """The sharded server's collectives at world 1: the reduce-scatter of one
+    shard is the identity (in place and out of place), the gather a copy."""
+    rng = np.random.default_rng(2)
+    a = rng.integers(0, 2**64 - 1, 70_001, dtype=np.uint64)
+    send = torch.from_numpy(a.view(np.int64).copy()).cuda()
+    out = torch.empty_like(send)
+    comm.reduce_scatter_u64(send, out)
+    comm.reduce_scatter_u64(send, send)  # in place
+    f = torch.from_numpy(rng.standard_normal(70_001)).cuda()
+    g = torch.empty_like(f)
+    comm.gather_f64(f, g, root=0)
+    torch.cuda.synchronize()
+    assert torch.equal(out, send) and torch.equal(send.cpu(), torch.from_numpy(a.view(np.int64)))
+    assert torch.equal(g, f)
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_sharded_server_pipeline_world1(comm, chunks):
+    """exchange="sharded" at world 1 (the whole vector is rank 0's shard):
+    8 co-located clients, every chunk reduce-scattered, decoded on the comm
+    stream and gathered, two rounds back to back (join=False); the decoded
+    result equals the oracle's decode of the server sum bit for bit."""
+    from oracle import secagg as o
+    from sfl_amd.parallel_sum import PipelinedMaskedSum, plan_generators, plan_rank
+
+    C, n = 8, 60_007
+    names = [f"client{c}" for c in range(C)]
+    seeds = o.seeds_for(names)
+    plan = plan_rank(names, 1, 0)
+    dev = torch.device("cuda", 0)
+    pipe = PipelinedMaskedSum(comm, dev, n, chunks, exchange="sharded")
+    assert pipe.buffer_len >= n
+    seed_of = lambda u, v: seeds[names[u]][names[v]]  # noqa: E731
+    s = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
+    decs, exps = [], []
+    for r in range(2):
+        rng = np.random.default_rng(300 + r)
+        xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
+        exps.append(o.decode(o.server_sum(o.secure_masked(xs, names, seeds=seeds, offset=r * n)), divisor=4.0))
+        gens = [plan_generators(plan, seed_of, offset=r * n + lo) for lo, _ in pipe.bounds]
+        decs.append(torch.empty(pipe.buffer_len, dtype=torch.float64, device=dev))
+        pipe.run([torch.from_numpy(x).to(dev) for x in xs], [1.0] * C, gens, plan.n_cross, s, None,
+                 dec=decs[-1], divisor=4.0, gather=True, join=False)
+    torch.cuda.synchronize()
+    for r in range(2):
+        assert np.array_equal(decs[r][:n].cpu().numpy(), exps[r]), r
