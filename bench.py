@@ -535,7 +535,7 @@ def main():
 
 
 def extra_measurements(args, xs, plan, gens, K, torch, dev) -> dict:
-    """Secondary rates on one GPU (DESIGN.md §4/§6), none of them `value`:
+    """Secondary rates on one GPU (DESIGN.md §4/§7), none of them `value`:
 
     * wire chain: every client's masked vector materialised by its own
       sa_mask launch (7 streams each, no pair sharing), then sa_sum_u64;

@@ -119,6 +119,35 @@ def test_notebook_kat_through_the_plugin():
     assert np.abs(avg - np.array(k["secure_average"])).max() < 1e-8
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_config1_two_parties_1m_bit_exact(dtype):
+    """BASELINE config 1's shape through the plugin: 2 parties, a 1M-element
+    numpy vector each (np.random.rand-style like the KAT), sum then average
+    (consecutive stream positions): decoded float64 equal to the oracle bit
+    for bit, and within the stated tolerance of the float sum (|err| <
+    C * 2^-fxp for the sum, / C for the average)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    names, n = ["alice", "bob"], 1_000_000
+    seeds = o.seeds_for(names)
+    pyus = [PYU(nm, 0) for nm in names]
+    agg = SecureAggregator(pyus[0], pyus, seeds={("alice", "bob"): seeds["alice"]["bob"]})
+    rng = np.random.default_rng(11)
+    xs = [rng.random(n).astype(dtype) for _ in names]
+    objs = [p(lambda x=x: x)() for p, x in zip(pyus, xs)]
+    s = rv(agg.sum(objs, axis=0))
+    avg = rv(agg.average(objs, axis=0))
+    assert s.dtype == np.float64 and avg.dtype == np.float64
+    assert np.array_equal(s, o.secure_sum(xs, names, seeds=seeds)[0])
+    assert np.array_equal(avg, o.secure_average(xs, names, seeds=seeds, offset=n)[0])
+    fsum = xs[0].astype(np.float64) + xs[1]
+    assert np.abs(s - fsum).max() < 2 * 2.0**-18
+    assert np.abs(avg - fsum / 2).max() < 2.0**-18
+
+
 @pytest.mark.parametrize("fused,keep", [(True, False), (False, True), (True, True)])
 def test_rounds_match_oracle_bit_exact(fused, keep):
     """Several FL-style rounds with explicit seeds: decoded results equal the

@@ -53,7 +53,7 @@ def main():
                    else o.secure_average(xs, names, seeds=seeds)[0])
             exact = bool(np.array_equal(first, ref))
             tol = float(np.max(np.abs(first - (xs[0].astype(np.float64) + xs[1]) / (1 if kind == "sum" else 2))))
-            for _ in range(3):
+            for _ in range(20):  # clocks ramp after idle
                 fn(objs, axis=0)
             ts = []
             for _ in range(args.reps):
