@@ -296,6 +296,11 @@ def workload(args, world: int) -> str:
     from sfl_amd.parallel_sum import client_shard
 
     C, N = args.clients, args.elems
+    if (world > 1 or args.dist) and args.shard == "elements":
+        return (f"{C} clients x {N} fp32 grad elems over {world} GPUs, element-sharded: every rank masks its "
+                f"1/{world} of every client's elements in one fused launch k_clients<float,float,{C},0> "
+                f"({C * (C - 1) // 2} pair streams jumped to the slice start), decodes its slice of the sum"
+                + (", float64 slices gathered to rank 0" if args.gather else ""))
     L = len(client_shard(C, world, 0))
     X = C - L
     pairs = L * (L - 1) // 2
@@ -337,7 +342,11 @@ def main():
                     help="N>1 exchange: ncclReduce of the partial sums to rank 0 (default), or the sharded "
                          "server of SURVEY.md 8(e): ncclReduceScatter, every rank decodes its shard")
     ap.add_argument("--gather", action="store_true",
-                    help="with --exchange sharded: also gather the decoded float64 shards to rank 0")
+                    help="with --exchange sharded or --shard elements: also gather the decoded float64 shards "
+                         "to rank 0")
+    ap.add_argument("--shard", choices=("clients", "elements"), default="clients",
+                    help="N>1: clients in contiguous blocks per GPU (default, config 3), or every GPU takes "
+                         "1/N of every client's elements (SURVEY.md 8(e)'s alternative; no exchange for the sum)")
     ap.add_argument("--digests", action="store_true",
                     help="also fold every client's masked values into an XOR digest (test checksum)")
     ap.add_argument("--dry-run", action="store_true",
@@ -379,7 +388,7 @@ def main():
 
     from sfl_amd import _lib
     from sfl_amd import kernels as K
-    from sfl_amd.parallel_sum import PipelinedMaskedSum, RcclComm, plan_generators, plan_rank
+    from sfl_amd.parallel_sum import PipelinedMaskedSum, RcclComm, element_shard, plan_generators, plan_rank
 
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
@@ -393,25 +402,37 @@ def main():
 
     C, N = args.clients, args.elems
     names = [f"client{c}" for c in range(C)]
-    plan = plan_rank(names, world, rank)
+    by_elems = multi and args.shard == "elements"
+    # element sharding (SURVEY.md §8(e)'s alternative): every rank holds ALL
+    # clients' elements [e0, e0 + n_loc) and masks them in one fused launch,
+    # streams jumped to e0; no exchange for the sum (each rank's slice of it
+    # is complete), the decoded float64 slices gathered to rank 0 on --gather
+    plan = plan_rank(names, 1 if by_elems else world, 0 if by_elems else rank)
     Lc = len(plan.clients)
+    e0, n_loc, k_el = element_shard(N, world, rank) if by_elems else (0, N, N)
     xs = []
     for c in plan.clients:
         g = torch.Generator(device=dev).manual_seed(20260116 + c)
-        xs.append(torch.randn(N, generator=g, device=dev, dtype=torch.float32) * 1e-2)
+        x = torch.randn(N, generator=g, device=dev, dtype=torch.float32) * 1e-2
+        xs.append(x[e0:e0 + n_loc].clone() if by_elems else x)  # the same data as at N = 1
+        del x
     total_steps = args.warmup + args.steps
-    chunks = args.chunks if args.chunks is not None else (8 if world > 1 else 1)
-    sharded = multi and args.exchange == "sharded"
-    pipe = PipelinedMaskedSum(comm, dev, N, chunks, exchange="sharded" if sharded else "reduce")
+    chunks = args.chunks if args.chunks is not None else (8 if world > 1 and not by_elems else 1)
+    sharded = multi and args.exchange == "sharded" and not by_elems
+    pipe = PipelinedMaskedSum(None if by_elems else comm, dev, n_loc, chunks,
+                              exchange="sharded" if sharded else "reduce")
     # every step is a new round: streams start i*N draws in, chunk j at +lo_j
-    gens = [[plan_generators(plan, pair_seed, offset=i * N + lo) for lo, _ in pipe.bounds]
+    gens = [[plan_generators(plan, pair_seed, offset=i * N + e0 + lo) for lo, _ in pipe.bounds]
             for i in range(total_steps)]
     # the partial sum is reduced IN PLACE (rank 0, the server, receives the
     # masked sum in sum_buf; at N=1 the reduce is a no-op)
     # (sharded server: padded to whole shards, the padding zeroed once; every
     # rank decodes its shard of each chunk into dec on the comm stream)
-    sum_buf = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
+    sum_buf = torch.zeros(max(pipe.buffer_len, k_el if by_elems else 0), dtype=torch.int64, device=dev)
     dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev) if sharded else None
+    if by_elems:  # this rank's decoded slice (padded to the equal gather count) and rank 0's whole result
+        dec = torch.zeros(k_el, dtype=torch.float64, device=dev)
+        dec_all = torch.zeros(world * k_el, dtype=torch.float64, device=dev) if rank == 0 and args.gather else None
     # no per-client digests: an XOR checksum the tests use to pin every
     # client's masked vector, not part of the reference's arithmetic; the
     # kernel forms each client's masked value and adds it to the sum either
@@ -422,6 +443,19 @@ def main():
     xev = []  # (start, end) events around every reduce of the timed steps (comm stream)
 
     def step(i, timed_idx=None):
+        if by_elems:
+            pipe.run(xs, [1.0] * Lc, gens[i], 0, sum_buf[:n_loc], None, fxp_bits=args.fxp_bits,
+                     digests=digests, flags=flags, kernel_events=kev if timed_idx is not None else None)
+            cs = torch.cuda.current_stream(dev)
+            if timed_idx is not None:
+                xev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                xev[-1][0].record(cs)
+            K.decode(sum_buf[:k_el], dec, fxp_bits=args.fxp_bits)
+            if args.gather:
+                comm.gather_f64(dec, dec_all, root=0)
+            if timed_idx is not None:
+                xev[-1][1].record(cs)
+            return
         # join=False: a round's exchange tail overlaps the next round's first
         # launches (each chunk's launch still waits for that chunk's previous
         # reduce); the timed region ends with a device synchronise
@@ -455,8 +489,8 @@ def main():
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = C * N / (ms_per_step / 1e3)
-    draws = (len(plan.pairs) + len(plan.cross)) * N
-    bytes_alg = 4 * Lc * N + 8 * N  # per step: fp32 reads of the local clients + one u64 sum write
+    draws = (len(plan.pairs) + len(plan.cross)) * n_loc
+    bytes_alg = 4 * Lc * n_loc + 8 * n_loc  # per step: fp32 reads of the local clients + one u64 sum write
     launches = len(pipe.bounds)
     achieved = bytes_alg / (kern_ms / 1e3) / 1e9
     kname = f"k_clients<float, float, {Lc}, {plan.n_cross}>"  # the launch's kernel
@@ -464,7 +498,7 @@ def main():
     fused = Lc <= 8 and n_streams <= 32  # sa_fused_clients' limits (kMaxLocal, kMaxStreams)
     if not fused:  # sa_fused_clients masks client by client (sa_mask passes of <= 16 streams)
         kname = f"k_clients<float, float, 1, X<=16> per client and pass (fallback for {Lc} local clients)"
-    pmc = pmc_traffic(f"void sa::{kname}", N // launches)
+    pmc = pmc_traffic(f"void sa::{kname}", n_loc // launches)
     draws_s = draws / (kern_ms / 1e3)
     peak_draws = ceiling["draws_per_s"] if ceiling else PCG_PAIR_DRAWS_2WAVE
     out = {
@@ -482,7 +516,7 @@ def main():
         "data": "synthetic (N(0,0.01^2) fp32 gradients generated on device)",
         "config": {"workload": workload(args, world),
                    "clients": C, "elems_per_client": N, "clients_per_gpu": Lc,
-                   "parallelism": f"clients{world}", "pipeline_chunks": launches,
+                   "parallelism": f"{'elements' if by_elems else 'clients'}{world}", "pipeline_chunks": launches,
                    "client_digests": bool(args.digests)},
         # per launch: algorithmic bytes of one launch / its average duration
         # (HIP events on the launch stream); the step's launches are equal
@@ -512,7 +546,12 @@ def main():
         # ranks.  nccl-tests' convention: reduce bus bandwidth = algbw.
         xb = 8 * N
         coll = "ncclReduce(uint64, sum) in place to rank 0"
-        if sharded:
+        if by_elems:
+            xb = 8 * k_el if args.gather else 0
+            coll = ("none for the sum (element sharding: each rank's slice of the masked sum is complete); "
+                    "k_decode of the slice" + (", float64 slices gathered to rank 0 (ncclSend/Recv)"
+                                               if args.gather else ""))
+        elif sharded:
             coll = ("sharded server: ncclReduceScatter(uint64, sum) in place, every rank decodes its shard "
                     "(k_decode on the comm stream)" + (", float64 shards gathered to rank 0 (ncclSend/Recv)"
                                                        if args.gather else ""))
@@ -520,10 +559,11 @@ def main():
                            "chunks": launches, "bytes_per_rank_per_step": xb,
                            "ms_per_step": xchg_ms,
                            "algbw_GBps": xb / (xchg_ms / 1e3) / 1e9 if xchg_ms > 0 and world > 1 else None,
-                           "overlap": "chunk j's reduce runs while chunk j+1 is masked; "
-                                      "ms_per_step ~ max(kernel, exchange) + one chunk of fill/drain"}
+                           "overlap": ("decode (and gather) run after the slice's launch on the compute stream"
+                                       if by_elems else "chunk j's reduce runs while chunk j+1 is masked; "
+                                       "ms_per_step ~ max(kernel, exchange) + one chunk of fill/drain")}
         if world == 1:
-            out["exchange"]["note"] = "world 1 (--dist rehearsal): the in-place reduce moves no data"
+            out["exchange"]["note"] = "world 1 (--dist rehearsal): the collectives move no data between GPUs"
     if args.extra and world == 1:
         out["extra"] = extra_measurements(args, xs, plan, gens, K, torch, dev)
     if rank == 0:

@@ -179,6 +179,18 @@ def rank_shards(bounds: list[tuple[int, int]], world: int, rank: int, n: int) ->
     return out
 
 
+def element_shard(n: int, world: int, rank: int) -> tuple[int, int, int]:
+    """Element sharding (SURVEY.md §8(e)'s alternative to client sharding):
+    rank ``rank`` masks elements [e0, e0 + n_loc) of EVERY client, each pair
+    stream jumped e0 draws ahead (``plan_generators(..., offset=round + e0)``),
+    so its slice of the masked sum is complete without any exchange.  Slices
+    are ``k`` elements (n / world rounded up to 128; the last one shorter or
+    empty), so a gather moves equal counts.  Returns (e0, n_loc, k)."""
+    k = shard_layout([(0, n)], world)[0][1]
+    e0 = min(n, rank * k)
+    return e0, min(n, e0 + k) - e0, k
+
+
 class PipelinedMaskedSum:
     """One rank's share of a secure-aggregation round with the exchange
     overlapped: the fused masking launch of chunk j (compute stream) runs

@@ -137,3 +137,18 @@ def test_sharded_server_layout(n, world, chunks):
         assert a == pos
         pos = e
     assert pos == n
+
+
+@pytest.mark.parametrize("n", [0, 1, 1000, 70_001, 10**8])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_element_shard_slices(n, world):
+    """Element sharding: the ranks' slices tile [0, n) in rank order, every
+    slice starts 512-B aligned and holds at most the gather count k."""
+    from sfl_amd.parallel_sum import element_shard
+
+    pos = 0
+    for r in range(world):
+        e0, m, k = element_shard(n, world, r)
+        assert e0 == pos and 0 <= m <= k and k % 128 == 0
+        pos += m
+    assert pos == n

@@ -149,3 +149,40 @@ def test_per_rank_shapes_full_size(W):
         del wire, imgs, s1, part
     torch.cuda.synchronize()
     assert torch.equal(total, q_sum)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_element_sharding_slices_match_oracle(world):
+    """bench.py --shard elements: every rank masks its slice of ALL 8 clients
+    in one fused launch with the pair streams jumped to the slice start; the
+    ranks' slices of the masked sum (and of its decode) laid side by side
+    equal the oracle's whole-vector sum, in round 3 of a run (stream
+    positions 3n + e0)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import secagg as o
+    from sfl_amd import kernels as K
+    from sfl_amd.parallel_sum import element_shard, plan_generators, plan_rank
+
+    C, n, rnd = 8, 90_011, 3
+    names = [f"client{c}" for c in range(C)]
+    seeds = o.seeds_for(names)
+    seed_of = lambda u, v: seeds[names[u]][names[v]]  # noqa: E731
+    rng = np.random.default_rng(world)
+    xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
+    ssum = o.server_sum(o.secure_masked(xs, names, seeds=seeds, offset=rnd * n))
+    plan = plan_rank(names, 1, 0)
+    dev = torch.device("cuda", 0)
+    got_s, got_d = [], []
+    for r in range(world):
+        e0, m, k = element_shard(n, world, r)
+        pg, ps, cross = plan_generators(plan, seed_of, offset=rnd * n + e0)
+        s = torch.zeros(k, dtype=torch.int64, device=dev)
+        K.fused_clients([torch.from_numpy(x[e0:e0 + m].copy()).to(dev) for x in xs], [1.0] * C, pg, ps, cross, 0,
+                        s[:m])
+        d = K.decode(s, torch.empty(k, dtype=torch.float64, device=dev))
+        torch.cuda.synchronize()
+        got_s.append(s[:m].cpu().numpy().view(np.uint64))
+        got_d.append(d[:m].cpu().numpy())
+    assert np.array_equal(np.concatenate(got_s), ssum)
+    assert np.array_equal(np.concatenate(got_d), o.decode(ssum))
