@@ -44,6 +44,36 @@ class GlooReduce:
         return recv
 
 
+def _run_ranks(target, world, args):
+    """Spawn ``world`` rank processes and collect one result each.  A stalled
+    rank fails the test within 150 s (every worker dumps its Python stacks
+    to stderr after 100 s first) instead of running into the GPU harness's
+    3-minute silence limit; leftover ranks are killed."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_with_dump, args=(target, r, world, port, *args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        return sorted(q.get(timeout=150) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+
+
+def _with_dump(target, *args):
+    import faulthandler
+    import sys
+
+    faulthandler.dump_traceback_later(100, exit=False, file=sys.stderr)
+    target(*args)
+
+
 def _worker(rank, world, port, n, chunks, offset, q):
     import torch
     import torch.distributed as dist
@@ -85,18 +115,7 @@ def _worker(rank, world, port, n, chunks, offset, q):
 def test_ranks_pipeline_and_in_place_reduce(world, chunks):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    import torch.multiprocessing as mp
-
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    n = 50_003
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, chunks, 10**9 + 5, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=240) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
+    res = _run_ranks(_worker, world, (50_003, chunks, 10**9 + 5))
     for rank, dig_ok, sum_ok, fl in res:
         assert dig_ok is True, (rank, dig_ok)
         assert sum_ok, f"rank {rank}: root's in-place reduced sum differs from the oracle"
@@ -175,19 +194,7 @@ def test_ranks_sharded_server(world, chunks):
     root's gathered decode equals the oracle's whole decoded sum."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    import torch.multiprocessing as mp
-
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    n = 70_001
-    procs = [ctx.Process(target=_worker_sharded, args=(r, world, port, n, chunks, 3 * 10**9 + 1, q))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=240) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
+    res = _run_ranks(_worker_sharded, world, (70_001, chunks, 3 * 10**9 + 1))
     for rank, shard_ok, full_ok in res:
         assert shard_ok is True, (rank, shard_ok)
         assert full_ok, f"rank {rank}: gathered decode differs from the oracle"
