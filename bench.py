@@ -174,7 +174,13 @@ def pmc_traffic(kernel: str, elems_per_launch: int) -> dict | None:
     doubled (MI355X_MICROARCH.md, HBM); both corrections were checked on the
     k_sum_u64 calibration launch in the same runs (known bytes)."""
     import csv
+    import re
 
+    def shape(name):  # (L, X, K) of a k_clients kernel name (K, the pair set, was added in round 2)
+        m = re.search(r"k_clients<float, float, (\d+), (\d+)(?:, (\d+))?>", name)
+        return (int(m.group(1)), int(m.group(2)), int(m.group(3) or 0)) if m else None
+
+    want = shape(kernel)
     for d in PMC_DIRS:
         vals = {}
         for counter, fname, scale in (("FETCH_SIZE", "pmc_fetch_size.csv", 2.0),
@@ -184,7 +190,7 @@ def pmc_traffic(kernel: str, elems_per_launch: int) -> dict | None:
                 break
             with open(path) as f:
                 v = [float(r["Counter_Value"]) for r in csv.DictReader(f)
-                     if r["Kernel_Name"].startswith(kernel) and r["Counter_Name"] == counter]
+                     if want is not None and shape(r["Kernel_Name"]) == want and r["Counter_Name"] == counter]
             if not v:
                 break
             vals[counter] = scale * 1024.0 * sum(v) / len(v) * elems_per_launch / PMC_ELEMS
@@ -305,6 +311,15 @@ def workload(args, world: int) -> str:
     X = C - L
     pairs = L * (L - 1) // 2
     if world == 1:
+        if L > 8 and X == 0 and not args.digests:  # the pair-shared multi-launch schedule
+            from sfl_amd.kernels import many_schedule
+
+            groups, blocks = many_schedule(C)
+            return (f"{C} clients x {N} fp32 grad elems on 1 GPU, fxp {args.fxp_bits}, ring 2^64: pair-shared "
+                    f"schedule, every pair stream expanded once ({pairs} pair streams): {len(groups)} "
+                    f"k_clients<float,float,<=8,0> launches (the groups' clients and internal pairs) + "
+                    f"{len(blocks)} k_clients<float,float,8,0,1> launches (two quads' cross pairs, "
+                    f"sa_fused_bipartite), all adding into the sum")
         if L > 8 or pairs + L * X > 32:  # beyond sa_fused_clients' shapes: client by client
             return (f"{C} clients x {N} fp32 grad elems on 1 GPU, fxp {args.fxp_bits}, ring 2^64: per-client "
                     f"sa_mask passes of <= 16 streams accumulating into the sum ({C - 1} streams per client, "
@@ -493,10 +508,13 @@ def main():
     bytes_alg = 4 * Lc * n_loc + 8 * n_loc  # per step: fp32 reads of the local clients + one u64 sum write
     launches = len(pipe.bounds)
     achieved = bytes_alg / (kern_ms / 1e3) / 1e9
-    kname = f"k_clients<float, float, {Lc}, {plan.n_cross}>"  # the launch's kernel
+    kname = f"k_clients<float, float, {Lc}, {plan.n_cross}, 0>"  # the launch's kernel (K = 0: all pairs)
     n_streams = len(plan.pairs) + len(plan.cross)
     fused = Lc <= 8 and n_streams <= 32  # sa_fused_clients' limits (kMaxLocal, kMaxStreams)
-    if not fused:  # sa_fused_clients masks client by client (sa_mask passes of <= 16 streams)
+    if not fused and Lc > 8 and plan.n_cross == 0 and not args.digests:  # kernels.fused_many
+        kname = (f"pair-shared schedule for {Lc} local clients: k_clients<float, float, 8, 0, 1> "
+                 f"(sa_fused_bipartite) + k_clients<float, float, <=8, 0> launches")
+    elif not fused:  # sa_fused_clients masks client by client (sa_mask passes of <= 16 streams)
         kname = f"k_clients<float, float, 1, X<=16> per client and pass (fallback for {Lc} local clients)"
     pmc = pmc_traffic(f"void sa::{kname}", n_loc // launches)
     draws_s = draws / (kern_ms / 1e3)

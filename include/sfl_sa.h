@@ -152,6 +152,23 @@ int sa_fused_clients(const sa_local_client* clients, int n_clients, int x_type, 
                      const sa_mask_stream* cross, int n_cross, uint64_t* sum_out, int accumulate,
                      uint64_t* digests, uint32_t* flags, void* stream);
 
+/* One block of the pair-shared schedule for MORE co-located clients than one
+ * sa_fused_clients launch holds (more than 8): the 8 slots are two quads of
+ * clients, (0-3) and (4-7), and the launch expands only the 16 streams of the
+ * pairs BETWEEN the quads, each once, applied to both clients (pair_gens /
+ * pair_sign a-major: pair p = (p / 4, 4 + p % 4); sign for the lower slot as
+ * in sa_fused_clients).  The masked values go straight into the sum
+ * (sum_out = or += their sum; no per-client outputs or digests); a slot with
+ * x == NULL contributes masks only, one with x its quantized x * weight too.
+ * A quad's internal pairs come from a sa_fused_clients launch over the clients
+ * of two quads, so every pair stream of C clients is expanded exactly once:
+ * C(C-1)/2 draws per element instead of C(C-1) (sfl_amd/kernels.py
+ * fused_many).  Replaces the per-party `_Masker.mask` + server sum of
+ * SURVEY 8a a2-a5 for simulations with many parties per GPU.  float32 only. */
+int sa_fused_bipartite(const sa_local_client* clients, int x_type, uint64_t n, int fxp_bits,
+                       const sa_pcg64* pair_gens, const int8_t* pair_sign, uint64_t* sum_out,
+                       int accumulate, uint32_t* flags, void* stream);
+
 /* Server `_sum`: out[i] = sum_k in[k][i] mod 2^64 (np.sum over uint64,
  * pattern of sfl/security/aggregation/sparse_plain_aggregator.py:88-94).
  * `in` is a HOST array of k device pointers; out may alias in[0]. */

@@ -302,6 +302,64 @@ extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, i
   return fn(a, stream);
 }
 
+extern "C" int sa_fused_bipartite(const sa_local_client* clients, int x_type, uint64_t n, int fxp_bits,
+                                  const sa_pcg64* pair_gens, const int8_t* pair_sign, uint64_t* sum_out,
+                                  int accumulate, uint32_t* flags, void* stream) {
+  constexpr int L = kBipartiteClients, H = L / 2, PB = H * (L - H);
+  if (check_type(x_type, "sa_fused_bipartite x_type")) return SA_ERR_ARG;
+  if (n == 0 && fxp_bits >= 0 && fxp_bits <= 62) return SA_OK;  // empty vectors
+  if (!clients || !pair_gens || !pair_sign || !sum_out || fxp_bits < 0 || fxp_bits > 62) {
+    sa_set_error("sa_fused_bipartite: bad arguments");
+    return SA_ERR_ARG;
+  }
+  if (!aligned16(sum_out)) {
+    sa_set_error("sa_fused_bipartite: sum_out must be 16-byte aligned");
+    return SA_ERR_ARG;
+  }
+  KArgs a;
+  memset(&a, 0, sizeof(a));
+  a.n = n;
+  a.fxp_bits = fxp_bits;
+  a.scale_d = (double)((uint64_t)1 << fxp_bits);
+  a.scale_f = (float)a.scale_d;
+  uint64_t bias[L] = {0};
+  for (int c = 0; c < L; c++) {
+    if ((clients[c].x && !aligned16(clients[c].x)) || clients[c].masked_out) {
+      sa_set_error("sa_fused_bipartite: client %d: x not 16-byte aligned, or a masked_out (unsupported)", c);
+      return SA_ERR_ARG;
+    }
+    a.c[c].x = clients[c].x;  // NULL: the slot adds no quantized value
+    a.c[c].w = clients[c].weight;
+    a.c[c].ws[0] = a.c[c].ws[1] = (float)clients[c].weight * a.scale_f;
+  }
+  for (int p = 0; p < PB; p++) {  // pair p = (p / (L - H), H + p % (L - H)), the kernel's Pairs<L, kBipartite>
+    const int u = p / (L - H), v = H + p % (L - H);
+    const int sg = pair_sign[p];
+    if (sg != 1 && sg != -1) {
+      sa_set_error("sa_fused_bipartite: pair %d sign %d", p, sg);
+      return SA_ERR_ARG;
+    }
+    fill_stream(a.s[p], pair_gens[p], sg);
+    if (sg > 0) {  // as sa_fused_clients: u adds m, v subtracts it
+      bias[u] += kMaskOffset;
+      bias[v] += 0 - kMaskOffset;
+    } else {
+      bias[u] += 1 - kMaskOffset;
+      bias[v] += kMaskOffset - 1;
+    }
+  }
+  for (int c = 0; c < L; c++) a.c[c].bias = bias[c];
+  a.sum_out = sum_out;
+  a.sum_mode = accumulate ? 2 : 1;
+  a.flags = flags;
+  LaunchFn fn = find_clients_kernel(x_type, x_type, L, 0, 1);
+  if (!fn) {
+    sa_set_error("sa_fused_bipartite: no kernel for x_type=%d", x_type);
+    return SA_ERR_UNSUPPORTED;
+  }
+  return fn(a, stream);
+}
+
 extern "C" int sa_sum_u64(const uint64_t* const* in, int k, uint64_t n, uint64_t* out,
                           void* stream) {
   if (k >= 1 && n == 0) return SA_OK;  // empty vectors (their pointers may be null)

@@ -10,7 +10,7 @@ namespace sa {
 LaunchFn find_other_kernel(int xt, int ct, int L, int X);
 
 #define F32(L, X) SA_ENTRY(float, float, SA_F32, SA_F32, L, X)
-LaunchFn find_clients_kernel(int xt, int ct, int L, int X) {
+LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K) {
   static const KernelEntry kEntriesF32[] = {
     F32(1, 0),  F32(1, 1),  F32(1, 2),  F32(1, 3),  F32(1, 4),  F32(1, 5),  F32(1, 6),
     F32(1, 7),  F32(1, 8),  F32(1, 9),  F32(1, 10), F32(1, 11), F32(1, 12), F32(1, 13),
@@ -19,10 +19,13 @@ LaunchFn find_clients_kernel(int xt, int ct, int L, int X) {
     F32(2, 0), F32(3, 0), F32(4, 0), F32(5, 0), F32(6, 0), F32(7, 0), F32(8, 0),
     // fused: C = 8 over W = 2 / 4 GPUs, C = 4 over 2 GPUs
     F32(4, 4), F32(2, 6), F32(2, 2),
+    // the pair-shared schedule of more than 8 co-located clients: two quads'
+    // 16 cross pairs per launch (sa_fused_bipartite)
+    SA_ENTRY_K(float, float, SA_F32, SA_F32, 8, 0, kBipartite),
   };
   for (const KernelEntry& e : kEntriesF32)
-    if (e.xt == xt && e.ct == ct && e.L == L && e.X == X) return e.fn;
-  return find_other_kernel(xt, ct, L, X);
+    if (e.xt == xt && e.ct == ct && e.L == L && e.X == X && e.K == K) return e.fn;
+  return K == kAllPairs ? find_other_kernel(xt, ct, L, X) : nullptr;
 }
 #undef F32
 

@@ -383,11 +383,20 @@ __device__ __forceinline__ void pcg_draw_one(uint32_t& s0, uint32_t& s1, uint32_
                : SA_PCG_DRAW_CLOBBERS);
 }
 
-// Compile-time enumeration of the internal pairs (u < v) of L clients.
-template <int L>
+// Compile-time enumeration of the pairs (u < v) a launch's L local clients
+// share.  K = kAllPairs: every internal pair of the L clients.  K =
+// kBipartite: only the pairs between the lower and the upper half (a, b),
+// a < L/2 <= b, a-major -- one block of the pair-shared schedule for more
+// co-located clients than one launch holds (kernels.fused_many: the quads
+// of clients pairwise, each pair stream still expanded exactly once).
+constexpr int kAllPairs = 0;
+constexpr int kBipartite = 1;
+template <int L, int K = kAllPairs>
 struct Pairs {
-  static constexpr int count = L * (L - 1) / 2;
+  static constexpr int H = L / 2;
+  static constexpr int count = K == kBipartite ? H * (L - H) : L * (L - 1) / 2;
   static constexpr int u(int p) {
+    if (K == kBipartite) return p / (L - H);
     int k = p;
     for (int a = 0; a < L; a++) {
       const int row = L - 1 - a;
@@ -397,6 +406,7 @@ struct Pairs {
     return -1;
   }
   static constexpr int v(int p) {
+    if (K == kBipartite) return H + p % (L - H);
     int k = p;
     for (int a = 0; a < L; a++) {
       const int row = L - 1 - a;
@@ -441,9 +451,9 @@ struct Group {
   bool fa, fb;          // cross stream of a negated client: inverted sign mask
   int F;                // first-touch bits: 1 ua, 2 va, 4 ub, 8 vb (sa_draw2.h template argument)
 };
-template <int L, int X>
+template <int L, int X, int K = kAllPairs>
 struct Sched {
-  static constexpr int PI = Pairs<L>::count;
+  static constexpr int PI = Pairs<L, K>::count;
   static constexpr int P = PI + L * X;
   int n = 0;
   Group g[P > 0 ? P : 1] = {};
@@ -457,7 +467,7 @@ struct Sched {
       const int c = (q - PI) / (X > 0 ? X : 1);
       return Role{c, -1, false, negated<L>(c)};
     }
-    const int u = Pairs<L>::u(q), v = Pairs<L>::v(q);
+    const int u = Pairs<L, K>::u(q), v = Pairs<L, K>::v(q);
     if (!negated<L>(v)) return Role{u, v, false, false};  // both plain: u += t, v -= t
     if (!negated<L>(u)) return Role{u, v, true, false};   // v negated: both add
     return Role{v, u, false, false};                      // both negated: -u -= t, -v += t
@@ -523,9 +533,9 @@ struct Sched {
   }
 };
 
-template <int L, int X>
+template <int L, int X, int K = kAllPairs>
 struct SchedOf {
-  static constexpr Sched<L, X> value{};
+  static constexpr Sched<L, X, K> value{};
 };
 
 // f(std::integral_constant<int, 0>{}), ..., f(std::integral_constant<int, N-1>{}):
@@ -571,10 +581,10 @@ __device__ __forceinline__ kargs_t* fenced_args() {
   return p;
 }
 
-template <typename XT, typename CT, int L, int X>
-__global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count + L * X, L))
+template <typename XT, typename CT, int L, int X, int K = kAllPairs>
+__global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::count + L * X, L))
     k_clients(const KArgs a) {
-  constexpr int PI = Pairs<L>::count;
+  constexpr int PI = Pairs<L, K>::count;
   constexpr int P = PI + L * X;
   constexpr bool kGeneral = (L == 1);  // continue mode + per-element weights + DP
   static_assert(L >= 1 && L <= kMaxLocal, "L");
@@ -693,6 +703,8 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
         if (SA_ABLATE & 8) {
 #pragma unroll
           for (int k = 0; k < kE; k++) xv[c].v[k] = (XT)(int)(i + k + c);
+        } else if constexpr (K == kBipartite) {  // a client without x adds no quantized value (reads 0)
+          xv[c] = bload2<XT>(make_rsrc(ka->c[c].x, ka->c[c].x ? n * sizeof(XT) : 0), i);
         } else {
           xv[c] = bload2<XT>(make_rsrc(ka->c[c].x, cont ? 0 : n * sizeof(XT)), i);
         }
@@ -705,7 +717,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
         // clients: X - bias, see negated<L>): written by the client's first
         // draw (first-touch variants), preset here only where the schedule
         // cannot (Sched::preset)
-        if ((SchedOf<L, X>::value.preset >> c) & 1) {
+        if ((SchedOf<L, X, K>::value.preset >> c) & 1) {
           const uint64_t bias = negated<L>(c) ? (uint64_t)X - ka->c[c].bias : ka->c[c].bias;
 #pragma unroll
           for (int k = 0; k < kE; k++) acc[k][c] = bias;
@@ -717,7 +729,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L>::count +
     // schedule pairs them; group g+1's constants are scalar-loaded during
     // group g's first draw
     if constexpr (P > 0) {
-      using SO = SchedOf<L, X>;  // the schedule (a static constexpr: usable in the lambdas)
+      using SO = SchedOf<L, X, K>;  // the schedule (a static constexpr: usable in the lambdas)
       Inc ni[2], nj[2];  // next group's plain-step / tile-jump addends
       uint32_t nm[2];
       auto fetch = [&](int g) {
@@ -937,10 +949,10 @@ int occupancy_blocks(const void* kernel);  // sa_api.hip
 constexpr uint64_t kChunkElems = (1ull << 29) - kTile;
 static_assert(kChunkElems % kTile == 0, "chunk");
 
-template <typename XT, typename CT, int L, int X>
+template <typename XT, typename CT, int L, int X, int K = kAllPairs>
 int launch_clients(const KArgs& in, void* stream) {
-  constexpr int P = Pairs<L>::count + L * X;
-  const void* kfn = reinterpret_cast<const void*>(&k_clients<XT, CT, L, X>);
+  constexpr int P = Pairs<L, K>::count + L * X;
+  const void* kfn = reinterpret_cast<const void*>(&k_clients<XT, CT, L, X, K>);
   const int maxb = occupancy_blocks(kfn);
   if (maxb <= 0) return SA_ERR_HIP;
   for (uint64_t off = 0; off < in.n; off += kChunkElems) {
@@ -986,7 +998,7 @@ int launch_clients(const KArgs& in, void* stream) {
       a.s[j].cj_w0 = (uint32_t)a.s[j].cj_lo;
       a.s[j].cj_w1 = a.s[j].cj_lo >> 32;
     }
-    hipLaunchKernelGGL((k_clients<XT, CT, L, X>), dim3(grid), dim3(kBlockThreads), 0,
+    hipLaunchKernelGGL((k_clients<XT, CT, L, X, K>), dim3(grid), dim3(kBlockThreads), 0,
                        (hipStream_t)stream, a);
     SA_HIP_CHECK(hipGetLastError());
   }

@@ -25,6 +25,7 @@ namespace sa {
 constexpr int kMaxLocal = 8;     // co-located clients per fused launch
 constexpr int kMaxStreams = 32;  // mask streams per launch (kernel-arg resident)
 constexpr int kMaskPass = 16;    // streams per pass of the single-client kernel
+constexpr int kBipartiteClients = 8;  // sa_fused_bipartite: two quads, their 16 cross pairs
 
 // Kernel-argument image (lives in the kernarg segment; read with scalar loads).
 struct StreamArg {
@@ -79,6 +80,8 @@ static_assert(sizeof(KArgs) <= 4096, "kernel arguments must fit the 4 KiB kernar
 typedef int (*LaunchFn)(const KArgs& a, void* stream);
 
 // Returns the launcher for (xt, ct, L, X) or nullptr when not instantiated.
-LaunchFn find_clients_kernel(int xt, int ct, int L, int X);
+// K: pair set of the launch (0: every internal pair of the L clients; 1:
+// bipartite, the pairs between the lower and upper half -- sa_fused_bipartite)
+LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K = 0);
 
 }  // namespace sa

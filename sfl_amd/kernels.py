@@ -105,12 +105,80 @@ def fused_clients(xs: Sequence[torch.Tensor], weights: Sequence[float], pair_gen
                                   carr, int(n_cross), _ptr(sum_out), int(bool(accumulate)),
                                   _ptr(digests), _ptr(flags), C.c_void_p(_stream(sum_out)))
     if rc == L.SA_ERR_UNSUPPORTED:
-        # shapes without a fused instantiation (e.g. 32 clients, 4 per GPU):
-        # every client masks with its own streams (both ends of each internal
-        # pair) and accumulates into the sum -- same result, no pair sharing
+        if (nc > 8 and n_cross == 0 and digests is None and not (masked_outs and any(m is not None for m in masked_outs))
+                and xs[0].dtype == torch.float32):
+            # more co-located clients than one launch holds, only the sum wanted:
+            # the pair-shared schedule (every pair stream still expanded once)
+            return fused_many(xs, weights, pair_gens, pair_signs, sum_out, fxp_bits=fxp_bits,
+                              accumulate=accumulate, flags=flags)
+        # other shapes without a fused instantiation (e.g. 32 clients, 4 per
+        # GPU, with cross streams; or per-client digests / wire images): every
+        # client masks with its own streams (both ends of each internal pair)
+        # and accumulates into the sum -- same result, no pair sharing
         return _fused_fallback(xs, weights, pair_gens, pair_signs, cross, n_cross, sum_out, fxp_bits,
                                accumulate, digests, flags, masked_outs)
     L.check(rc, "sa_fused_clients")
+    return sum_out
+
+
+def many_schedule(nc: int) -> tuple[list[list[int]], list[tuple[list[int], list[int]]]]:
+    """The pair-shared schedule of ``nc`` co-located clients (more than one
+    launch holds): clients in quads of 4 (the last may be short), quads in
+    groups of two.  Returns (groups, bipartite blocks): one sa_fused_clients
+    launch per group (its clients' quantized values and every pair inside the
+    group) and one sa_fused_bipartite launch per pair of quads in different
+    groups (their cross pairs) -- every pair of clients exactly once."""
+    quads = [list(range(q, min(nc, q + 4))) for q in range(0, nc, 4)]
+    groups = [quads[g] + (quads[g + 1] if g + 1 < len(quads) else []) for g in range(0, len(quads), 2)]
+    blocks = [(quads[a], quads[b]) for a in range(len(quads)) for b in range(a + 1, len(quads)) if a // 2 != b // 2]
+    return groups, blocks
+
+
+_PAD_STREAM = (0, 1)  # (state, inc) of a padding slot's pairs: drawn, and cancelled in the sum
+
+
+def fused_many(xs: Sequence[torch.Tensor], weights: Sequence[float], pair_gens: Sequence, pair_signs: Sequence[int],
+               sum_out: torch.Tensor, *, fxp_bits: int = 18, accumulate: bool = False,
+               flags: torch.Tensor | None = None) -> torch.Tensor:
+    """Masked sum of ``len(xs)`` co-located float32 clients (any number) with
+    every pair stream expanded ONCE and applied to both of its clients
+    (``many_schedule``; ``pair_gens`` / ``pair_signs`` in sa_fused_clients'
+    u-major order).  All launches add into ``sum_out``; the sum equals the
+    per-client path's bit for bit.  A short last quad is padded with slots
+    that have no input and dummy pair streams, whose masks cancel in the sum."""
+    _require_gpu(sum_out, flags, *xs)
+    nc, n = len(xs), sum_out.numel()
+    pidx, p = {}, 0
+    for u in range(nc):
+        for v in range(u + 1, nc):
+            pidx[(u, v)] = p
+            p += 1
+    groups, blocks = many_schedule(nc)
+    first = not accumulate
+    for grp in groups:
+        gp = [(u, v) for i, u in enumerate(grp) for v in grp[i + 1:]]
+        fused_clients([xs[c] for c in grp], [weights[c] for c in grp], [pair_gens[pidx[q]] for q in gp],
+                      [pair_signs[pidx[q]] for q in gp], [], 0, sum_out, fxp_bits=fxp_bits, accumulate=not first,
+                      flags=flags)
+        first = False
+    pad = L.PCG64.of(*_PAD_STREAM)
+    clients = (L.LocalClient * 8)()
+    for c in range(8):
+        clients[c].x, clients[c].weight, clients[c].masked_out = None, 1.0, None
+    for qa, qb in blocks:
+        gens, signs = [], []
+        for i in range(4):
+            for j in range(4):
+                if i < len(qa) and j < len(qb):
+                    q = pidx[(qa[i], qb[j])]
+                    gens.append(pair_gens[q])
+                    signs.append(int(pair_signs[q]))
+                else:
+                    gens.append(pad)
+                    signs.append(1)
+        L.check(L.lib().sa_fused_bipartite(clients, L.SA_F32, n, int(fxp_bits), (L.PCG64 * 16)(*gens),
+                                           (C.c_int8 * 16)(*signs), _ptr(sum_out), 1, _ptr(flags),
+                                           C.c_void_p(_stream(sum_out))), "sa_fused_bipartite")
     return sum_out
 
 

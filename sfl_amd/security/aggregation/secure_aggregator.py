@@ -248,7 +248,7 @@ class SecureAggregator(Aggregator):
         of small models)."""
         if as_torch or not self._fused or self._keep_masked or n == 0:
             return False
-        if not 2 <= len(data) <= MAX_FUSED_CLIENTS:
+        if len(data) < 2 or (len(data) > MAX_FUSED_CLIENTS and self._careful):
             return False
         sgpu = self._device.gpu
         if any(d.device.gpu != sgpu for d in data):
@@ -405,8 +405,13 @@ class SecureAggregator(Aggregator):
         names = [p.party for p in parties]
         C = len(names)
         s = torch.empty(n, dtype=K.U64, device=sdev)
-        digests = torch.zeros(C, dtype=K.U64, device=sdev)
-        fusable = (self._fused and 2 <= C <= MAX_FUSED_CLIENTS
+        # more co-located parties than one launch holds: the pair-shared
+        # multi-launch schedule (kernels.fused_many), which forms only the sum
+        # (no per-party digests; wire images and the careful replay take the
+        # per-party path below)
+        many = C > MAX_FUSED_CLIENTS
+        digests = None if many else torch.zeros(C, dtype=K.U64, device=sdev)
+        fusable = (self._fused and C >= 2 and (not many or not (self._keep_masked or self._careful))
                    and all(p.gpu == server.gpu for p in parties)
                    and all(ct == np.dtype(np.float32) for ct in cts)
                    and all(x.dtype == torch.float32 for x in xs)
@@ -433,6 +438,8 @@ class SecureAggregator(Aggregator):
             if self._keep_masked:
                 masked_keep.append(masked)
         else:
+            if digests is None:
+                digests = torch.zeros(C, dtype=K.U64, device=sdev)
             masked = []
             for ci, p in enumerate(parties):
                 out = torch.empty(n, dtype=K.U64, device=p.torch_device)

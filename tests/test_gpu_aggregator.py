@@ -322,3 +322,34 @@ def test_zero_size_and_ragged_layers(fused):
     got = rv(agg.sum([p(lambda x=x: x)() for p, x in zip(pyus, xs)], axis=0))
     exp, _, _ = o.secure_sum(xs, names, seeds=seeds, offset=5)
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("as_torch", [False, True])
+def test_many_colocated_parties_pair_shared(as_torch):
+    """12 / 13 parties on one GPU (more than one fused launch holds): the
+    plugin takes the pair-shared schedule (every pair stream expanded once);
+    three weighted rounds, numpy (host latency path) or torch payloads, equal
+    the oracle's decoded averages bit for bit at the advancing stream
+    positions."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    C = 13 if as_torch else 12
+    names = [f"p{c:02d}" for c in range(C)][::-1]
+    seeds = o.seeds_for(names)
+    pyus = [PYU(nm, 0) for nm in names]
+    agg = SecureAggregator(PYU("server", 0), pyus,
+                           seeds={(a, b): seeds[a][b] for a in names for b in names if a < b})
+    rng = np.random.default_rng(C)
+    offset = 0
+    for rnd in range(3):
+        xs = [(rng.standard_normal(1001) * 0.1).astype(np.float32) for _ in names]
+        w = [3 * c + rnd + 1 for c in range(C)]
+        objs = [p(lambda x=x: torch.from_numpy(x).cuda() if as_torch else x)() for p, x in zip(pyus, xs)]
+        got = rv(agg.average(objs, axis=0, weights=w))
+        got = got.cpu().numpy() if as_torch else got
+        exp = o.secure_average(xs, names, weights=w, seeds=seeds, offset=offset)[0]
+        assert np.array_equal(got, exp), rnd
+        offset += xs[0].size

@@ -4,6 +4,8 @@ Bar: bit-exact for every integer output (masked vectors, masked sums, XOR
 digests); decoded float64 equal to the oracle's float64 (same IEEE ops) and
 within C * 2^-fxp of the float sum (the quantization tolerance).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -470,6 +472,52 @@ def test_fused_more_than_8_clients_falls_back():
     torch.cuda.synchronize()
     assert np.array_equal(_u64(s), o.server_sum(masked))
     assert [int(v) for v in _u64(dig)] == [o.digest(m) for m in masked]
+
+
+@pytest.mark.parametrize("C", [9, 12, 13, 16, 21, 32])
+@pytest.mark.parametrize("n", [5, 4099, 70001])
+def test_fused_many_pair_shared_bit_exact(C, n):
+    """More co-located clients than one launch holds and only the sum wanted
+    (no digests / wire images): fused_clients routes to the pair-shared
+    schedule -- groups of up to 8 through sa_fused_clients, every pair of
+    quads in different groups through sa_fused_bipartite, a short last quad
+    padded -- so every pair stream is expanded once.  The sum equals the
+    oracle's bit for bit (weighted clients, mixed pair signs), also
+    accumulated onto a prior sum, and the PRG flag stays clear."""
+    K = _K()
+    offset = 5 * n + 3
+    names, xs, seeds, pg, ps = _fused_setup(C, n, offset)
+    w = [1 + c % 3 for c in range(C)]
+    exp = o.server_sum(o.secure_masked(xs, names, weights=w, seeds=seeds, offset=offset))
+    xt = [torch.from_numpy(x).to(DEV) for x in xs]
+    s = torch.empty(n, dtype=torch.int64, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.fused_clients(xt, [float(v) for v in w], pg, ps, [], 0, s, flags=flags)
+    base = np.random.default_rng(C).integers(0, 2**63, n, dtype=np.uint64)
+    acc = torch.from_numpy(base.view(np.int64).copy()).to(DEV)
+    K.fused_many(xt, [float(v) for v in w], pg, ps, acc, accumulate=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(s), exp)
+    assert np.array_equal(_u64(acc), base + exp)
+    assert int(flags.item()) == 0
+
+
+def test_fused_many_padding_streams_cancel():
+    """A bipartite launch whose slots are all padding (no input, dummy pair
+    streams) leaves the sum unchanged: the padded pairs' masks cancel."""
+    K, L = _K(), _L()
+    n = 10_007
+    base = np.random.default_rng(5).integers(0, 2**64 - 1, n, dtype=np.uint64)
+    s = torch.from_numpy(base.view(np.int64).copy()).to(DEV)
+    clients = (L.LocalClient * 8)()
+    for c in range(8):
+        clients[c].x, clients[c].weight, clients[c].masked_out = None, 1.0, None
+    gens = (L.PCG64 * 16)(*[L.pcg64_from_seed(1000 + p) for p in range(16)])
+    signs = (ctypes.c_int8 * 16)(*[1 if p % 3 else -1 for p in range(16)])
+    L.check(L.lib().sa_fused_bipartite(clients, L.SA_F32, n, 18, gens, signs, ctypes.c_void_p(s.data_ptr()), 1, None,
+                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "bipartite")
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(s), base)
 
 
 def test_chunked_launch_past_4gib():

@@ -15,6 +15,6 @@ for line in sys.stdin:
             cur[key.split()[0] + ("Spill" if "Spill" in key else "")] = int(m.group(1))
 for r in rows:
     n = r["name"]
-    m = re.search(r"k_clientsI(\w+?)Li(\d+)ELi(\d+)E", n)
-    tag = f"{m.group(1)} L={m.group(2)} X={m.group(3)}" if m else n
+    m = re.search(r"k_clientsI(\w+?)Li(\d+)ELi(\d+)E(?:Li(\d+)E)?", n)
+    tag = f"{m.group(1)} L={m.group(2)} X={m.group(3)}" + (" K=1" if m.group(4) == "1" else "") if m else n
     print(f"{tag:28s} vgpr={r.get('VGPRs')} vspill={r.get('VGPRsSpill')} sspill={r.get('SGPRsSpill')} scratch={r.get('ScratchSize')} occ={r.get('Occupancy')}")
