@@ -144,7 +144,9 @@ int sa_mask(const void* x, int x_type, int compute_type, uint64_t n, double weig
  *   digests         n_clients u64 (XOR-accumulated; zero them first)
  * Shapes without a fused kernel (more than 8 clients, more than 32 streams,
  * or an uninstantiated (C, n_cross)) return SA_ERR_UNSUPPORTED: the caller
- * then masks client by client with sa_mask(..., sum_accum), same result.
+ * then masks client by client with sa_mask(..., sum_accum), same result, or
+ * -- more than 8 clients, only the sum wanted -- runs the pair-shared
+ * schedule with sa_fused_bipartite below.
  * Replaces: the client-side `mask` calls plus server `_sum`'s
  * np.sum(..., axis=0) for co-located parties. */
 int sa_fused_clients(const sa_local_client* clients, int n_clients, int x_type, uint64_t n,
@@ -157,11 +159,12 @@ int sa_fused_clients(const sa_local_client* clients, int n_clients, int x_type, 
  * clients, (0-3) and (4-7), and the launch expands only the 16 streams of the
  * pairs BETWEEN the quads, each once, applied to both clients (pair_gens /
  * pair_sign a-major: pair p = (p / 4, 4 + p % 4); sign for the lower slot as
- * in sa_fused_clients).  The masked values go straight into the sum
- * (sum_out = or += their sum; no per-client outputs or digests); a slot with
- * x == NULL contributes masks only, one with x its quantized x * weight too.
- * A quad's internal pairs come from a sa_fused_clients launch over the clients
- * of two quads, so every pair stream of C clients is expanded exactly once:
+ * in sa_fused_clients).  Masks only: the slots' x and masked_out must be
+ * NULL (the clients' quantized values, and each quad's internal pairs, come
+ * from a sa_fused_clients launch over the clients of two quads); the 16
+ * masks, added to both clients of each pair, go straight into the sum
+ * (sum_out = or += their sum), so every pair stream of C clients is expanded
+ * exactly once:
  * C(C-1)/2 draws per element instead of C(C-1) (sfl_amd/kernels.py
  * fused_many).  Replaces the per-party `_Masker.mask` + server sum of
  * SURVEY 8a a2-a5 for simulations with many parties per GPU.  float32 only. */

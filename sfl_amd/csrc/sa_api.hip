@@ -324,11 +324,10 @@ extern "C" int sa_fused_bipartite(const sa_local_client* clients, int x_type, ui
   a.scale_f = (float)a.scale_d;
   uint64_t bias[L] = {0};
   for (int c = 0; c < L; c++) {
-    if ((clients[c].x && !aligned16(clients[c].x)) || clients[c].masked_out) {
-      sa_set_error("sa_fused_bipartite: client %d: x not 16-byte aligned, or a masked_out (unsupported)", c);
+    if (clients[c].x || clients[c].masked_out) {
+      sa_set_error("sa_fused_bipartite: client %d: masks only (x and masked_out must be NULL)", c);
       return SA_ERR_ARG;
     }
-    a.c[c].x = clients[c].x;  // NULL: the slot adds no quantized value
     a.c[c].w = clients[c].weight;
     a.c[c].ws[0] = a.c[c].ws[1] = (float)clients[c].weight * a.scale_f;
   }

@@ -703,8 +703,8 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
         if (SA_ABLATE & 8) {
 #pragma unroll
           for (int k = 0; k < kE; k++) xv[c].v[k] = (XT)(int)(i + k + c);
-        } else if constexpr (K == kBipartite) {  // a client without x adds no quantized value (reads 0)
-          xv[c] = bload2<XT>(make_rsrc(ka->c[c].x, ka->c[c].x ? n * sizeof(XT) : 0), i);
+        } else if constexpr (K == kBipartite) {  // masks only: the clients' values enter elsewhere
+          xv[c].v[0] = xv[c].v[1] = (XT)0;
         } else {
           xv[c] = bload2<XT>(make_rsrc(ka->c[c].x, cont ? 0 : n * sizeof(XT)), i);
         }
@@ -842,7 +842,19 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
     };
     static_assert(kE == 2, "finish() takes the lane's two elements");
     float p[L][kE];
-    if (cont) {  // a further pass: add the prior pass's masked vector
+    if constexpr (K == kBipartite) {
+      // masks only (sa_fused_bipartite): the sum of the 8 accumulators, the
+      // upper quad's stored negated
+#pragma unroll
+      for (int k = 0; k < kE; k++) {
+        uint64_t A = acc[k][0], B = acc[k][L / 2];
+#pragma unroll
+        for (int c = 1; c < L / 2; c++) A += acc[k][c];
+#pragma unroll
+        for (int c = L / 2 + 1; c < L; c++) B += acc[k][c];
+        sum[k] = A - B;
+      }
+    } else if (cont) {  // a further pass: add the prior pass's masked vector
 #pragma unroll
       for (int c = 0; c < L; c++) finish(c, pv[kGeneral ? c : 0].v[0], pv[kGeneral ? c : 0].v[1]);
     } else if (__builtin_expect(fast_products<XT, CT, L, kGeneral>(xv, wv, ka, qs, p), 1)) {
