@@ -502,6 +502,38 @@ def test_fused_many_pair_shared_bit_exact(C, n):
     assert int(flags.item()) == 0
 
 
+def test_fused_many_full_size_32_clients():
+    """Config 5's 32 clients on one GPU at 64M elements each (the bench runs
+    256M): the pair-shared schedule's sum equals the sum of the unmasked
+    quantized vectors (every pair's masks cancel) and the per-client path's
+    sum (both ends of every pair drawn separately, with digests), bit for
+    bit; no PRG flag."""
+    K, L = _K(), _L()
+    C, n = 32, 64 * 2**20 + 77
+    names = [f"client{c:02d}" for c in range(C)]
+    seeds = o.seeds_for(names)
+    xs = [torch.randn(n, device=DEV, dtype=torch.float32) * 1e-2 for _ in range(C)]
+    pg, ps = [], []
+    for u in range(C):
+        for v in range(u + 1, C):
+            pg.append(L.pcg64_advance(L.pcg64_from_seed(seeds[names[u]][names[v]]), 7 * n))
+            ps.append(1 if names[v] > names[u] else -1)
+    s = torch.empty(n, dtype=torch.int64, device=DEV)
+    flags = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.fused_clients(xs, [1.0] * C, pg, ps, [], 0, s, flags=flags)  # -> fused_many
+    q_sum = torch.zeros(n, dtype=torch.int64, device=DEV)
+    qbuf = torch.empty(n, dtype=torch.int64, device=DEV)
+    for x in xs:
+        K.mask(x, qbuf, [], sum_accum=q_sum)
+    s2 = torch.empty(n, dtype=torch.int64, device=DEV)
+    dig = torch.zeros(C, dtype=torch.int64, device=DEV)
+    K.fused_clients(xs, [1.0] * C, pg, ps, [], 0, s2, digests=dig)  # per-client path
+    torch.cuda.synchronize()
+    assert torch.equal(s, q_sum)
+    assert torch.equal(s, s2)
+    assert int(flags.item()) == 0
+
+
 def test_fused_many_padding_streams_cancel():
     """A bipartite launch whose slots are all padding (no input, dummy pair
     streams) leaves the sum unchanged: the padded pairs' masks cancel."""
