@@ -8,7 +8,7 @@ role RCCL plays on the GPUs).  Rank 0 compares with the oracle's full
 server sum: the sharding must lose or double no mask.
 """
 import os
-import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -16,22 +16,13 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def _worker(rank, world, port, C, n, q):
+def _worker(rank, world, init, C, n, q):
     import torch
 
     from oracle import secagg as o
     from sfl_amd.parallel_sum import client_shard, plan_rank
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     names = [f"client{c}" for c in range(C)][::-1]  # names not in index order: signs matter
     rng = np.random.default_rng(0)
     xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
@@ -65,8 +56,8 @@ def _worker(rank, world, port, C, n, q):
 def test_sharded_masked_sum_world2(C):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, C, 777, q)) for r in range(2)]
+    init = "file://" + os.path.join(tempfile.mkdtemp(prefix="sfl_gloo_"), "store")  # no TCP port to race for
+    procs = [ctx.Process(target=_worker, args=(r, 2, init, C, 777, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

@@ -11,21 +11,12 @@ uint64 reduce.  Everything else is the product code path the N > 1 bench
 runs.  The root's buffer must equal the oracle's server sum bit for bit, and
 every client's digest the oracle's."""
 import os
-import socket
 
 import numpy as np
 import pytest
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 class GlooReduce:
@@ -51,10 +42,14 @@ def _run_ranks(target, world, args):
     3-minute silence limit; leftover ranks are killed."""
     import torch.multiprocessing as mp
 
+    import tempfile
+
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_with_dump, args=(target, r, world, port, *args, q)) for r in range(world)]
+    # file-based rendezvous: no TCP port that another process could take
+    # between choosing it and binding it (a rank would then wait forever)
+    init = "file://" + os.path.join(tempfile.mkdtemp(prefix="sfl_ranks_"), "store")
+    procs = [ctx.Process(target=_with_dump, args=(target, r, world, init, *args, q)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -74,7 +69,7 @@ def _with_dump(target, *args):
     target(*args)
 
 
-def _worker(rank, world, port, n, chunks, offset, q):
+def _worker(rank, world, init, n, chunks, offset, q):
     import torch
     import torch.distributed as dist
 
@@ -82,8 +77,7 @@ def _worker(rank, world, port, n, chunks, offset, q):
     from sfl_amd.parallel_sum import PipelinedMaskedSum, plan_generators, plan_rank
 
     try:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
         C = 8
         names = [f"client{c}" for c in range(C)]
         seeds = o.seeds_for(names)
@@ -150,7 +144,7 @@ class GlooShardedServer:
         return recv
 
 
-def _worker_sharded(rank, world, port, n, chunks, offset, q):
+def _worker_sharded(rank, world, init, n, chunks, offset, q):
     import torch
     import torch.distributed as dist
 
@@ -158,8 +152,7 @@ def _worker_sharded(rank, world, port, n, chunks, offset, q):
     from sfl_amd.parallel_sum import PipelinedMaskedSum, plan_generators, plan_rank, rank_shards
 
     try:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
         C = 8
         names = [f"client{c}" for c in range(C)]
         seeds = o.seeds_for(names)
