@@ -74,3 +74,27 @@ def test_world_one_runs_in_process():
     assert line["n_gpus"] == 1 and line["ranks"][0]["pid"] != os.getpid()
     assert line["cpu_baseline"] is None
     assert "k_clients<float,float,8,0>" in line["config"]["workload"]
+
+
+@pytest.mark.parametrize("opts,expect", [
+    (["--exchange", "sharded", "--gather"], "ncclReduceScatter(uint64) of the partial sum"),
+    (["--shard", "elements"], "element-sharded: every rank masks its 1/2 of every client's elements"),
+])
+def test_exchange_options_reach_every_rank(opts, expect):
+    """The N>1 exchange options (sharded server, element sharding) pass
+    through the self-launcher to the ranks and name themselves in
+    config.workload."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--cpu-baseline-seconds", "0", *opts],
+                       capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    assert line["n_gpus"] == 2 and expect in line["config"]["workload"]
+
+
+def test_many_client_workload_names_the_pair_shared_schedule():
+    r = subprocess.run([sys.executable, BENCH, "--dry-run", "--cpu-baseline-seconds", "0", "--clients", "32",
+                        "--elems", "1000"], capture_output=True, text=True, timeout=120, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    assert "pair-shared schedule" in line["config"]["workload"] and "24 k_clients<float,float,8,0,1>" in \
+        line["config"]["workload"]
