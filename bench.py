@@ -634,14 +634,18 @@ def extra_measurements(args, xs, plan, gens, K, torch, dev) -> dict:
         K.sum_u64(outs, s)
 
     t = timeit(wire)
-    res.update({"wire_chain_ms": t * 1e3, "wire_chain_grad_elems_per_s": C * N / t})
+    # SURVEY.md 8(d)'s wire-faithful bytes: per client 4 B read + 8 B written
+    # (sa_mask), 8 B read again by the server sum, plus the 8-B sum written
+    res.update({"wire_chain_ms": t * 1e3, "wire_chain_grad_elems_per_s": C * N / t,
+                "wire_chain_algorithmic_GBps": (20 * C * N + 8 * N) / t / 1e9})
     pg, ps, cross = plan_generators_full(plan)
 
     def fused_wire():
         K.fused_clients(xs, [1.0] * C, pg, ps, cross, plan.n_cross, s, masked_outs=outs)
 
     t = timeit(fused_wire)
-    res.update({"fused_wire_images_ms": t * 1e3, "fused_wire_images_grad_elems_per_s": C * N / t})
+    res.update({"fused_wire_images_ms": t * 1e3, "fused_wire_images_grad_elems_per_s": C * N / t,
+                "fused_wire_images_algorithmic_GBps": (12 * C * N + 8 * N) / t / 1e9})
 
     # ---- host-resident, overlapped
     host_x = torch.stack([x.cpu() for x in xs]).pin_memory()        # [C, N] fp32
