@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--shapes", default="8:1,8:2,8:4,8:8", help="C:W pairs")
+    ap.add_argument("--bipartite", action="store_true",
+                    help="also time one sa_fused_bipartite launch (16 cross pairs of two quads, masks only, "
+                         "accumulating into the sum: 16 B of HBM traffic per element)")
     ap.add_argument("--calib", type=int, default=0,
                     help="also launch sa_sum_u64 over this many u64 inputs (known bytes, for PMC calibration)")
     args = ap.parse_args()
@@ -60,6 +63,35 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             cs["times"].append(e0.elapsed_time(e1) / args.reps)
+    bip = None
+    if args.bipartite:
+        import ctypes as C
+
+        from sfl_amd import _lib as L
+
+        clients = (L.LocalClient * 8)()
+        for c in range(8):
+            clients[c].x, clients[c].weight, clients[c].masked_out = None, 1.0, None
+        gens = (L.PCG64 * 16)(*[L.pcg64_from_seed(pair_seed(p // 4, 4 + p % 4)) for p in range(16)])
+        signs = (C.c_int8 * 16)(*([1] * 16))
+        sb = torch.zeros(N, dtype=torch.int64, device=dev)
+
+        def run_bip():
+            L.check(L.lib().sa_fused_bipartite(clients, L.SA_F32, N, 18, gens, signs, C.c_void_p(sb.data_ptr()), 1,
+                                               None, C.c_void_p(torch.cuda.current_stream().cuda_stream)), "bip")
+        times = []
+        for _ in range(args.rounds):
+            run_bip()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                run_bip()
+            e1.record()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) / args.reps)
+        t = sorted(times)[len(times) // 2]
+        bip = {"kernel": "k_clients<float, float, 8, 0, 1> (sa_fused_bipartite)", "ms_median": t,
+               "pair_draws_per_s": 16 * N / (t / 1e3), "hbm_GBps": 16 * N / (t / 1e3) / 1e9}
     if args.calib:
         ins = [torch.randint(0, 1 << 62, (N,), device=dev) for _ in range(args.calib)]
         so = torch.empty(N, dtype=torch.int64, device=dev)
@@ -75,7 +107,10 @@ def main():
         out.append({"C": cs["C"], "W": cs["W"], "L": cs["L"], "ms_median": ms, "ms_min": t[0],
                     "draws_per_s": draws / (ms / 1e3), "local_grad_elems_per_s": cs["L"] * N / (ms / 1e3),
                     "hbm_GBps": (4 * cs["L"] * N + 8 * N) / (ms / 1e3) / 1e9})
-    print(json.dumps({"lib": os.environ.get("SFL_SA_LIB", "default"), "elems": N, "cases": out}))
+    res = {"lib": os.environ.get("SFL_SA_LIB", "default"), "elems": N, "cases": out}
+    if bip:
+        res["bipartite"] = bip
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":
