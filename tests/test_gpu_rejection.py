@@ -185,3 +185,35 @@ def test_layers_after_a_rejection_use_shifted_positions():
     for c in range(len(NAMES)):
         img = np.concatenate([agg.last_masked[li][c].cpu().numpy().view(np.uint64) for li in range(2)])
         assert np.array_equal(img, masked[c])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("host", [False, True])
+def test_many_parties_rejection_replays_per_party(host):
+    """10 co-located parties (the pair-shared many-client schedule): a raw 0
+    on the (p03, p08) stream -- a pair drawn in a bipartite launch -- flags
+    the round, which is replayed on the per-party path with numpy's
+    rejection; this round and the next equal numpy's bit for bit, and the
+    pair's position runs one raw draw ahead."""
+    _gpu()
+    from sfl_amd.device import PYU, reveal
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    names = [f"p{c:02d}" for c in range(10)]
+    seeds = o.seeds_for(names)
+    pair = {(a, b): seeds[a][b] for a in names for b in names if a < b}
+    pair[("p03", "p08")] = forced_zero_state(777)
+    n = 2001
+    pyus = [PYU(nm, 0) for nm in names]
+    agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
+    ora = o.OracleMaskers(names, pair)
+    rng = np.random.default_rng(12)
+    for rnd in range(2):
+        xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in names]
+        objs = [p(lambda x=x: x if host else torch.from_numpy(x).cuda())() for p, x in zip(pyus, xs)]
+        got = reveal(agg.sum(objs, axis=0))
+        got = got.cpu().numpy() if isinstance(got, torch.Tensor) else got
+        _, ssum = ora.round(xs)
+        assert np.array_equal(got, o.decode(ssum)), (host, rnd)
+    assert agg._maskers["p03"].position("p08") == 2 * n + 1
+    assert agg._maskers["p00"].position("p01") == 2 * n
