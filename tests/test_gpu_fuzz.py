@@ -181,3 +181,43 @@ def test_fused_launch_random_shapes_match_oracle(seed):
     if want_dig:
         assert [int(v) for v in K.as_u64(dig)] == [o.digest(masked[u]) for u in local], ctx
     assert int(flags.item()) == 0
+
+
+N_MANY_CASES = 24
+
+
+@pytest.mark.parametrize("seed", range(N_MANY_CASES))
+def test_many_clients_random_cases_match_oracle(seed):
+    """The pair-shared many-client schedule (kernels.fused_many) on random
+    shapes: 9..40 co-located clients (short last quads and groups included),
+    random n, stream offsets up to 2^50, python-int weights, random names
+    (mixed pair signs), sum written or accumulated: equal to the oracle's
+    server sum bit for bit, and to the per-client path."""
+    from sfl_amd import _lib as L
+    from sfl_amd import kernels as K
+
+    rng = np.random.default_rng(5000 + seed)
+    C = int(rng.integers(9, 41))
+    n = int(rng.integers(1, 50_000))
+    offset = int(rng.integers(0, 1 << 50))
+    names = [f"n{int(v):05d}" for v in rng.permutation(100_000)[:C]]
+    seeds = o.seeds_for(names)
+    w = [int(v) for v in rng.integers(1, 50, C)]
+    xs = [(rng.standard_normal(n) * 0.05).astype(np.float32) for _ in range(C)]
+    pg, ps = [], []
+    for u in range(C):
+        for v in range(u + 1, C):
+            pg.append(L.pcg64_advance(L.pcg64_from_seed(seeds[names[u]][names[v]]), offset))
+            ps.append(1 if names[v] > names[u] else -1)
+    exp = o.server_sum(o.secure_masked(xs, names, weights=w, seeds=seeds, offset=offset))
+    dev = torch.device("cuda", 0)
+    xt = [torch.from_numpy(x).to(dev) for x in xs]
+    accumulate = bool(rng.integers(0, 2))
+    base = rng.integers(0, 2**64 - 1, n, dtype=np.uint64) if accumulate else np.zeros(n, dtype=np.uint64)
+    s = torch.from_numpy(base.view(np.int64).copy()).to(dev)
+    K.fused_many(xt, [float(v) for v in w], pg, ps, s, accumulate=accumulate)
+    s2 = torch.empty(n, dtype=torch.int64, device=dev)
+    K.fused_clients(xt, [float(v) for v in w], pg, ps, [], 0, s2, digests=torch.zeros(C, dtype=torch.int64, device=dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(K.as_u64(s), base + exp), (C, n)
+    assert np.array_equal(K.as_u64(s2), exp), (C, n)
