@@ -97,6 +97,11 @@ class SecureAggregator(Aggregator):
         keep_masked: also materialise every party's masked vector (the wire
             image) and expose the last ones as ``last_masked``; co-located
             parties still take the fused launch, which stores the images.
+
+    ``last_digests``: per launch group of the last aggregation, the XOR
+    digest of every party's masked vector (a checksum the tests pin) -- None
+    for a group of more co-located parties than one launch holds, whose
+    pair-shared schedule forms only the masked sum.
     """
 
     def __init__(self, device: PYU, participants: List[PYU], fxp_bits: int = 18, *,
