@@ -203,7 +203,11 @@ int sa_mask_impl(const void* x, int x_type, int compute_type, uint64_t n, double
       a.dp_block0 = dp->counter0 / 4;
     }
     const int ct = compute_type;
-    LaunchFn fn = find_clients_kernel(x_type, ct, 1, cnt);
+    // the lean single-client kernel unless a general path is needed
+    // (continue mode, per-element weights, DP): float32 kernels only
+    LaunchFn fn = (!a.continue_mode && !weight_vec && !dp) ? find_clients_kernel(x_type, ct, 1, cnt, kLean1)
+                                                           : nullptr;
+    if (!fn) fn = find_clients_kernel(x_type, ct, 1, cnt);
     if (!fn) {
       sa_set_error("sa_mask: no kernel for x_type=%d compute_type=%d streams=%d", x_type, ct, cnt);
       return SA_ERR_UNSUPPORTED;
@@ -293,7 +297,9 @@ extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, i
   a.digests = digests;
   a.do_digest = digests ? 1 : 0;
   a.flags = flags;
-  LaunchFn fn = find_clients_kernel(x_type, x_type, L, n_cross);
+  // one client: the lean kernel (a fused launch never uses the general paths)
+  LaunchFn fn = L == 1 ? find_clients_kernel(x_type, x_type, 1, n_cross, kLean1) : nullptr;
+  if (!fn) fn = find_clients_kernel(x_type, x_type, L, n_cross);
   if (!fn) {
     sa_set_error("sa_fused_clients: no kernel for x_type=%d clients=%d cross=%d", x_type, L,
                  n_cross);
@@ -351,7 +357,7 @@ extern "C" int sa_fused_bipartite(const sa_local_client* clients, int x_type, ui
   a.sum_out = sum_out;
   a.sum_mode = accumulate ? 2 : 1;
   a.flags = flags;
-  LaunchFn fn = find_clients_kernel(x_type, x_type, L, 0, 1);
+  LaunchFn fn = find_clients_kernel(x_type, x_type, L, 0, kBipartite);
   if (!fn) {
     sa_set_error("sa_fused_bipartite: no kernel for x_type=%d", x_type);
     return SA_ERR_UNSUPPORTED;

@@ -10,6 +10,7 @@ namespace sa {
 LaunchFn find_other_kernel(int xt, int ct, int L, int X);
 
 #define F32(L, X) SA_ENTRY(float, float, SA_F32, SA_F32, L, X)
+#define L1(X) SA_ENTRY_K(float, float, SA_F32, SA_F32, 1, X, kLean1)
 LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K) {
   static const KernelEntry kEntriesF32[] = {
     F32(1, 0),  F32(1, 1),  F32(1, 2),  F32(1, 3),  F32(1, 4),  F32(1, 5),  F32(1, 6),
@@ -22,12 +23,16 @@ LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K) {
     // the pair-shared schedule of more than 8 co-located clients: two quads'
     // 16 cross pairs per launch (sa_fused_bipartite)
     SA_ENTRY_K(float, float, SA_F32, SA_F32, 8, 0, kBipartite),
+    // one client without the general paths (continue, weight vectors, DP)
+    L1(0), L1(1), L1(2), L1(3), L1(4), L1(5), L1(6), L1(7), L1(8), L1(9), L1(10), L1(11), L1(12),
+    L1(13), L1(14), L1(15), L1(16),
   };
   for (const KernelEntry& e : kEntriesF32)
     if (e.xt == xt && e.ct == ct && e.L == L && e.X == X && e.K == K) return e.fn;
   return K == kAllPairs ? find_other_kernel(xt, ct, L, X) : nullptr;
 }
 #undef F32
+#undef L1
 
 }  // namespace sa
 

@@ -389,8 +389,6 @@ __device__ __forceinline__ void pcg_draw_one(uint32_t& s0, uint32_t& s1, uint32_
 // a < L/2 <= b, a-major -- one block of the pair-shared schedule for more
 // co-located clients than one launch holds (kernels.fused_many: the quads
 // of clients pairwise, each pair stream still expanded exactly once).
-constexpr int kAllPairs = 0;
-constexpr int kBipartite = 1;
 template <int L, int K = kAllPairs>
 struct Pairs {
   static constexpr int H = L / 2;
@@ -586,7 +584,9 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
     k_clients(const KArgs a) {
   constexpr int PI = Pairs<L, K>::count;
   constexpr int P = PI + L * X;
-  constexpr bool kGeneral = (L == 1);  // continue mode + per-element weights + DP
+  // the single-client kernel's general paths: continue mode + per-element
+  // weights + DP (kLean1: the same single client without them)
+  constexpr bool kGeneral = (L == 1) && K != kLean1;
   static_assert(L >= 1 && L <= kMaxLocal, "L");
   static_assert(P <= kMaxStreams, "P");
 

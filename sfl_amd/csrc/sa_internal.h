@@ -27,6 +27,19 @@ constexpr int kMaxStreams = 32;  // mask streams per launch (kernel-arg resident
 constexpr int kMaskPass = 16;    // streams per pass of the single-client kernel
 constexpr int kBipartiteClients = 8;  // sa_fused_bipartite: two quads, their 16 cross pairs
 
+// Pair set / variant of a masking-kernel instantiation (k_clients' K): every
+// internal pair of its L clients; the pairs between the lower and the upper
+// half (sa_fused_bipartite); or one client without the general paths.
+constexpr int kAllPairs = 0;
+constexpr int kBipartite = 1;
+// kLean1: one client (L = 1) without the general single-client paths
+// (continue mode, per-element weights, the DP pre-step): the fused per-rank
+// shape <1, X> and first-pass sa_mask of float32 data with a scalar weight;
+// 76 instead of 81 VGPRs for 7 streams and ~8 % less time per launch
+// (profiles/r02/ab_lean1_kb.jsonl).  Pairs: as kAllPairs (none for L = 1).
+constexpr int kLean1 = 2;
+
+
 // Kernel-argument image (lives in the kernarg segment; read with scalar loads).
 struct StreamArg {
   uint64_t s_lo, s_hi;      // generator state before draw 0 of this call
@@ -82,6 +95,6 @@ typedef int (*LaunchFn)(const KArgs& a, void* stream);
 // Returns the launcher for (xt, ct, L, X) or nullptr when not instantiated.
 // K: pair set of the launch (0: every internal pair of the L clients; 1:
 // bipartite, the pairs between the lower and upper half -- sa_fused_bipartite)
-LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K = 0);
+LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K = kAllPairs);
 
 }  // namespace sa

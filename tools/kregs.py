@@ -16,6 +16,6 @@ for path in sys.argv[1:]:
             cur[m.group(1)] = int(m.group(2))
             if m.group(1) == "vgpr_spill_count":
                 n = re.search(r"k_clientsI(\w+?)Li(\d+)ELi(\d+)E(?:Li(\d+)E)?", cur["name"])
-                tag = f"{n.group(1)} L={n.group(2)} X={n.group(3)}" + (" K=1" if n.group(4) == "1" else "") if n else cur["name"]
+                tag = f"{n.group(1)} L={n.group(2)} X={n.group(3)}" + (f" K={n.group(4)}" if n.group(4) not in (None, "0") else "") if n else cur["name"]
                 print(f"{tag:22s} vgpr={cur.get('vgpr_count'):4d} vspill={cur['vgpr_spill_count']:3d} "
                       f"sgpr={cur.get('sgpr_count'):3d} sspill={cur.get('sgpr_spill_count')}")

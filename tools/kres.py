@@ -16,5 +16,5 @@ for line in sys.stdin:
 for r in rows:
     n = r["name"]
     m = re.search(r"k_clientsI(\w+?)Li(\d+)ELi(\d+)E(?:Li(\d+)E)?", n)
-    tag = f"{m.group(1)} L={m.group(2)} X={m.group(3)}" + (" K=1" if m.group(4) == "1" else "") if m else n
+    tag = f"{m.group(1)} L={m.group(2)} X={m.group(3)}" + (f" K={m.group(4)}" if m.group(4) not in (None, "0") else "") if m else n
     print(f"{tag:28s} vgpr={r.get('VGPRs')} vspill={r.get('VGPRsSpill')} sspill={r.get('SGPRsSpill')} scratch={r.get('ScratchSize')} occ={r.get('Occupancy')}")
