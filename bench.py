@@ -176,9 +176,9 @@ def pmc_traffic(kernel: str, elems_per_launch: int) -> dict | None:
     import csv
     import re
 
-    def shape(name):  # (L, X, K) of a k_clients kernel name (K, the pair set, was added in round 2)
+    def shape(name):  # (L, X) of a k_clients kernel name; its variant K moves the same bytes
         m = re.search(r"k_clients<float, float, (\d+), (\d+)(?:, (\d+))?>", name)
-        return (int(m.group(1)), int(m.group(2)), int(m.group(3) or 0)) if m else None
+        return (int(m.group(1)), int(m.group(2))) if m else None
 
     want = shape(kernel)
     for d in PMC_DIRS:
@@ -200,6 +200,19 @@ def pmc_traffic(kernel: str, elems_per_launch: int) -> dict | None:
                     "source": os.path.relpath(d, ROOT) + "/pmc_{fetch,write}_size.csv",
                     "scaled_from_elems": PMC_ELEMS}
     return None
+
+
+# k_clients' variant flags (sfl_amd/csrc/sa_internal.h): the instantiation a
+# fused launch takes, as sa_fused_clients dispatches it
+K_LEAN1, K_SUM_ONLY = 2, 4
+SUM_ONLY_SHAPES = {(2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (4, 4), (2, 6), (2, 2), (1, 1), (1, 3), (1, 7)}
+
+
+def kernel_variant(L: int, X: int, digests: bool) -> int:
+    lean = K_LEAN1 if L == 1 else 0
+    if not digests and (L, X) in SUM_ONLY_SHAPES:
+        return lean | K_SUM_ONLY
+    return lean
 
 
 def _free_port() -> int:
@@ -508,7 +521,7 @@ def main():
     bytes_alg = 4 * Lc * n_loc + 8 * n_loc  # per step: fp32 reads of the local clients + one u64 sum write
     launches = len(pipe.bounds)
     achieved = bytes_alg / (kern_ms / 1e3) / 1e9
-    kname = f"k_clients<float, float, {Lc}, {plan.n_cross}, 0>"  # the launch's kernel (K = 0: all pairs)
+    kname = f"k_clients<float, float, {Lc}, {plan.n_cross}, {kernel_variant(Lc, plan.n_cross, args.digests)}>"
     n_streams = len(plan.pairs) + len(plan.cross)
     fused = Lc <= 8 and n_streams <= 32  # sa_fused_clients' limits (kMaxLocal, kMaxStreams)
     if not fused and Lc > 8 and plan.n_cross == 0 and not args.digests:  # kernels.fused_many

@@ -297,8 +297,13 @@ extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, i
   a.digests = digests;
   a.do_digest = digests ? 1 : 0;
   a.flags = flags;
-  // one client: the lean kernel (a fused launch never uses the general paths)
-  LaunchFn fn = L == 1 ? find_clients_kernel(x_type, x_type, 1, n_cross, kLean1) : nullptr;
+  // one client: the lean kernel (a fused launch never uses the general
+  // paths); only the sum wanted: the sum-only instantiation where there is one
+  bool any_out = digests != nullptr;
+  for (int c = 0; c < L; c++) any_out = any_out || clients[c].masked_out != nullptr;
+  const int lean = L == 1 ? kLean1 : 0;
+  LaunchFn fn = any_out ? nullptr : find_clients_kernel(x_type, x_type, L, n_cross, lean | kSumOnly);
+  if (!fn && lean) fn = find_clients_kernel(x_type, x_type, 1, n_cross, kLean1);
   if (!fn) fn = find_clients_kernel(x_type, x_type, L, n_cross);
   if (!fn) {
     sa_set_error("sa_fused_clients: no kernel for x_type=%d clients=%d cross=%d", x_type, L,

@@ -11,6 +11,7 @@ LaunchFn find_other_kernel(int xt, int ct, int L, int X);
 
 #define F32(L, X) SA_ENTRY(float, float, SA_F32, SA_F32, L, X)
 #define L1(X) SA_ENTRY_K(float, float, SA_F32, SA_F32, 1, X, kLean1)
+#define SO(L, X) SA_ENTRY_K(float, float, SA_F32, SA_F32, L, X, kSumOnly)
 LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K) {
   static const KernelEntry kEntriesF32[] = {
     F32(1, 0),  F32(1, 1),  F32(1, 2),  F32(1, 3),  F32(1, 4),  F32(1, 5),  F32(1, 6),
@@ -23,6 +24,12 @@ LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K) {
     // the pair-shared schedule of more than 8 co-located clients: two quads'
     // 16 cross pairs per launch (sa_fused_bipartite)
     SA_ENTRY_K(float, float, SA_F32, SA_F32, 8, 0, kBipartite),
+    // sum-only fused launches (no digests / wire images): the co-located and
+    // per-rank shapes above
+    SO(2, 0), SO(3, 0), SO(4, 0), SO(5, 0), SO(6, 0), SO(7, 0), SO(8, 0), SO(4, 4), SO(2, 6), SO(2, 2),
+    SA_ENTRY_K(float, float, SA_F32, SA_F32, 1, 1, kLean1 | kSumOnly),
+    SA_ENTRY_K(float, float, SA_F32, SA_F32, 1, 3, kLean1 | kSumOnly),
+    SA_ENTRY_K(float, float, SA_F32, SA_F32, 1, 7, kLean1 | kSumOnly),
     // one client without the general paths (continue, weight vectors, DP)
     L1(0), L1(1), L1(2), L1(3), L1(4), L1(5), L1(6), L1(7), L1(8), L1(9), L1(10), L1(11), L1(12),
     L1(13), L1(14), L1(15), L1(16),
@@ -33,6 +40,7 @@ LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K) {
 }
 #undef F32
 #undef L1
+#undef SO
 
 }  // namespace sa
 

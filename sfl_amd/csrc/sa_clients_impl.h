@@ -392,9 +392,10 @@ __device__ __forceinline__ void pcg_draw_one(uint32_t& s0, uint32_t& s1, uint32_
 template <int L, int K = kAllPairs>
 struct Pairs {
   static constexpr int H = L / 2;
-  static constexpr int count = K == kBipartite ? H * (L - H) : L * (L - 1) / 2;
+  static constexpr bool kBip = (K & kBipartite) != 0;
+  static constexpr int count = kBip ? H * (L - H) : L * (L - 1) / 2;
   static constexpr int u(int p) {
-    if (K == kBipartite) return p / (L - H);
+    if (kBip) return p / (L - H);
     int k = p;
     for (int a = 0; a < L; a++) {
       const int row = L - 1 - a;
@@ -404,7 +405,7 @@ struct Pairs {
     return -1;
   }
   static constexpr int v(int p) {
-    if (K == kBipartite) return H + p % (L - H);
+    if (kBip) return H + p % (L - H);
     int k = p;
     for (int a = 0; a < L; a++) {
       const int row = L - 1 - a;
@@ -586,7 +587,10 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
   constexpr int P = PI + L * X;
   // the single-client kernel's general paths: continue mode + per-element
   // weights + DP (kLean1: the same single client without them)
-  constexpr bool kGeneral = (L == 1) && K != kLean1;
+  constexpr bool kGeneral = (L == 1) && !(K & kLean1);
+  // only the masked sum leaves the launch (no digests, no wire images): the
+  // finish and epilogue carry no digest / store code at all
+  constexpr bool kSum = (K & (kSumOnly | kBipartite)) != 0;
   static_assert(L >= 1 && L <= kMaxLocal, "L");
   static_assert(P <= kMaxStreams, "P");
 
@@ -703,7 +707,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
         if (SA_ABLATE & 8) {
 #pragma unroll
           for (int k = 0; k < kE; k++) xv[c].v[k] = (XT)(int)(i + k + c);
-        } else if constexpr (K == kBipartite) {  // masks only: the clients' values enter elsewhere
+        } else if constexpr ((K & kBipartite) != 0) {  // masks only: the clients' values enter elsewhere
           xv[c].v[0] = xv[c].v[1] = (XT)0;
         } else {
           xv[c] = bload2<XT>(make_rsrc(ka->c[c].x, cont ? 0 : n * sizeof(XT)), i);
@@ -820,11 +824,11 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
     const QScale qs{ka->scale_f, ka->scale_d, ka->fxp_bits};
     // elements past n only occur in the wave's last tile (uniform test)
     const bool wave_full = base + wave_off + 64 * kE <= n;
-    const uint32_t mmask = ka->masked_mask;
+    const uint32_t mmask = kSum ? 0u : ka->masked_mask;
     // per-client XOR digests only when the caller asked for them (a
     // checksum for tests and the wire path, not part of the reference's
     // arithmetic): one wave-uniform branch per tile
-    const bool dig_on = ka->do_digest;
+    const bool dig_on = kSum ? false : (bool)ka->do_digest;
     uint64_t sum[kE] = {0, 0};
     auto finish = [&](int c, uint64_t q0, uint64_t q1) {
       const uint64_t a0 = negated<L>(c) ? q0 - acc[0][c] : acc[0][c] + q0;
@@ -842,7 +846,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
     };
     static_assert(kE == 2, "finish() takes the lane's two elements");
     float p[L][kE];
-    if constexpr (K == kBipartite) {
+    if constexpr ((K & kBipartite) != 0) {
       // masks only (sa_fused_bipartite): the sum of the 8 accumulators, the
       // upper quad's stored negated
 #pragma unroll
@@ -917,7 +921,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
   // through LDS, one 64-bit atomic per client per BLOCK.  Every wave ends at
   // about the same time, so per-wave atomics on the same L clients' words
   // serialised at the L2: ~2,000 per address cost ~0.13 ms per launch.
-  if (a.do_digest) {
+  if (!kSum && a.do_digest) {
     __shared__ uint64_t wdig[kBlockThreads / 64][L];
 #pragma unroll
     for (int c = 0; c < L; c++) {

@@ -38,6 +38,12 @@ constexpr int kBipartite = 1;
 // 76 instead of 81 VGPRs for 7 streams and ~8 % less time per launch
 // (profiles/r02/ab_lean1_kb.jsonl).  Pairs: as kAllPairs (none for L = 1).
 constexpr int kLean1 = 2;
+// kSumOnly: only the masked sum leaves the launch (no per-client digests, no
+// wire images): the same arithmetic without the digest / store code; the
+// fused launches of the benches and of the many-client schedule.  8-client
+// launch -1.25 % in A/B (profiles/r02/ab_sum_only_kernel_kb.jsonl).  Flags
+// combine (kLean1 | kSumOnly); kBipartite launches are masks-only sums.
+constexpr int kSumOnly = 4;
 
 
 // Kernel-argument image (lives in the kernarg segment; read with scalar loads).
