@@ -354,10 +354,13 @@ class FLModel:
         for d, w in self._workers.items():
             w.set_data(x[d], y[d], batch_size)
         steps = max(w.steps_per_epoch() for w in self._workers.values())
-        history = {"train_loss": [], "val_loss": [], "val_accuracy": [], "aggregation_s": [], "round_s": []}
+        history = {"train_loss": [], "val_loss": [], "val_accuracy": [], "aggregation_s": [], "round_s": [],
+                   "init_s": 0.0, "eval_s": 0.0}
         # reference fit (fl_model.py:473): the initial weights are averaged
         # through the aggregator before the first epoch
+        t_init = time.perf_counter()
         init = self.initialize_weights()
+        history["init_s"] = time.perf_counter() - t_init
         if round_hook is not None:
             round_hook(-1, reveal(init))
         rnd = 0
@@ -388,7 +391,9 @@ class FLModel:
                 w.apply_weights(reveal(model_params_list[idx]))
             history["train_loss"].append(float(np.mean([w.last_loss for w in self._workers.values()])))
             if validation_data is not None:
+                t_eval = time.perf_counter()
                 vl, va = self.evaluate(*validation_data)
+                history["eval_s"] += time.perf_counter() - t_eval
                 history["val_loss"].append(vl)
                 history["val_accuracy"].append(va)
         return history

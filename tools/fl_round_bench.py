@@ -46,7 +46,7 @@ def main():
                    aggregator=SecureAggregator(PYU("server", 0), pyus, seeds=pair), random_seed=1234,
                    train_device=args.train_device)
     warm.fit({p: x for p, x in zip(pyus, xs)}, {p: y for p, y in zip(pyus, ys)}, batch_size=32, epochs=1,
-             aggregate_freq=1)
+             aggregate_freq=1, validation_data=(np.concatenate(xs), np.concatenate(ys)))  # first evaluate too
     for label, agg in (("hip", SecureAggregator(PYU("server", 0), pyus, seeds=pair)),
                        ("oracle_numpy", T.OracleAggregator(names, seeds))):
         model = TorchModel(model_fn=T.MlpNet, loss_fn=torch.nn.CrossEntropyLoss,
@@ -64,6 +64,7 @@ def main():
                       "aggregation_ms_median": 1e3 * float(np.median(agg_s)),
                       "first_aggregations_ms": [1e3 * float(v) for v in h["aggregation_s"][:3]],
                       "outside_rounds_s": wall - float(np.sum(h["round_s"])),
+                      "init_average_s": h["init_s"], "evaluate_s": h["eval_s"],
                       "aggregation_share": float(np.sum(agg_s) / np.sum(h["round_s"][1:])),
                       "val_accuracy": h["val_accuracy"][-1]}
     n_params = sum(p.numel() for p in T.MlpNet().parameters())
