@@ -98,3 +98,21 @@ def test_many_client_workload_names_the_pair_shared_schedule():
     (line,) = _json_lines(r.stdout)
     assert "pair-shared schedule" in line["config"]["workload"] and "24 k_clients<float,float,8,0,1>" in \
         line["config"]["workload"]
+
+
+def test_bench_kernel_variant_table_matches_the_registry():
+    """bench.py names the k_clients instantiation a fused launch dispatches
+    (roofline.kernel); its table of sum-only shapes must be the registry's
+    (sfl_amd/csrc/sa_clients_f32.hip)."""
+    import re
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    src = open(os.path.join(ROOT, "sfl_amd", "csrc", "sa_clients_f32.hip")).read()
+    shapes = {(int(a), int(b)) for a, b in re.findall(r"\bSO\((\d+), (\d+)\)", src)}
+    shapes |= {(int(a), int(b)) for a, b in
+               re.findall(r"SA_ENTRY_K\(float, float, SA_F32, SA_F32, (\d+), (\d+), kLean1 \| kSumOnly\)", src)}
+    assert shapes == bench.SUM_ONLY_SHAPES
+    assert bench.kernel_variant(8, 0, False) == 4 and bench.kernel_variant(8, 0, True) == 0
+    assert bench.kernel_variant(1, 7, False) == 6 and bench.kernel_variant(1, 5, False) == 2
