@@ -12,14 +12,18 @@ N=1 (default): all 8 clients on one MI355X in ONE fused launch
 (sa_fused_clients: L=8 local clients, 28 pair streams each expanded once).
 N>1: one process per GPU, clients sharded in contiguous blocks (8/N per
 GPU, config 3 at N=8); each rank runs the fused masking over its clients
-(internal pairs + cross streams), pipelined in chunks against ncclReduce of
-the uint64 partial sums to rank 0 (the server) over xGMI.  Total work is
-fixed as N grows: "scaling": "strong".  `--exchange sharded` replaces the
-reduce with the sharded server of SURVEY.md §8(e) (ncclReduceScatter, every
-rank decodes its shard; `--gather` also gathers the float64 shards to rank 0).  `python bench.py --gpus N` starts
-its N rank processes itself (torch.distributed.run as a child process,
-before this process touches the GPU); under an outer torchrun (WORLD_SIZE
-set) it runs as one rank.
+(internal pairs + cross streams), pipelined in chunks against the exchange
+of the uint64 partial sums over xGMI.  `value` is measured on the sharded
+server (ncclReduceScatter in place, every rank decodes its
+shard of the masked sum); the same process group then times every other
+design (`exchange_variants`: the shards also gathered to rank 0, ncclReduce
+of the partial sums to rank 0, element sharding with and without the
+gather), so one run reports them all.  Total work is fixed as N grows:
+"scaling": "strong".  `python bench.py --gpus N` starts its N rank
+processes itself (torch.distributed.run as a child process with a c10d
+rendezvous on 127.0.0.1 port 0, before this process touches the GPU); under
+an outer torchrun (WORLD_SIZE set) it runs as one rank.  A rank still
+running after --watchdog-seconds (480) dumps every thread's stack and exits.
 
 Inputs: synthetic N(0, 0.01^2) fp32 gradients generated on the GPU
 (torch.Generator seeded 20260116+c); pair seeds (0x5ECA66<<32)|(u<<16)|v as
@@ -43,7 +47,7 @@ HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # PCG64 draw-loop ceilings (tools/microbench/draw_issue.hip,
 # profiles/r01/draw_issue_microbench.txt), the draw loop alone with the
 # product kernel's operand layout and schedule; the first is measured live on
-# the bench's own box when the tool is built (draw_loop_ceiling), this
+# the bench's own box when the tool is built (draw_loop_ceilings), this
 # constant is the fallback:
 PCG_PAIR_DRAWS_2WAVE = 1.34e12  # pair draws (both ends accumulated), 2 waves/SIMD = the L=8 kernel's
                                 # occupancy ("dual pair28 E2", best of 1.29-1.34e12 run to run)
@@ -160,27 +164,40 @@ def cpu_baseline_parallel(C: int, fxp_bits: int, n: int) -> dict:
             "seconds": round(t, 3)}
 
 
-PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r02", "r01")]  # newest first
+PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r03", "r02", "r01")]  # newest first
 PMC_ELEMS = 100_000_000  # element positions per launch of the committed PMC passes
 
 
-def pmc_traffic(kernel: str, elems_per_launch: int) -> dict | None:
+def kernel_key(name: str):
+    """The instantiation a PMC row belongs to: (L, X, K) of a k_clients kernel
+    (K, the variant flags of sa_internal.h, is 0 in round-1 names that carry
+    none), otherwise the bare kernel name.  The variant decides the bytes:
+    k_clients<8, 0, 1> (kBipartite, masks only) moves 16 B per element
+    position, k_clients<8, 0, 4> (kSumOnly) 40 B."""
+    import re
+
+    m = re.search(r"k_clients<float, float, (\d+), (\d+)(?:, (\d+))?>", name)
+    if m:
+        return ("k_clients", int(m.group(1)), int(m.group(2)), int(m.group(3) or 0))
+    name = name.strip()
+    if name.startswith("void "):
+        name = name[5:]
+    return name.split("(")[0].strip()
+
+
+def pmc_traffic(kernel: str, elems_per_launch: int, pmc_elems: int = PMC_ELEMS) -> dict | None:
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (tools/gpu_profile.sh: separate FETCH_SIZE / WRITE_SIZE runs of
     tools/kernel_bench.py, every per-rank shape at 100M element positions per
     launch), scaled to this run's launch size (the kernel streams: its bytes
-    are linear in the element count).  Units are KiB; gfx950 reports
-    FETCH_SIZE at half the bytes of 16-B/lane streaming reads, so it is
-    doubled (MI355X_MICROARCH.md, HBM); both corrections were checked on the
+    are linear in the element count).  Rows are matched on the kernel's full
+    instantiation (kernel_key).  Units are KiB; gfx950 reports FETCH_SIZE at
+    half the bytes of 16-B/lane streaming reads, so it is doubled
+    (MI355X_MICROARCH.md, HBM); both corrections were checked on the
     k_sum_u64 calibration launch in the same runs (known bytes)."""
     import csv
-    import re
 
-    def shape(name):  # (L, X) of a k_clients kernel name; its variant K moves the same bytes
-        m = re.search(r"k_clients<float, float, (\d+), (\d+)(?:, (\d+))?>", name)
-        return (int(m.group(1)), int(m.group(2))) if m else None
-
-    want = shape(kernel)
+    want = kernel_key(kernel)
     for d in PMC_DIRS:
         vals = {}
         for counter, fname, scale in (("FETCH_SIZE", "pmc_fetch_size.csv", 2.0),
@@ -190,16 +207,29 @@ def pmc_traffic(kernel: str, elems_per_launch: int) -> dict | None:
                 break
             with open(path) as f:
                 v = [float(r["Counter_Value"]) for r in csv.DictReader(f)
-                     if want is not None and shape(r["Kernel_Name"]) == want and r["Counter_Name"] == counter]
+                     if r["Counter_Name"] == counter and kernel_key(r["Kernel_Name"]) == want]
             if not v:
                 break
-            vals[counter] = scale * 1024.0 * sum(v) / len(v) * elems_per_launch / PMC_ELEMS
+            vals[counter] = scale * 1024.0 * sum(v) / len(v) * elems_per_launch / pmc_elems
         if len(vals) == 2:
             return {"bytes": vals["FETCH_SIZE"] + vals["WRITE_SIZE"], "read": vals["FETCH_SIZE"],
-                    "write": vals["WRITE_SIZE"],
+                    "write": vals["WRITE_SIZE"], "rows_matched": kernel_key(kernel),
                     "source": os.path.relpath(d, ROOT) + "/pmc_{fetch,write}_size.csv",
-                    "scaled_from_elems": PMC_ELEMS}
+                    "scaled_from_elems": pmc_elems}
     return None
+
+
+def traffic_field(pmc: dict | None, alg_bytes_per_launch: float):
+    """roofline.traffic from the PMC bytes: never a figure below the
+    algorithmic bytes without saying so (HBM traffic under the bytes the
+    launch must move means the rows belong to another kernel, or the
+    kernel skipped work) -- such a figure is withheld (None) with a note."""
+    if pmc is None:
+        return None, None
+    if pmc["bytes"] < 0.98 * alg_bytes_per_launch:
+        return None, dict(pmc, note=f"PMC bytes {pmc['bytes']:.4g} below the algorithmic "
+                                    f"{alg_bytes_per_launch:.4g} B per launch: withheld")
+    return pmc["bytes"], pmc
 
 
 # k_clients' variant flags (sfl_amd/csrc/sa_internal.h): the instantiation a
@@ -215,22 +245,61 @@ def kernel_variant(L: int, X: int, digests: bool) -> int:
     return lean
 
 
-def _free_port() -> int:
-    import socket
+# ---------------------------------------------------------------- N > 1 designs
+#
+# Every N > 1 run measures ALL of these in one process group (the headline
+# first, with --steps; the rest with --variant-steps), so one driver run of
+# `bench.py --gpus N` reports each exchange design:
+#   sharded          client sharding, every chunk's uint64 partial sum
+#                    ncclReduceScatter'ed in place, each rank decodes its shard
+#                    (the sharded server) -- the default
+#   sharded+gather   ... and the float64 shards gathered to rank 0
+#   reduce           client sharding, ncclReduce of the partial sums to rank 0
+#   elements         element sharding: every rank masks 1/N of EVERY client's
+#                    elements, no exchange for the sum (not config 3: a
+#                    client's raw gradient on every GPU), decodes its slice
+#   elements+gather  ... and the float64 slices gathered to rank 0
+VARIANTS = ("sharded", "sharded+gather", "reduce", "elements", "elements+gather")
 
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+
+class Variant:
+    def __init__(self, name: str):
+        if name not in VARIANTS and name != "local":
+            raise ValueError(f"unknown exchange variant {name!r}")
+        self.name = name
+        self.shard = "elements" if name.startswith("elements") else "clients"
+        self.exchange = name.split("+")[0] if self.shard == "clients" and name != "local" else None
+        self.gather = name.endswith("+gather")
+
+
+def headline_variant(args, multi: bool) -> Variant:
+    """The design `value` is measured on: one fused launch at N = 1; at N > 1
+    (or --dist) the one the flags name, the sharded server by default."""
+    if not multi:
+        return Variant("local")
+    if args.shard == "elements":
+        return Variant("elements+gather" if args.gather else "elements")
+    ex = args.exchange or "sharded"
+    return Variant("sharded+gather" if ex == "sharded" and args.gather else ex)
+
+
+def other_variants(args, head: Variant) -> list[Variant]:
+    if args.variants == "none":
+        return []
+    names = VARIANTS if args.variants == "all" else tuple(v for v in args.variants.split(",") if v)
+    return [Variant(v) for v in names if v != head.name]
 
 
 def launch_ranks(args) -> int:
     """`--gpus N` without an outer torchrun (WORLD_SIZE unset): measure the CPU
     baseline here, then start the N rank processes as ONE child process
-    (torch.distributed.run, rendezvous on 127.0.0.1) and return its exit
-    code.  This process never touches the GPU (it imports no torch), so
-    nothing is exec'd from a process that initialised HIP."""
+    (torch.distributed.run with a c10d rendezvous on 127.0.0.1 port 0: the
+    store binds a port the kernel picks, no probe-then-bind race) and return
+    its exit code.  This process never touches the GPU (it imports no torch),
+    so nothing is exec'd from a process that initialised HIP."""
     import subprocess
     import tempfile
+    import uuid
 
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -243,8 +312,8 @@ def launch_ranks(args) -> int:
             json.dump(cpu, f)
         env["SFL_BENCH_CPU_BASELINE"] = tmp
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
-           *sys.argv[1:]]
+           "--rdzv-backend", "c10d", "--rdzv-endpoint", "127.0.0.1:0", "--rdzv-id", f"sfl-bench-{uuid.uuid4().hex}",
+           "--local-addr", "127.0.0.1", os.path.abspath(__file__), *sys.argv[1:]]
     try:
         return subprocess.run(cmd, env=env).returncode
     finally:
@@ -252,24 +321,39 @@ def launch_ranks(args) -> int:
             os.unlink(tmp)
 
 
-def draw_loop_ceiling() -> dict | None:
-    """The PCG64 draw loop alone with the 8-client kernel's operand layout,
-    schedule and occupancy (tools/microbench/draw_issue, "dual pair28 E2" at
-    2 waves/SIMD: median of 15 launches after 40 warm-up ones), measured on THIS box in a child
-    process before this process touches the GPU, so roofline.valu compares
-    the kernel with a same-box ceiling (boards differ by a few % in clock
-    under the power limit).  None if the tool is missing or fails."""
+def _draw_issue(case: str, waves: int, local_rank: int | None) -> dict | None:
     import subprocess
 
     exe = os.path.join(ROOT, "tools", "microbench", "draw_issue")
     if not os.path.exists(exe):
         return None
+    env = dict(os.environ)
+    if local_rank is not None:  # this rank's GPU only (an index into the visible list)
+        vis = [v for v in env.get("HIP_VISIBLE_DEVICES", "").split(",") if v]
+        env["HIP_VISIBLE_DEVICES"] = vis[local_rank] if local_rank < len(vis) else str(local_rank)
     try:
-        r = subprocess.run([exe, "dual pair28 E2", "2"], capture_output=True, text=True, timeout=120)
+        r = subprocess.run([exe, case, str(waves)], capture_output=True, text=True, timeout=120, env=env)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
         return json.loads(line)
     except (subprocess.SubprocessError, IndexError, ValueError, OSError):
         return None
+
+
+def draw_loop_ceilings(local_rank: int | None = None) -> dict:
+    """The PCG64 draw loop alone with the masking kernel's operand layout and
+    schedule (tools/microbench/draw_issue: median of 15 launches after 40
+    warm-up ones), measured on THIS rank's GPU in a child process before this
+    process touches the GPU, so roofline.valu compares the kernel with a
+    same-box ceiling (boards differ by a few % in clock under the power
+    limit): pair draws ("dual pair28 E2" at the 8-client kernel's 2
+    waves/SIMD) and one-sided draws ("dual one7 E2" at 8 waves/SIMD, the
+    cross streams' kind).  Missing entries if the tool is absent or fails."""
+    out = {}
+    for kind, case, w in (("pair", "dual pair28 E2", 2), ("one", "dual one7 E2", 8)):
+        r = _draw_issue(case, w, local_rank)
+        if r:
+            out[kind] = r
+    return out
 
 
 def rank_cpu_seconds(args, world: int) -> float:
@@ -292,38 +376,46 @@ def rank_cpu_baseline(args, world: int, rank: int):
 
 def dry_run(args, world: int, rank: int, cpu) -> None:
     """Launcher rehearsal without a GPU (tests/test_bench_launcher.py): every
-    rank joins a gloo group and reports its pid; rank 0 prints one line."""
+    rank joins a gloo group and reports its pid; rank 0 prints one line
+    naming the headline design and every variant the GPU run would time."""
     import torch.distributed as dist
 
     multi = world > 1 or args.dist
-    ranks = [{"rank": rank, "pid": os.getpid(), "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}]
+    ranks = [{"rank": rank, "pid": os.getpid(), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+              "master_port": os.environ.get("MASTER_PORT")}]
     if multi:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         allr = [None] * world
         dist.all_gather_object(allr, ranks[0])
         ranks = allr
         dist.destroy_process_group()
+    head = headline_variant(args, multi)
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "dry_run": True, "n_gpus": world, "ranks": ranks,
-                          "config": {"workload": workload(args, world)}, "cpu_baseline": cpu}), flush=True)
+        line = {"metric": METRIC, "value": None, "dry_run": True, "n_gpus": world, "ranks": ranks,
+                "config": {"workload": workload(args, world, head)}, "cpu_baseline": cpu,
+                "watchdog_seconds": args.watchdog_seconds}
+        if multi:
+            line["exchange_variants"] = [{"name": v.name, "workload": workload(args, world, v)}
+                                         for v in [head, *other_variants(args, head)]]
+        print(json.dumps(line), flush=True)
 
 
 METRIC = "grad elems/s device-resident: 100M-float quantize+mask+sum, 8 clients"
 
 
-def workload(args, world: int) -> str:
+def workload(args, world: int, v: Variant) -> str:
     from sfl_amd.parallel_sum import client_shard
 
     C, N = args.clients, args.elems
-    if (world > 1 or args.dist) and args.shard == "elements":
+    if v.shard == "elements":
         return (f"{C} clients x {N} fp32 grad elems over {world} GPUs, element-sharded: every rank masks its "
                 f"1/{world} of every client's elements in one fused launch k_clients<float,float,{C},0> "
                 f"({C * (C - 1) // 2} pair streams jumped to the slice start), decodes its slice of the sum"
-                + (", float64 slices gathered to rank 0" if args.gather else ""))
+                + (", float64 slices gathered to rank 0" if v.gather else ""))
     L = len(client_shard(C, world, 0))
     X = C - L
     pairs = L * (L - 1) // 2
-    if world == 1:
+    if world == 1 and v.name == "local":
         if L > 8 and X == 0 and not args.digests:  # the pair-shared multi-launch schedule
             from sfl_amd.kernels import many_schedule
 
@@ -343,8 +435,159 @@ def workload(args, world: int) -> str:
             f"{L} local client(s), {pairs} internal pair + {L * X} cross streams "
             f"(k_clients<float,float,{L},{X}>), pipelined " +
             ("ncclReduceScatter(uint64) of the partial sum, each rank decoding its shard (sharded server)"
-             + (" and gathering the float64 shards to rank 0" if args.gather else "")
-             if args.exchange == "sharded" else "ncclReduce(uint64) of the partial sum to rank 0"))
+             + (" and gathering the float64 shards to rank 0" if v.gather else "")
+             if v.exchange == "sharded" else "ncclReduce(uint64) of the partial sum to rank 0"))
+
+
+def collective_text(v: Variant) -> str:
+    if v.shard == "elements":
+        return ("none for the sum (element sharding: each rank's slice of the masked sum is complete); "
+                "k_decode of the slice" + (", float64 slices gathered to rank 0 (ncclSend/Recv)"
+                                           if v.gather else ""))
+    if v.exchange == "sharded":
+        return ("sharded server: ncclReduceScatter(uint64, sum) in place, every rank decodes its shard "
+                "(k_decode on the comm stream)" + (", float64 shards gathered to rank 0 (ncclSend/Recv)"
+                                                   if v.gather else ""))
+    return "ncclReduce(uint64, sum) in place to rank 0"
+
+
+def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
+    """Time `steps` steps (after `warmup`) of design `v` on this rank: the
+    masking launches on the compute stream, the design's exchange on the
+    comm stream, bracketed by a barrier + device synchronise on both sides;
+    elapsed, kernel and exchange times are the max over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    from sfl_amd import kernels as K
+    from sfl_amd.parallel_sum import PipelinedMaskedSum, element_shard, plan_generators, plan_rank
+
+    args, world, rank, dev, comm = ctx["args"], ctx["world"], ctx["rank"], ctx["dev"], ctx["comm"]
+    multi = comm is not None
+    C, N = args.clients, args.elems
+    by_elems = v.shard == "elements"
+    plan = plan_rank(ctx["names"], 1 if by_elems else world, 0 if by_elems else rank)
+    Lc = len(plan.clients)
+    e0, n_loc, k_el = element_shard(N, world, rank) if by_elems else (0, N, N)
+    xs = []
+    for c in plan.clients:
+        g = torch.Generator(device=dev).manual_seed(20260116 + c)
+        x = torch.randn(N, generator=g, device=dev, dtype=torch.float32) * 1e-2
+        xs.append(x[e0:e0 + n_loc].clone() if by_elems else x)  # the same data as at N = 1
+        del x
+    total = warmup + steps
+    chunks = args.chunks if args.chunks is not None else (8 if world > 1 and not by_elems else 1)
+    sharded = v.exchange == "sharded"
+    pipe = PipelinedMaskedSum(None if by_elems else comm, dev, n_loc, chunks,
+                              exchange="sharded" if sharded else "reduce")
+    # every step is a new round: streams start i*N draws in, chunk j at +lo_j
+    gens = [[plan_generators(plan, pair_seed, offset=i * N + e0 + lo) for lo, _ in pipe.bounds]
+            for i in range(total)]
+    # the partial sum is reduced IN PLACE (rank 0, the server, receives the
+    # masked sum in sum_buf; at N=1 there is no exchange); the sharded
+    # server's buffers are padded to whole shards, the padding zeroed once,
+    # every rank decoding its shard of each chunk into dec on the comm stream
+    sum_buf = torch.zeros(max(pipe.buffer_len, k_el if by_elems else 0), dtype=torch.int64, device=dev)
+    dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev) if sharded else None
+    dec_all = None
+    if by_elems:  # this rank's decoded slice (padded to the equal gather count) and rank 0's whole result
+        dec = torch.zeros(k_el, dtype=torch.float64, device=dev)
+        dec_all = torch.zeros(world * k_el, dtype=torch.float64, device=dev) if rank == 0 and v.gather else None
+    # no per-client digests: an XOR checksum the tests use to pin every
+    # client's masked vector, not part of the reference's arithmetic; the
+    # kernel forms each client's masked value and adds it to the sum either
+    # way (DESIGN.md §4).  --digests restores them (+1.6 % kernel time).
+    digests = torch.zeros(Lc, dtype=torch.int64, device=dev) if args.digests else None
+    flags = torch.zeros(1, dtype=torch.int32, device=dev)
+    kev, xev = [], []  # event pairs around every masking launch / exchange of the timed steps
+
+    def step(i, timed):
+        if by_elems:
+            pipe.run(xs, [1.0] * Lc, gens[i], 0, sum_buf[:n_loc], None, fxp_bits=args.fxp_bits,
+                     digests=digests, flags=flags, kernel_events=kev if timed else None)
+            cs = torch.cuda.current_stream(dev)
+            if timed and multi:
+                xev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                xev[-1][0].record(cs)
+            if multi:
+                K.decode(sum_buf[:k_el], dec, fxp_bits=args.fxp_bits)
+                if v.gather:
+                    comm.gather_f64(dec, dec_all, root=0)
+            if timed and multi:
+                xev[-1][1].record(cs)
+            return
+        # join=False: a round's exchange tail overlaps the next round's first
+        # launches (each chunk's launch still waits for that chunk's previous
+        # exchange); the timed region ends with a device synchronise
+        pipe.run(xs, [1.0] * Lc, gens[i], plan.n_cross, sum_buf, None, fxp_bits=args.fxp_bits,
+                 digests=digests, flags=flags, kernel_events=kev if timed else None,
+                 exchange_events=xev if timed else None, join=False, dec=dec, gather=v.gather)
+
+    for i in range(warmup):
+        step(i, False)
+    torch.cuda.synchronize()
+    if multi:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i, True)
+    torch.cuda.synchronize()
+    if multi:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in kev) / steps  # masking kernel time per step
+    xchg_ms = sum(a.elapsed_time(b) for a, b in xev) / steps  # exchange time per step (comm stream)
+    if multi:
+        t = torch.tensor([elapsed, kern_ms, xchg_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms, xchg_ms = float(t[0]), float(t[1]), float(t[2])
+    flagged = bool(int(flags.item()))
+    ms = elapsed * 1e3 / steps
+    n_streams = len(plan.pairs) + len(plan.cross)
+    kname = f"k_clients<float, float, {Lc}, {plan.n_cross}, {kernel_variant(Lc, plan.n_cross, args.digests)}>"
+    fused = Lc <= 8 and n_streams <= 32  # sa_fused_clients' limits (kMaxLocal, kMaxStreams)
+    if not fused and Lc > 8 and plan.n_cross == 0 and not args.digests:  # kernels.fused_many
+        kname = (f"pair-shared schedule for {Lc} local clients: k_clients<float, float, 8, 0, 1> "
+                 f"(sa_fused_bipartite) + k_clients<float, float, <=8, 0> launches")
+    elif not fused:  # sa_fused_clients masks client by client (sa_mask passes of <= 16 streams)
+        kname = f"k_clients<float, float, 1, X<=16> per client and pass (fallback for {Lc} local clients)"
+    res = {"name": v.name, "ms_per_step": ms, "value": C * N / (ms / 1e3), "steps": steps, "warmup": warmup,
+           "kernel_ms_per_step": kern_ms, "chunks": len(pipe.bounds), "kernel": kname, "fused": fused,
+           "local_clients": Lc, "n_loc": n_loc, "pair_draws": len(plan.pairs) * n_loc,
+           "one_sided_draws": len(plan.cross) * n_loc, "zero_draw_flag": flagged}
+    if multi:
+        # bytes each rank hands the exchange per step; algbw as nccl-tests
+        # defines it (buffer bytes / time), busbw the per-rank wire bytes
+        if by_elems:
+            xb = 8 * k_el * world if v.gather else 0
+            busbw_f = (world - 1) / world
+        elif sharded:
+            xb = 8 * pipe.buffer_len
+            busbw_f = (world - 1) / world
+        else:
+            xb = 8 * N
+            busbw_f = 1.0
+        algbw = xb / (xchg_ms / 1e3) / 1e9 if xchg_ms > 0 and world > 1 and xb else None
+        res["exchange"] = {
+            "collective": collective_text(v), "chunks": len(pipe.bounds), "bytes_per_rank_per_step": xb,
+            "ms_per_step": xchg_ms, "algbw_GBps": algbw, "busbw_GBps": algbw * busbw_f if algbw else None,
+            "timing": ("HIP events on the comm stream from each chunk's launch end on this rank to its "
+                       "exchange end (waiting for slower peers counts), summed per step, max over ranks"
+                       if not by_elems else "HIP events around the slice's decode (and gather) on the "
+                       "compute stream, max over ranks"),
+            "overlap": ("decode (and gather) run after the slice's launch on the compute stream" if by_elems
+                        else "chunk j's exchange runs while chunk j+1 is masked; ms_per_step ~ "
+                        "max(kernel, exchange) + one chunk of fill/drain")}
+        if world == 1:
+            res["exchange"]["note"] = "world 1 (--dist rehearsal): the collectives move no data between GPUs"
+    if keep:
+        ctx["kept"] = {"xs": xs, "plan": plan, "gens": gens}
+    else:
+        del xs, gens, sum_buf, dec, dec_all, pipe
+        torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -362,43 +605,56 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0, help="0 disables")
     ap.add_argument("--extra", action="store_true", help="also time the wire chain and H2D/D2H-inclusive rate")
     ap.add_argument("--dist", action="store_true",
-                    help="run the multi-GPU code path (RCCL communicator, reduce) even at N=1 "
+                    help="run the multi-GPU code path (RCCL communicator, exchange) even at N=1 "
                          "(rehearsal of the N>1 path on one GPU)")
     ap.add_argument("--chunks", type=int, default=None,
-                    help="masking/reduce pipeline depth (default 8 for N>1, 1 at N=1)")
-    ap.add_argument("--exchange", choices=("reduce", "sharded"), default="reduce",
-                    help="N>1 exchange: ncclReduce of the partial sums to rank 0 (default), or the sharded "
-                         "server of SURVEY.md 8(e): ncclReduceScatter, every rank decodes its shard")
+                    help="masking/exchange pipeline depth (default 8 for N>1, 1 at N=1)")
+    ap.add_argument("--exchange", choices=("reduce", "sharded"), default=None,
+                    help="N>1 headline exchange: the sharded server of SURVEY.md 8(e) (default: "
+                         "ncclReduceScatter, every rank decodes its shard), or ncclReduce of the partial sums "
+                         "to rank 0")
     ap.add_argument("--gather", action="store_true",
                     help="with --exchange sharded or --shard elements: also gather the decoded float64 shards "
                          "to rank 0")
     ap.add_argument("--shard", choices=("clients", "elements"), default="clients",
                     help="N>1: clients in contiguous blocks per GPU (default, config 3), or every GPU takes "
                          "1/N of every client's elements (SURVEY.md 8(e)'s alternative; no exchange for the sum)")
+    ap.add_argument("--variants", default="all",
+                    help="N>1: the other exchange designs timed after the headline in the same process group "
+                         f"('all' = {','.join(VARIANTS)}; a comma list; 'none')")
+    ap.add_argument("--variant-steps", type=int, default=200, help="timed steps per extra design")
     ap.add_argument("--digests", action="store_true",
                     help="also fold every client's masked values into an XOR digest (test checksum)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher rehearsal without a GPU: ranks join a gloo group, rank 0 prints one line")
-    ap.add_argument("--watchdog-seconds", type=float, default=900.0,
-                    help="a rank still running after this long exits with status 3 (a hung collective "
-                         "cannot be interrupted from Python; torchrun then stops the other ranks); 0 disables")
+    ap.add_argument("--watchdog-seconds", type=float, default=480.0,
+                    help="a rank still running after this long dumps every thread's stack (faulthandler) and "
+                         "exits (a hung collective cannot be interrupted from Python; torchrun then stops the "
+                         "other ranks); below the driver's 600 s lease; 0 disables")
     args = ap.parse_args()
+    for v in (args.variants.split(",") if args.variants not in ("all", "none") else []):
+        if v and v not in VARIANTS:
+            ap.error(f"--variants: unknown design {v!r} (choose from {', '.join(VARIANTS)})")
 
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dist):
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.watchdog_seconds > 0:
+        import faulthandler
         import threading
 
-        def _expire():
-            print(f"bench.py rank {rank}: still running after {args.watchdog_seconds:.0f} s, exiting",
-                  file=sys.stderr, flush=True)
-            os._exit(3)
+        def _note():
+            print(f"bench.py rank {rank}: still running after {args.watchdog_seconds - 2:.0f} s; dumping every "
+                  f"thread's stack and exiting", file=sys.stderr, flush=True)
 
-        wd = threading.Timer(args.watchdog_seconds, _expire)
-        wd.daemon = True
-        wd.start()
+        t = threading.Timer(max(0.0, args.watchdog_seconds - 2), _note)
+        t.daemon = True
+        t.start()
+        # a C thread: dumps and exits even while the main thread sits in a
+        # collective holding the GIL
+        faulthandler.dump_traceback_later(args.watchdog_seconds, exit=True)
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # CPU baseline first: its per-client worker processes are forked, which
@@ -407,196 +663,99 @@ def main():
     if args.dry_run:
         dry_run(args, world, rank, cpu)
         return
-    # same-box draw-loop ceiling (N = 1: the headline's 8-client kernel),
-    # also before this process initialises the GPU
-    ceiling = draw_loop_ceiling() if world == 1 and not args.dist and args.clients == 8 else None
+    multi = world > 1 or args.dist
+    # same-box draw-loop ceilings, also before this process initialises the GPU
+    ceil = draw_loop_ceilings(local_rank if world > 1 else None)
 
     import torch
     import torch.distributed as dist
 
     from sfl_amd import _lib
-    from sfl_amd import kernels as K
-    from sfl_amd.parallel_sum import PipelinedMaskedSum, RcclComm, element_shard, plan_generators, plan_rank
+    from sfl_amd.parallel_sum import RcclComm
 
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     _lib.lib()
     comm = None
-    multi = world > 1 or args.dist
     if multi:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         comm = RcclComm(rank, world, local_rank)
 
     C, N = args.clients, args.elems
-    names = [f"client{c}" for c in range(C)]
-    by_elems = multi and args.shard == "elements"
-    # element sharding (SURVEY.md §8(e)'s alternative): every rank holds ALL
-    # clients' elements [e0, e0 + n_loc) and masks them in one fused launch,
-    # streams jumped to e0; no exchange for the sum (each rank's slice of it
-    # is complete), the decoded float64 slices gathered to rank 0 on --gather
-    plan = plan_rank(names, 1 if by_elems else world, 0 if by_elems else rank)
-    Lc = len(plan.clients)
-    e0, n_loc, k_el = element_shard(N, world, rank) if by_elems else (0, N, N)
-    xs = []
-    for c in plan.clients:
-        g = torch.Generator(device=dev).manual_seed(20260116 + c)
-        x = torch.randn(N, generator=g, device=dev, dtype=torch.float32) * 1e-2
-        xs.append(x[e0:e0 + n_loc].clone() if by_elems else x)  # the same data as at N = 1
-        del x
-    total_steps = args.warmup + args.steps
-    chunks = args.chunks if args.chunks is not None else (8 if world > 1 and not by_elems else 1)
-    sharded = multi and args.exchange == "sharded" and not by_elems
-    pipe = PipelinedMaskedSum(None if by_elems else comm, dev, n_loc, chunks,
-                              exchange="sharded" if sharded else "reduce")
-    # every step is a new round: streams start i*N draws in, chunk j at +lo_j
-    gens = [[plan_generators(plan, pair_seed, offset=i * N + e0 + lo) for lo, _ in pipe.bounds]
-            for i in range(total_steps)]
-    # the partial sum is reduced IN PLACE (rank 0, the server, receives the
-    # masked sum in sum_buf; at N=1 the reduce is a no-op)
-    # (sharded server: padded to whole shards, the padding zeroed once; every
-    # rank decodes its shard of each chunk into dec on the comm stream)
-    sum_buf = torch.zeros(max(pipe.buffer_len, k_el if by_elems else 0), dtype=torch.int64, device=dev)
-    dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev) if sharded else None
-    if by_elems:  # this rank's decoded slice (padded to the equal gather count) and rank 0's whole result
-        dec = torch.zeros(k_el, dtype=torch.float64, device=dev)
-        dec_all = torch.zeros(world * k_el, dtype=torch.float64, device=dev) if rank == 0 and args.gather else None
-    # no per-client digests: an XOR checksum the tests use to pin every
-    # client's masked vector, not part of the reference's arithmetic; the
-    # kernel forms each client's masked value and adds it to the sum either
-    # way.  --digests restores them (+1.6 % kernel time).
-    digests = torch.zeros(Lc, dtype=torch.int64, device=dev) if args.digests else None
-    flags = torch.zeros(1, dtype=torch.int32, device=dev)
-    kev = []  # (start, end) events around every masking launch of the timed steps (compute stream)
-    xev = []  # (start, end) events around every reduce of the timed steps (comm stream)
-
-    def step(i, timed_idx=None):
-        if by_elems:
-            pipe.run(xs, [1.0] * Lc, gens[i], 0, sum_buf[:n_loc], None, fxp_bits=args.fxp_bits,
-                     digests=digests, flags=flags, kernel_events=kev if timed_idx is not None else None)
-            cs = torch.cuda.current_stream(dev)
-            if timed_idx is not None:
-                xev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
-                xev[-1][0].record(cs)
-            K.decode(sum_buf[:k_el], dec, fxp_bits=args.fxp_bits)
-            if args.gather:
-                comm.gather_f64(dec, dec_all, root=0)
-            if timed_idx is not None:
-                xev[-1][1].record(cs)
-            return
-        # join=False: a round's exchange tail overlaps the next round's first
-        # launches (each chunk's launch still waits for that chunk's previous
-        # reduce); the timed region ends with a device synchronise
-        pipe.run(xs, [1.0] * Lc, gens[i], plan.n_cross, sum_buf, None, fxp_bits=args.fxp_bits,
-                 digests=digests, flags=flags, kernel_events=kev if timed_idx is not None else None,
-                 exchange_events=xev if timed_idx is not None else None, join=False,
-                 dec=dec, gather=args.gather)
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if multi:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i, i)
-    torch.cuda.synchronize()
-    if multi:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in kev) / args.steps  # masking kernel time per step
-    xchg_ms = sum(a.elapsed_time(b) for a, b in xev) / args.steps  # reduce time per step (comm stream)
-    if multi:
-        t = torch.tensor([elapsed, kern_ms, xchg_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, xchg_ms = float(t[0]), float(t[1]), float(t[2])
-    if int(flags.item()):
+    ctx = {"args": args, "world": world, "rank": rank, "dev": dev, "comm": comm,
+           "names": [f"client{c}" for c in range(C)]}
+    head = headline_variant(args, multi)
+    r = run_design(ctx, head, args.steps, args.warmup, keep=args.extra and world == 1)
+    if r["zero_draw_flag"]:
         print("warning: PRG zero-draw flag raised", file=sys.stderr)
-
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = C * N / (ms_per_step / 1e3)
-    draws = (len(plan.pairs) + len(plan.cross)) * n_loc
+    kern_ms, launches = r["kernel_ms_per_step"], r["chunks"]
+    n_loc, Lc = r["n_loc"], r["local_clients"]
     bytes_alg = 4 * Lc * n_loc + 8 * n_loc  # per step: fp32 reads of the local clients + one u64 sum write
-    launches = len(pipe.bounds)
     achieved = bytes_alg / (kern_ms / 1e3) / 1e9
-    kname = f"k_clients<float, float, {Lc}, {plan.n_cross}, {kernel_variant(Lc, plan.n_cross, args.digests)}>"
-    n_streams = len(plan.pairs) + len(plan.cross)
-    fused = Lc <= 8 and n_streams <= 32  # sa_fused_clients' limits (kMaxLocal, kMaxStreams)
-    if not fused and Lc > 8 and plan.n_cross == 0 and not args.digests:  # kernels.fused_many
-        kname = (f"pair-shared schedule for {Lc} local clients: k_clients<float, float, 8, 0, 1> "
-                 f"(sa_fused_bipartite) + k_clients<float, float, <=8, 0> launches")
-    elif not fused:  # sa_fused_clients masks client by client (sa_mask passes of <= 16 streams)
-        kname = f"k_clients<float, float, 1, X<=16> per client and pass (fallback for {Lc} local clients)"
-    pmc = pmc_traffic(f"void sa::{kname}", n_loc // launches)
-    draws_s = draws / (kern_ms / 1e3)
-    peak_draws = ceiling["draws_per_s"] if ceiling else PCG_PAIR_DRAWS_2WAVE
+    pmc = pmc_traffic(f"void sa::{r['kernel']}", n_loc // launches)
+    traffic, traffic_detail = traffic_field(pmc, bytes_alg / launches)
+    # VALU: the step's draws against the same-box draw loop at the same draw
+    # kinds: ideal time = pair draws / pair ceiling + one-sided / one-sided ceiling
+    pair_peak = ceil["pair"]["draws_per_s"] if "pair" in ceil else PCG_PAIR_DRAWS_2WAVE
+    one_peak = ceil["one"]["draws_per_s"] if "one" in ceil else PCG_ONE_DRAWS_8WAVE
+    draws = r["pair_draws"] + r["one_sided_draws"]
+    ideal_s = r["pair_draws"] / pair_peak + r["one_sided_draws"] / one_peak
     out = {
         "metric": METRIC,
-        "value": value,
+        "value": r["value"],
         "unit": "grad elems/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
+        "ms_per_step": r["ms_per_step"],
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (N(0,0.01^2) fp32 gradients generated on device)",
-        "config": {"workload": workload(args, world),
-                   "clients": C, "elems_per_client": N, "clients_per_gpu": Lc,
-                   "parallelism": f"{'elements' if by_elems else 'clients'}{world}", "pipeline_chunks": launches,
-                   "client_digests": bool(args.digests)},
+        "config": {"workload": workload(args, world, head),
+                   "clients": C, "elems_per_client": N, "clients_per_gpu": Lc, "design": head.name,
+                   "parallelism": f"{'elements' if head.shard == 'elements' else 'clients'}{world}",
+                   "pipeline_chunks": launches, "client_digests": bool(args.digests)},
         # per launch: algorithmic bytes of one launch / its average duration
         # (HIP events on the launch stream); the step's launches are equal
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
-                     "traffic": pmc["bytes"] if pmc else None, "traffic_detail": pmc,
-                     "kernel": f"{kname} (sa_fused_clients)" if fused else kname, "kernel_ms_per_step": kern_ms,
+                     "traffic": traffic, "traffic_detail": traffic_detail,
+                     "kernel": f"{r['kernel']} (sa_fused_clients)" if r["fused"] else r["kernel"],
+                     "kernel_ms_per_step": kern_ms,
                      "launches_per_step": launches,
                      "algorithmic_bytes_per_launch": bytes_alg / launches,
                      "kernel_ms_per_launch": kern_ms / launches,
-                     "valu": {"pcg64_draws_per_step": draws, "draws_per_s": draws_s,
-                              "peak_draws_per_s": peak_draws,
-                              "peak_source": ("measured on this box: tools/microbench/draw_issue 'dual pair28 E2' "
-                                              "at 2 waves/SIMD, median of 15 launches after 40 warm-up" if ceiling else
-                                              "constant from profiles/r01/draw_issue_microbench.txt (another box)"),
-                              "peak_note": "draw loop alone, pair draws at 2 waves/SIMD (the L=8 kernel's "
-                                           "occupancy); one-sided draws at 8 waves/SIMD reach "
-                                           f"{PCG_ONE_DRAWS_8WAVE:.3g}",
-                              "frac": draws_s / peak_draws,
-                              "frac_vs_one_sided_8wave": draws_s / PCG_ONE_DRAWS_8WAVE}},
+                     "valu": {"pcg64_draws_per_step": draws, "pair_draws_per_step": r["pair_draws"],
+                              "one_sided_draws_per_step": r["one_sided_draws"],
+                              "draws_per_s": draws / (kern_ms / 1e3),
+                              "peak_pair_draws_per_s": pair_peak, "peak_one_sided_draws_per_s": one_peak,
+                              "peak_source": ("measured on this rank's GPU before the bench touched it: "
+                                              "tools/microbench/draw_issue 'dual pair28 E2' at 2 waves/SIMD and "
+                                              "'dual one7 E2' at 8, median of 15 launches after 40 warm-up"
+                                              if len(ceil) == 2 else
+                                              "constants from profiles/r01/draw_issue_microbench.txt (another "
+                                              "box): the same-box measurement failed"),
+                              "ideal_ms_per_step": ideal_s * 1e3,
+                              "frac": ideal_s / (kern_ms / 1e3)}},
     }
     if multi:
-        # the exchange step: every rank's uint64 partial sum
-        # reduced in place to rank 0, one ncclReduce per pipeline chunk on a
-        # comm stream beside the masking launches; time from each chunk's
-        # launch end on this rank to its reduce end, summed per step, max over
-        # ranks.  nccl-tests' convention: reduce bus bandwidth = algbw.
-        xb = 8 * N
-        coll = "ncclReduce(uint64, sum) in place to rank 0"
-        if by_elems:
-            xb = 8 * k_el if args.gather else 0
-            coll = ("none for the sum (element sharding: each rank's slice of the masked sum is complete); "
-                    "k_decode of the slice" + (", float64 slices gathered to rank 0 (ncclSend/Recv)"
-                                               if args.gather else ""))
-        elif sharded:
-            coll = ("sharded server: ncclReduceScatter(uint64, sum) in place, every rank decodes its shard "
-                    "(k_decode on the comm stream)" + (", float64 shards gathered to rank 0 (ncclSend/Recv)"
-                                                       if args.gather else ""))
-        out["exchange"] = {"collective": coll,
-                           "chunks": launches, "bytes_per_rank_per_step": xb,
-                           "ms_per_step": xchg_ms,
-                           "algbw_GBps": xb / (xchg_ms / 1e3) / 1e9 if xchg_ms > 0 and world > 1 else None,
-                           "overlap": ("decode (and gather) run after the slice's launch on the compute stream"
-                                       if by_elems else "chunk j's reduce runs while chunk j+1 is masked; "
-                                       "ms_per_step ~ max(kernel, exchange) + one chunk of fill/drain")}
-        if world == 1:
-            out["exchange"]["note"] = "world 1 (--dist rehearsal): the collectives move no data between GPUs"
+        out["exchange"] = r["exchange"]
+        variants = [r]
+        for v in other_variants(args, head):
+            variants.append(run_design(ctx, v, args.variant_steps, min(5, args.warmup)))
+        out["exchange_variants"] = [
+            {"name": x["name"], "value": x["value"], "ms_per_step": x["ms_per_step"], "steps": x["steps"],
+             "kernel_ms_per_step": x["kernel_ms_per_step"], "kernel": x["kernel"], "chunks": x["chunks"],
+             "xchg_ms": x["exchange"]["ms_per_step"], "bytes_per_rank_per_step": x["exchange"]["bytes_per_rank_per_step"],
+             "algbw_GBps": x["exchange"]["algbw_GBps"], "busbw_GBps": x["exchange"]["busbw_GBps"],
+             "collective": x["exchange"]["collective"]} for x in variants]
     if args.extra and world == 1:
-        out["extra"] = extra_measurements(args, xs, plan, gens, K, torch, dev)
+        from sfl_amd import kernels as K
+
+        kept = ctx["kept"]
+        out["extra"] = extra_measurements(args, kept["xs"], kept["plan"], kept["gens"], K, torch, dev)
     if rank == 0:
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)

@@ -180,13 +180,15 @@ int sa_sum_u64(const uint64_t* const* in, int k, uint64_t n, uint64_t* out, void
 /* Server decode: out[i] = (double)(int64)s[i] / 2^fxp / div, with
  * div = divisor_vec[i] when divisor_vec != NULL (per-element weights,
  * CHANGELOG.md:994) else `divisor` (1.0 for sum, C or sum(w) for average).
- * Division is IEEE (correctly rounded), matching numpy float64. */
+ * Division is IEEE (correctly rounded), matching numpy float64.  16-byte
+ * aligned s / out / divisor_vec take 16-B accesses (two elements per lane),
+ * other alignments one 8-B element per lane. */
 int sa_decode(const uint64_t* s, uint64_t n, int fxp_bits, double divisor,
               const double* divisor_vec, double* out, void* stream);
 
 /* Element-wise sum of per-client weight arrays for per-element-weight
  * averages: out[i] = sum_k w[k][i] (float64), `w` a HOST array of k device
- * pointers. */
+ * pointers.  16-B accesses when every buffer is 16-byte aligned. */
 int sa_sum_f64(const double* const* w, int k, uint64_t n, double* out, void* stream);
 
 /* ------------------------------------------------------------------ */

@@ -89,6 +89,14 @@ class SecureAggregator:
 
     def average(self, data: List, axis=None, weights=None):
         if weights is not None and not _is_device_object(weights):
+            assert len(weights) == len(data), (
+                f"Length of the weights does not match the data: {len(weights)} vs {len(data)}.")
+            for i, w in enumerate(weights):
+                # a device-object weight must live on its data's party
+                # (stateful_fedgen_aggregator.py:74-78), checked before it is revealed
+                if _is_device_object(w) and _is_device_object(data[i]):
+                    assert _party(w.device) == _party(data[i].device), (
+                        "Device of weight does not match the corresponding data device.")
             weights = [self._value(w) if _is_device_object(w) else w for w in weights]
         out = self._inner.average(self._objects(data), axis=axis, weights=weights)
         return self._wrap(self._sf_device, _reveal_local(out))

@@ -39,8 +39,31 @@ int occupancy_blocks(const void* kernel) {
 }
 
 // ---------------------------------------------------------------------------
-// server sum: out = sum_k in[k]  (mod 2^64), 2 u64 per lane per step
+// The server kernels stream HBM: 16-B accesses (two 8-B elements per lane and
+// access), one tile of 256 x kUnroll accesses per block over a grid that
+// covers the vector (no grid-stride loop), non-temporal loads and stores (the
+// vectors are read once and written once).  tools/microbench/stream_rate.hip
+// measured these choices on MI355X (profiles/r03/stream_rate.jsonl): copy
+// 6.38 TB/s, two inputs 6.42, eight inputs 6.20, against 4.9-5.6 TB/s for an
+// occupancy-sized grid-stride loop with default-policy accesses.  An odd last
+// element is done by one lane of block 0.
 // ---------------------------------------------------------------------------
+constexpr int kUnroll = 4;
+constexpr int kTileAccesses = 256 * kUnroll;  // 16-B accesses per block and input
+
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+template <typename T>
+__device__ __forceinline__ T ld_nt(const T* p) {
+  return __builtin_nontemporal_load(p);
+}
+template <typename T>
+__device__ __forceinline__ void st_nt(T* p, T v) {
+  __builtin_nontemporal_store(v, p);
+}
+
+// server sum: out = sum_k in[k]  (mod 2^64)
 constexpr int kSumMaxIn = 32;
 struct SumArgs {
   const uint64_t* in[kSumMaxIn];
@@ -51,37 +74,71 @@ struct SumArgs {
 
 __global__ void __launch_bounds__(256) k_sum_u64(const SumArgs a) {
   const uint64_t n2 = a.n / 2;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
-    ulonglong2 s = reinterpret_cast<const ulonglong2*>(a.in[0])[i];
-    for (int j = 1; j < a.k; j++) {
-      const ulonglong2 v = reinterpret_cast<const ulonglong2*>(a.in[j])[i];
-      s.x += v.x;
-      s.y += v.y;
-    }
-    reinterpret_cast<ulonglong2*>(a.out)[i] = s;
+  const uint64_t base = (uint64_t)blockIdx.x * kTileAccesses + threadIdx.x;
+  u64x2 s[kUnroll];
+#pragma unroll
+  for (int u = 0; u < kUnroll; u++)
+    s[u] = base + u * 256 < n2 ? ld_nt(reinterpret_cast<const u64x2*>(a.in[0]) + base + u * 256) : u64x2{0, 0};
+  for (int j = 1; j < a.k; j++) {
+    const u64x2* in = reinterpret_cast<const u64x2*>(a.in[j]);
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++)
+      if (base + u * 256 < n2) s[u] += ld_nt(in + base + u * 256);
   }
+#pragma unroll
+  for (int u = 0; u < kUnroll; u++)
+    if (base + u * 256 < n2) st_nt(reinterpret_cast<u64x2*>(a.out) + base + u * 256, s[u]);
   if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    uint64_t s = 0;
-    for (int j = 0; j < a.k; j++) s += a.in[j][a.n - 1];
-    a.out[a.n - 1] = s;
+    uint64_t t = 0;
+    for (int j = 0; j < a.k; j++) t += a.in[j][a.n - 1];
+    a.out[a.n - 1] = t;
   }
 }
 
-// ---------------------------------------------------------------------------
 // decode: out = (double)(int64)s / 2^fxp / div
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_decode(const uint64_t* __restrict__ s, uint64_t n,
-                                                double inv_scale, double div,
-                                                const double* __restrict__ divv,
-                                                double* __restrict__ out) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const double v = (double)(long long)s[i] * inv_scale;  // exact power-of-two scaling
-    out[i] = v / (divv ? divv[i] : div);                   // IEEE division
-  }
+__device__ __forceinline__ double decode1(uint64_t s, double inv_scale, double div) {
+  const double v = (double)(long long)s * inv_scale;  // exact power-of-two scaling
+  return v / div;                                     // IEEE division
 }
 
+// s, out (and divv) 16-B aligned
+template <bool kVec>
+__global__ void __launch_bounds__(256) k_decode(const uint64_t* __restrict__ s, uint64_t n, double inv_scale,
+                                                double div, const double* __restrict__ divv,
+                                                double* __restrict__ out) {
+  const uint64_t n2 = n / 2;
+  const uint64_t base = (uint64_t)blockIdx.x * kTileAccesses + threadIdx.x;
+  const u64x2* s2 = reinterpret_cast<const u64x2*>(s);
+  const f64x2* d2 = reinterpret_cast<const f64x2*>(divv);
+  f64x2* o2 = reinterpret_cast<f64x2*>(out);
+  u64x2 v[kUnroll];
+  f64x2 d[kUnroll];
+#pragma unroll
+  for (int u = 0; u < kUnroll; u++) {
+    const bool in = base + u * 256 < n2;
+    v[u] = in ? ld_nt(s2 + base + u * 256) : u64x2{0, 0};
+    if (kVec) d[u] = in ? ld_nt(d2 + base + u * 256) : f64x2{1.0, 1.0};
+  }
+#pragma unroll
+  for (int u = 0; u < kUnroll; u++)
+    if (base + u * 256 < n2)
+      st_nt(o2 + base + u * 256, f64x2{decode1(v[u].x, inv_scale, kVec ? d[u].x : div),
+                                       decode1(v[u].y, inv_scale, kVec ? d[u].y : div)});
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0)
+    out[n - 1] = decode1(s[n - 1], inv_scale, kVec ? divv[n - 1] : div);
+}
+
+// any alignment (8-B elements one per lane): sub-vectors the caller sliced at odd offsets
+__global__ void __launch_bounds__(256) k_decode_unaligned(const uint64_t* __restrict__ s, uint64_t n,
+                                                          double inv_scale, double div,
+                                                          const double* __restrict__ divv,
+                                                          double* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = decode1(s[i], inv_scale, divv ? divv[i] : div);
+}
+
+// per-element weight sums (the average's divisor vector): out = [out +] sum_k in[k]
 struct SumF64Args {
   const double* in[kSumMaxIn];
   double* out;
@@ -90,12 +147,48 @@ struct SumF64Args {
   int accumulate;
 };
 __global__ void __launch_bounds__(256) k_sum_f64(const SumF64Args a) {
+  const uint64_t n2 = a.n / 2;
+  const uint64_t base = (uint64_t)blockIdx.x * kTileAccesses + threadIdx.x;
+  const int j0 = a.accumulate ? 0 : 1;
+  const f64x2* first = reinterpret_cast<const f64x2*>(a.accumulate ? a.out : a.in[0]);
+  f64x2 s[kUnroll];
+#pragma unroll
+  for (int u = 0; u < kUnroll; u++) s[u] = base + u * 256 < n2 ? ld_nt(first + base + u * 256) : f64x2{0, 0};
+  for (int j = j0; j < a.k; j++) {
+    const f64x2* in = reinterpret_cast<const f64x2*>(a.in[j]);
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++)
+      if (base + u * 256 < n2) s[u] += ld_nt(in + base + u * 256);
+  }
+#pragma unroll
+  for (int u = 0; u < kUnroll; u++)
+    if (base + u * 256 < n2) st_nt(reinterpret_cast<f64x2*>(a.out) + base + u * 256, s[u]);
+  if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    double t = a.accumulate ? a.out[a.n - 1] : a.in[0][a.n - 1];
+    for (int j = j0; j < a.k; j++) t += a.in[j][a.n - 1];
+    a.out[a.n - 1] = t;
+  }
+}
+
+// any alignment: one element per lane
+__global__ void __launch_bounds__(256) k_sum_f64_unaligned(const SumF64Args a) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
     double s = a.accumulate ? a.out[i] : a.in[0][i];
     for (int j = a.accumulate ? 0 : 1; j < a.k; j++) s += a.in[j][i];
     a.out[i] = s;
   }
+}
+
+// one block per tile of kTileAccesses 16-B accesses (at least one block for
+// the odd-element lane)
+static int tile_grid(uint64_t n) {
+  const uint64_t b = (n / 2 + kTileAccesses - 1) / kTileAccesses;
+  if (b >= (1ull << 31)) {
+    sa_set_error("vector of %llu elements exceeds one server-kernel launch", (unsigned long long)n);
+    return -1;
+  }
+  return b < 1 ? 1 : (int)b;
 }
 
 static int stream_grid(uint64_t work_items, const void* kfn) {
@@ -387,8 +480,8 @@ extern "C" int sa_sum_u64(const uint64_t* const* in, int k, uint64_t n, uint64_t
     return SA_ERR_ARG;
   }
   if (n == 0) return SA_OK;
-  const int grid = stream_grid(n / 2 + 1, (const void*)&k_sum_u64);
-  if (grid < 0) return SA_ERR_HIP;
+  const int grid = tile_grid(n);
+  if (grid < 0) return SA_ERR_ARG;
   // chain launches of up to 32 inputs; later launches fold the running sum in as input 0
   for (int j0 = 0; j0 < k;) {
     SumArgs a;
@@ -412,11 +505,21 @@ extern "C" int sa_decode(const uint64_t* s, uint64_t n, int fxp_bits, double div
     return SA_ERR_ARG;
   }
   if (n == 0) return SA_OK;
-  const int grid = stream_grid(n, (const void*)&k_decode);
-  if (grid < 0) return SA_ERR_HIP;
   const double inv_scale = 1.0 / (double)((uint64_t)1 << fxp_bits);
-  hipLaunchKernelGGL(k_decode, dim3(grid), dim3(256), 0, (hipStream_t)stream, s, n, inv_scale,
-                     divisor, divisor_vec, out);
+  const bool vec = aligned16(s) && aligned16(out) && aligned16(divisor_vec);
+  const void* kfn = !vec ? (const void*)&k_decode_unaligned
+                         : divisor_vec ? (const void*)&k_decode<true> : (const void*)&k_decode<false>;
+  const int grid = vec ? tile_grid(n) : stream_grid(n, kfn);
+  if (grid < 0) return vec ? SA_ERR_ARG : SA_ERR_HIP;
+  if (!vec)
+    hipLaunchKernelGGL(k_decode_unaligned, dim3(grid), dim3(256), 0, (hipStream_t)stream, s, n, inv_scale,
+                       divisor, divisor_vec, out);
+  else if (divisor_vec)
+    hipLaunchKernelGGL(k_decode<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, s, n, inv_scale, divisor,
+                       divisor_vec, out);
+  else
+    hipLaunchKernelGGL(k_decode<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, s, n, inv_scale,
+                       divisor, divisor_vec, out);
   SA_HIP_CHECK(hipGetLastError());
   return SA_OK;
 }
@@ -427,8 +530,16 @@ extern "C" int sa_sum_f64(const double* const* w, int k, uint64_t n, double* out
     sa_set_error("sa_sum_f64: bad arguments");
     return SA_ERR_ARG;
   }
-  const int grid = stream_grid(n, (const void*)&k_sum_f64);
-  if (grid < 0) return SA_ERR_HIP;
+  bool vec = aligned16(out);
+  for (int j = 0; j < k; j++) {
+    if (!w[j]) {
+      sa_set_error("sa_sum_f64: input %d null", j);
+      return SA_ERR_ARG;
+    }
+    vec = vec && aligned16(w[j]);
+  }
+  const int grid = vec ? tile_grid(n) : stream_grid(n, (const void*)&k_sum_f64_unaligned);
+  if (grid < 0) return vec ? SA_ERR_ARG : SA_ERR_HIP;
   for (int j0 = 0; j0 < k;) {
     SumF64Args a;
     memset(&a, 0, sizeof(a));
@@ -438,7 +549,10 @@ extern "C" int sa_sum_f64(const double* const* w, int k, uint64_t n, double* out
     a.k = m;
     a.out = out;
     a.n = n;
-    hipLaunchKernelGGL(k_sum_f64, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    if (vec)
+      hipLaunchKernelGGL(k_sum_f64, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(k_sum_f64_unaligned, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
     SA_HIP_CHECK(hipGetLastError());
   }
   return SA_OK;

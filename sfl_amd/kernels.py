@@ -321,12 +321,18 @@ def xor_digest(v: torch.Tensor, digest: torch.Tensor) -> torch.Tensor:
     return digest
 
 
-def rejected_draws(gen, n: int, device) -> tuple[list, int]:
+def rejected_draws(gen, n: int, device, first: int | None = -1) -> tuple[list, int]:
     """numpy's Generator.integers over n elements from ``gen``: the
     (element, shift) points where a rejected raw 0 moves the stream one raw
     draw further (element e >= k uses raw[e + shift]), and the total number
-    of raw draws consumed (n + rejections)."""
+    of raw draws consumed (n + rejections).  ``first``: the stream's first
+    zero in [0, n) when already searched (None: there is none)."""
+    if first is None:
+        return [], n
     pts, e0, s = [], 0, 0
+    if first != -1:
+        e0, s = first, 1
+        pts.append((e0, s))
     while e0 < n:
         # elements >= e0 use raw[e + s]: search raw[e0 + s, n + s)
         z = find_zero_draws([L.pcg64_advance(gen, e0 + s)], n - e0, device)[0]
@@ -335,3 +341,12 @@ def rejected_draws(gen, n: int, device) -> tuple[list, int]:
         e0, s = e0 + z, s + 1
         pts.append((e0, s))
     return pts, n + s
+
+
+def rejected_draws_many(gens: Sequence, n: int, device) -> list:
+    """``rejected_draws`` for many streams: the first zero of every stream is
+    searched by ONE sa_pcg64_find_zero call (up to 64 generators per launch
+    inside it) and one host sync; only the streams with a hit are followed
+    further."""
+    first = find_zero_draws(list(gens), n, device)
+    return [rejected_draws(g, n, device, first=f) for g, f in zip(gens, first)]

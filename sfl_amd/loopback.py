@@ -337,8 +337,9 @@ class LoopbackClient:
             # numpy's Generator.integers rejected a raw 0 on some stream: move
             # the masked vector onto numpy's stream from there (sa_stream_shift)
             with torch.cuda.stream(cs):
-                for peer, (gen, sign, _) in zip(self.masker.peers, self.masker.streams()):
-                    pts, total = K.rejected_draws(gen, n, dev)
+                streams = self.masker.streams()
+                found = K.rejected_draws_many([g for g, _, _ in streams], n, dev)
+                for peer, (gen, sign, _), (pts, total) in zip(self.masker.peers, streams, found):
                     for k, shift in pts:
                         K.stream_shift(dm, gen, sign, k, shift)
                     if total > n:

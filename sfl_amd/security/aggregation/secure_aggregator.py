@@ -157,16 +157,28 @@ class SecureAggregator(Aggregator):
         same stream positions in careful mode, which re-positions the
         affected streams exactly as numpy does (``_fix_rejections``)."""
         snap = {nm: m.snapshot() for nm, m in self._maskers.items()}
+
+        def restore():
+            for nm, m in self._maskers.items():
+                m.restore(snap[nm])
+
         try:
             return self._aggregate_once(data, axis, weights, average)
         except _Rejected:
-            for nm, m in self._maskers.items():
-                m.restore(snap[nm])
-            self._careful = True
-            try:
-                return self._aggregate_once(data, axis, weights, average)
-            finally:
-                self._careful = False
+            restore()
+        except BaseException:
+            # any other failure part-way through a multi-group round: put every
+            # stream back where the peers (and numpy) still have it
+            restore()
+            raise
+        self._careful = True
+        try:
+            return self._aggregate_once(data, axis, weights, average)
+        except BaseException:
+            restore()
+            raise
+        finally:
+            self._careful = False
 
     def _aggregate_once(self, data, axis, weights, average: bool) -> DeviceObject:
         assert data, "Data to aggregate should not be None or empty!"
@@ -422,13 +434,17 @@ class SecureAggregator(Aggregator):
                    and all(x.dtype == torch.float32 for x in xs)
                    and all(wv is None for wv in wvecs)
                    and set(names) == set(self._maskers))
+        # the pair streams (one host jump-ahead each) only where a path uses
+        # them: the fused launch and the careful replay's rejection search
+        want_pairs = fusable or self._careful
         pair_gens, pair_signs = [], []
         for u in range(C):
             for v in range(u + 1, C):
                 mu, mv = self._maskers[names[u]], self._maskers[names[v]]
                 assert mu.position(names[v]) == mv.position(names[u]), "pair streams out of step"
-                pair_gens.append(mu.generator(names[v]))
-                pair_signs.append(mu.sign(names[v]))
+                if want_pairs:
+                    pair_gens.append(mu.generator(names[v]))
+                    pair_signs.append(mu.sign(names[v]))
         # per-party (generator, sign, peer) lists: the wire path's launches and the
         # careful-mode rejection fix-up need them (built lazily: 7 jump-aheads a party)
         client_streams = (None if fusable and not self._careful else
@@ -492,10 +508,13 @@ class SecureAggregator(Aggregator):
         C = len(names)
         fixes = {c: [] for c in range(C)}  # client -> [(gen, sign, points)]
         extra = {}
+        # one batched search over every pair stream first (64 generators per
+        # launch); only streams with a hit are followed further
+        found = K.rejected_draws_many(pair_gens, n, sdev)
         p = 0
         for u in range(C):
             for v in range(u + 1, C):
-                pts, total = K.rejected_draws(pair_gens[p], n, sdev)
+                pts, total = found[p]
                 if pts:
                     fixes[u].append((pair_gens[p], pair_signs[p], pts))
                     fixes[v].append((pair_gens[p], -pair_signs[p], pts))

@@ -11,7 +11,6 @@ ranks join a gloo group instead of touching a GPU).
 """
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -53,11 +52,9 @@ def test_self_launch_spawns_n_ranks_and_prints_one_line(n):
 
 
 def test_outer_torchrun_rank0_measures_cpu_baseline():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "2",
+                        "--rdzv-backend", "c10d", "--rdzv-endpoint", "127.0.0.1:0", "--rdzv-id", "outer-test",
+                        "--local-addr", "127.0.0.1", BENCH, "--gpus", "2",
                         "--dry-run", "--cpu-baseline-seconds", "0.2"],
                        capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -78,6 +75,7 @@ def test_world_one_runs_in_process():
 
 @pytest.mark.parametrize("opts,expect", [
     (["--exchange", "sharded", "--gather"], "ncclReduceScatter(uint64) of the partial sum"),
+    (["--exchange", "reduce"], "ncclReduce(uint64) of the partial sum to rank 0"),
     (["--shard", "elements"], "element-sharded: every rank masks its 1/2 of every client's elements"),
 ])
 def test_exchange_options_reach_every_rank(opts, expect):
@@ -116,3 +114,70 @@ def test_bench_kernel_variant_table_matches_the_registry():
     assert shapes == bench.SUM_ONLY_SHAPES
     assert bench.kernel_variant(8, 0, False) == 4 and bench.kernel_variant(8, 0, True) == 0
     assert bench.kernel_variant(1, 7, False) == 6 and bench.kernel_variant(1, 5, False) == 2
+
+
+def test_n_gt_1_line_names_every_exchange_design_and_a_safe_launch():
+    """One `bench.py --gpus N` run times every N>1 design in the same process
+    group (exchange_variants, the headline first); the ranks rendezvous on a
+    port the store bound itself (no probe); the watchdog fires before the
+    driver's 600 s lease."""
+    import bench
+
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--cpu-baseline-seconds", "0"],
+                       capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    names = [v["name"] for v in line["exchange_variants"]]
+    assert names[0] == "sharded" and sorted(names) == sorted(bench.VARIANTS) and len(names) >= 3
+    assert "ncclReduceScatter(uint64) of the partial sum" in line["config"]["workload"]
+    ports = {x["master_port"] for x in line["ranks"]}
+    assert len(ports) == 1 and None not in ports
+    assert 0 < line["watchdog_seconds"] < 600
+    src = open(BENCH).read()
+    assert ".bind(" not in src and "--master-port" not in src.split("def launch_ranks")[1].split("def ")[0]
+    # a subset, and the headline taken from the flags
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--cpu-baseline-seconds", "0",
+                        "--exchange", "reduce", "--variants", "elements"],
+                       capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    assert [v["name"] for v in line["exchange_variants"]] == ["reduce", "elements"]
+
+
+def test_pmc_traffic_keys_on_the_full_instantiation():
+    """roofline.traffic comes from the committed PMC rows of exactly the
+    kernel the bench times: every k_clients instantiation the bench can name
+    resolves to rows of its own (L, X, K), whose bytes are the launch's
+    algorithmic bytes (4 L N read + 8 N written), never the average with
+    another variant's rows (the bipartite <8,0,1> masks-only launch moves
+    16 B per element position, the sum-only <8,0,4> 40 B)."""
+    import csv
+
+    import bench
+
+    n = 10 ** 8
+    for L in (8, 4, 2, 1):  # the per-rank shapes of N = 1, 2, 4, 8
+        X = 8 - L
+        k = bench.kernel_variant(L, X, False)
+        name = f"void sa::k_clients<float, float, {L}, {X}, {k}>"
+        p = bench.pmc_traffic(name, n)
+        assert p is not None, name
+        assert p["rows_matched"] == ("k_clients", L, X, k)
+        alg = 4 * L * n + 8 * n
+        assert abs(p["bytes"] - alg) / alg < 0.01, (name, p["bytes"], alg)
+        assert bench.traffic_field(p, alg)[0] == p["bytes"]
+    p = bench.pmc_traffic("void sa::k_clients<float, float, 8, 0, 4>", n)
+    assert abs(p["bytes"] - 4.0e9) / 4.0e9 < 1e-3
+    b = bench.pmc_traffic("void sa::k_clients<float, float, 8, 0, 1>", n)
+    assert abs(b["bytes"] - 1.6e9) / 1.6e9 < 0.01
+    # every kernel row in the committed files resolves to rows of its own key only
+    for d in bench.PMC_DIRS:
+        path = os.path.join(d, "pmc_fetch_size.csv")
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            keys = {bench.kernel_key(r["Kernel_Name"]) for r in csv.DictReader(f) if "sa::" in r["Kernel_Name"]}
+        assert len(keys) >= 2
+    # a figure below the algorithmic bytes is withheld, with a note
+    t, detail = bench.traffic_field({"bytes": 2.8e9, "read": 2.0e9, "write": 0.8e9}, 4.0e9)
+    assert t is None and "withheld" in detail["note"]

@@ -58,6 +58,13 @@ def test_adapter_maps_devices_and_installs():
         agg.sum([], axis=0)
     with pytest.raises(AssertionError, match="not a participant"):
         agg.sum([FakeObj(FakePYU("mallory"), np.zeros(3))], axis=0)
+    # a device-object weight on another party than its data is refused before
+    # anything is revealed (stateful_fedgen_aggregator.py:74-78)
+    data = [alice(lambda: np.ones(3))(), bob(lambda: np.ones(3))()]
+    with pytest.raises(AssertionError, match="Device of weight does not match"):
+        agg.average(data, axis=0, weights=[bob(lambda: 1)(), bob(lambda: 2)()])
+    with pytest.raises(AssertionError, match="Length of the weights"):
+        agg.average(data, axis=0, weights=[1])
 
 
 @pytest.mark.gpu

@@ -127,10 +127,14 @@ def test_pair01_isa_check_flags_a_broken_alias(tmp_path):
 """
     bad_src = good.replace("v[30:31], s[42:43], v30", "v[30:31], s[42:43], v28")
     bad_add = good.replace("v_add_co_u32_e64 v31, s[44:45], v31", "v_add_co_u32_e64 v29, s[44:45], v29")
+    # the pair's high half overwritten between the mad and its in-place add:
+    # an in-place add on v31 still exists, but it no longer completes this
+    # mad's limb 1 (the order-aware check catches it)
+    bad_order = good.replace("\tv_add_co_u32_e64 v31", "\tv_mov_b32 v31, v5\n\tv_add_co_u32_e64 v31")
     tool = os.path.join(ROOT, "tools", "check_pair01.py")
     rcs = []
-    for i, text in enumerate((good, bad_src, bad_add)):
+    for i, text in enumerate((good, bad_src, bad_add, bad_order)):
         p = tmp_path / f"k{i}.s"
         p.write_text(text)
         rcs.append(subprocess.run([sys.executable, tool, str(p)], capture_output=True).returncode)
-    assert rcs == [0, 1, 1]
+    assert rcs == [0, 1, 1, 1]

@@ -267,7 +267,11 @@ def test_subclass_with_reference_constructor_contract():
     xs = [np.arange(6, dtype=np.float32) * (i + 1) for i in range(2)]
     out = rv(agg.average([p(lambda x=x: x)() for p, x in zip(parties, xs)], axis=0, weights=[1, 1]))
     assert out["generator_params"] == "gen-weights"
-    assert np.allclose(rv(out["model_params"]), (xs[0] + xs[1]) / 2, atol=2 * 2.0**-18)
+    # the subclass averages with weights=None (stateful_fedgen_aggregator.py:59):
+    # bit-exact vs the oracle's unweighted secure average (PRG-independent)
+    exp = o.secure_average(xs, ["a", "b"])[0]
+    assert np.array_equal(rv(out["model_params"]), exp)
+    assert np.allclose(exp, (xs[0] + xs[1]) / 2, atol=2 * 2.0**-18)
 
 
 @pytest.mark.parametrize("as_list", [False, True])

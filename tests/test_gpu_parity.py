@@ -346,6 +346,49 @@ def test_decode_and_divisors():
     assert np.array_equal(out.cpu().numpy(), o.decode(s, 18, dv))
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 1024, 4099, 262_147, 3_000_001])
+@pytest.mark.parametrize("shift", [0, 1])
+def test_server_kernels_sizes_and_alignment(n, shift):
+    """k_decode / k_sum_f64 / k_sum_u64 take 16-B accesses with 4 in flight
+    per lane (an unrolled body, a remainder loop and an odd last element);
+    sub-vectors at odd element offsets (8-B aligned only) take the one-element
+    kernels.  Every size and alignment bit-exact vs the oracle / numpy."""
+    K = _K()
+    rng = np.random.default_rng(n + 7 * shift)
+    s = rng.integers(0, 2**64 - 1, n, dtype=np.uint64)
+    st = torch.from_numpy(s.view(np.int64).copy()).to(DEV)
+    # shift: the buffers start one element into a fresh allocation
+    sb = torch.empty(n + 1, dtype=torch.int64, device=DEV)
+    sb[shift:shift + n] = st
+    sv = sb[shift:shift + n]
+    ob = torch.full((n + 1,), float("nan"), dtype=torch.float64, device=DEV)
+    out = ob[shift:shift + n]
+    K.decode(sv, out, divisor=3.0)
+    dv = rng.integers(1, 100, n).astype(np.float64)
+    dvb = torch.empty(n + 1, dtype=torch.float64, device=DEV)
+    dvb[shift:shift + n] = torch.from_numpy(dv).to(DEV)
+    out2 = torch.empty(n + 1, dtype=torch.float64, device=DEV)[shift:shift + n]
+    K.decode(sv, out2, divisor_vec=dvb[shift:shift + n])
+    ws = [rng.standard_normal(n) for _ in range(3)]
+    wb = []
+    for w in ws:
+        b = torch.empty(n + 1, dtype=torch.float64, device=DEV)
+        b[shift:shift + n] = torch.from_numpy(w).to(DEV)
+        wb.append(b[shift:shift + n])
+    fs = K.sum_f64(wb, torch.empty(n + 1, dtype=torch.float64, device=DEV)[shift:shift + n])
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), o.decode(s, 18, 3.0))
+    assert np.isnan(ob[(n if shift == 0 else 0)].item())  # nothing written past the vector
+    assert np.array_equal(out2.cpu().numpy(), o.decode(s, 18, dv))
+    assert np.array_equal(fs.cpu().numpy(), (ws[0] + ws[1]) + ws[2])
+    if shift == 0:  # sa_sum_u64 needs 16-B aligned buffers
+        ins = [torch.from_numpy(rng.integers(0, 2**64 - 1, n, dtype=np.uint64).view(np.int64)).to(DEV)
+               for _ in range(5)]
+        got = K.sum_u64(ins, torch.empty(n, dtype=torch.int64, device=DEV))
+        torch.cuda.synchronize()
+        assert np.array_equal(_u64(got), o.server_sum([_u64(t) for t in ins]))
+
+
 def test_prg_zero_draw_is_flagged():
     """Force a raw PCG64 draw of 0 (hi == lo after the step) at element 5:
     numpy's Lemire bounded draw would reject it, so the kernel must flag."""
@@ -411,6 +454,12 @@ def test_full_size_properties(C, n):
     assert torch.equal(s, s3)
     assert torch.equal(dig, wdig)
     assert int(flags.item()) == 0
+    # (3a) the bench's own launch (sum-only <C,0,4>) pinned to the oracle
+    # directly: >= 8 windows of 4096 element positions (both ends, the
+    # middle, random offsets), every pair stream jumped to the window start
+    from oracle_windows import check_partial_sum_windows
+
+    assert check_partial_sum_windows(s3, xs, list(range(C)), names, seeds, 0, k_random=6, seed=C) >= 8 * 4096
     # (3) oracle spot checks of individual masked elements at far offsets
     rng = np.random.default_rng(0)
     idx = np.concatenate([[0, 1, n - 1], rng.integers(0, n, 20)])

@@ -2,8 +2,11 @@
 init / reduce / allreduce / destroy through the C-ABI, and the pipelined
 masking + reduce of one rank (multi-rank runs need the 8-GPU node the driver
 uses; the sharding logic is covered by gloo tests)."""
+import json
 import os
-import socket
+import subprocess
+import sys
+import tempfile
 
 import numpy as np
 import pytest
@@ -20,16 +23,17 @@ def comm():
 
     from sfl_amd.parallel_sum import RcclComm
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=0, world_size=1)
+    # a file-store rendezvous: no port to probe (and race for)
+    fd, path = tempfile.mkstemp(prefix="sfl_rccl_store_")
+    os.close(fd)
+    os.unlink(path)
+    dist.init_process_group("gloo", store=dist.FileStore(path, 1), rank=0, world_size=1)
     c = RcclComm(0, 1, 0)
     yield c
     c.close()
     dist.destroy_process_group()
+    if os.path.exists(path):
+        os.unlink(path)
 
 
 def test_rccl_world1_reduce_is_identity(comm):
@@ -159,3 +163,69 @@ def test_sharded_server_pipeline_world1(comm, chunks):
     torch.cuda.synchronize()
     for r in range(2):
         assert np.array_equal(decs[r][:n].cpu().numpy(), exps[r]), r
+
+
+@pytest.mark.parametrize("exchange", ["reduce", "sharded"])
+def test_pipelined_world1_at_1m_matches_oracle_server_sum(comm, exchange):
+    """bench.py --gpus 1 --dist's data path at n = 1,000,003: 8 co-located
+    clients, the bench's 8-chunk pipeline through RcclComm (ncclReduce in
+    place to the root, or the sharded server's ncclReduceScatter + decode),
+    round 2's stream positions; the root's masked sum equals the oracle's
+    server_sum bit for bit, and the sharded decode the oracle's decode."""
+    from oracle import secagg as o
+    from sfl_amd.parallel_sum import PipelinedMaskedSum, plan_generators, plan_rank
+
+    C, n, rnd = 8, 1_000_003, 2
+    names = [f"client{c}" for c in range(C)]
+    seeds = o.seeds_for(names)
+    plan = plan_rank(names, 1, 0)
+    rng = np.random.default_rng(4242)
+    xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
+    exp = o.server_sum(o.secure_masked(xs, names, seeds=seeds, offset=rnd * n))
+    dev = torch.device("cuda", 0)
+    pipe = PipelinedMaskedSum(comm, dev, n, 8, exchange=exchange)
+    assert len(pipe.bounds) == 8
+    seed_of = lambda u, v: seeds[names[u]][names[v]]  # noqa: E731
+    gens = [plan_generators(plan, seed_of, offset=rnd * n + lo) for lo, _ in pipe.bounds]
+    s = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
+    dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev) if exchange == "sharded" else None
+    flags = torch.zeros(1, dtype=torch.int32, device=dev)
+    pipe.run([torch.from_numpy(x).to(dev) for x in xs], [1.0] * C, gens, plan.n_cross, s, None, flags=flags,
+             dec=dec)
+    torch.cuda.synchronize()
+    assert int(flags.item()) == 0
+    assert np.array_equal(s[:n].cpu().numpy().view(np.uint64), exp)
+    if dec is not None:
+        assert np.array_equal(dec[:n].cpu().numpy(), o.decode(exp))
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("opts", [["--exchange", "reduce"], ["--exchange", "sharded", "--gather"]])
+def test_bench_self_launched_dist_world1(opts):
+    """The driver's N>1 bench path on this box's one GPU: `bench.py --gpus 1
+    --dist` starts torchrun as a child process (not an exec), whose rank runs
+    init_process_group("nccl") -> RcclComm -> the pipelined exchange, then
+    times every other design in the same process group.  One JSON line,
+    n_gpus 1, the exchange and all five designs reported."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dist", "--elems",
+                        "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
+                        "--cpu-baseline-seconds", "0", "--watchdog-seconds", "100", *opts],
+                       capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 1 and line["value"] > 0 and line["steps"] == 3
+    ex = line["exchange"]
+    assert ex["chunks"] == 1 and ex["ms_per_step"] > 0 and ex["bytes_per_rank_per_step"] > 0
+    want = "reduce" if opts[1] == "reduce" else "sharded+gather"
+    assert line["config"]["design"] == want
+    names = [v["name"] for v in line["exchange_variants"]]
+    assert names[0] == want and len(names) == 5
+    assert all(v["value"] > 0 and v["kernel_ms_per_step"] > 0 for v in line["exchange_variants"])
+    assert line["roofline"]["kernel"].startswith("k_clients<float, float, 8, 0, 4>")

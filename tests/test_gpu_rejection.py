@@ -68,6 +68,36 @@ def test_rejected_draws_bookkeeping(monkeypatch):
     assert pts == [] and total == 5
 
 
+def test_rejected_draws_many_searches_all_streams_at_once(monkeypatch):
+    """The careful replay's search: one batched find over every stream, then
+    only the streams with a hit are followed; the bookkeeping equals
+    rejected_draws stream by stream."""
+    from sfl_amd import kernels as K
+
+    zeros = {5, 9, 10, 1005, 2000}
+    calls = []
+
+    def adv(gen, d):
+        return gen + d
+
+    def find(gens, n, device):
+        calls.append(len(gens))
+        out = []
+        for start in gens:
+            out.append(next((i for i in range(n) if start + i in zeros), None))
+        return out
+
+    monkeypatch.setattr(K.L, "pcg64_advance", adv)
+    monkeypatch.setattr(K, "find_zero_draws", find)
+    gens = [0, 100, 1000, 1990, 3000]
+    got = K.rejected_draws_many(gens, 20, None)
+    assert calls[0] == len(gens)  # one search over all of them first
+    assert sum(1 for c in calls[1:] if c != 1) == 0  # then per-stream follow-ups only
+    calls.clear()
+    assert got == [K.rejected_draws(g, 20, None) for g in gens]
+    assert [t for _, t in got] == [23, 20, 21, 21, 20]
+
+
 def test_oracle_generator_rejects_zero():
     s, inc = forced_zero_state(5)
     raw = o.pcg64_raw_py(s, inc, 12)

@@ -75,6 +75,7 @@ def test_per_rank_shapes_full_size(W):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from oracle import secagg as o
+    from oracle_windows import check_partial_sum_windows
     from sfl_amd import _lib as L
     from sfl_amd import kernels as K
     from sfl_amd.parallel_sum import PipelinedMaskedSum, plan_generators, plan_rank
@@ -114,6 +115,11 @@ def test_per_rank_shapes_full_size(W):
         pipe.run(local, [1.0] * Lc, gens, plan.n_cross, part_so, None)
         torch.cuda.synchronize()
         assert torch.equal(part_so, part), r
+        # the bench's launches themselves pinned to the oracle: windows of
+        # 4096 at both ends, the middle, across every chunk join and at
+        # random offsets (the <1,7> lean shape at W = 8)
+        assert check_partial_sum_windows(part_so, xs, plan.clients, names, seeds, offset, joins=joins,
+                                         seed=r) >= 8 * 4096
         del part_so
         wire, wdig = [], torch.zeros(Lc, dtype=torch.int64, device=dev)
         for i, c in enumerate(plan.clients):

@@ -33,6 +33,14 @@ would read two SGPRs (bias and borrow), one more than the gfx9 constant bus
 allows; the kernel's schedule orders groups so that no client is first
 touched as a subtracting partner (and presets any that would be).
 
+The s0 / s1 operands are declared as inputs although the pair-writing mad
+overwrites their registers: the inline-asm contract has no way to say "the
+low half of that 64-bit operand", so correctness rests on the register
+allocator placing them in the pair's halves.  tools/check_pair01.py verifies
+that on the ISA of every build (the library's masking kernels and
+tools/microbench/draw_issue); a hipcc upgrade must pass it before its build
+is used, and a failing build leaves no object behind.
+
 usage: python tools/gen_draw2.py > sfl_amd/csrc/sa_draw2.h
 """
 
