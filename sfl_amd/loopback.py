@@ -26,8 +26,10 @@ from __future__ import annotations
 import json
 import os
 import socket
+import threading
 import time
-from concurrent.futures import ThreadPoolExecutor
+from collections import defaultdict
+from contextlib import contextmanager
 
 import numpy as np
 
@@ -35,6 +37,34 @@ from . import wire as W
 from .wire import META
 
 CHUNK_ELEMS = 8 << 20  # 64 MiB of u64 per pinned staging buffer
+
+
+class StageClock:
+    """Wall and thread-CPU seconds (user + system, so the kernel's socket
+    copies count) per named stage of a round, summed over the threads that
+    ran it: the host-side profile of the loopback path
+    (tools/loopback_bench.py --stages)."""
+
+    def __init__(self):
+        self._t = defaultdict(lambda: [0.0, 0.0, 0])
+        self._lock = threading.Lock()
+
+    @contextmanager
+    def __call__(self, name: str):
+        w0, c0 = time.perf_counter(), time.thread_time()
+        try:
+            yield
+        finally:
+            w, c = time.perf_counter() - w0, time.thread_time() - c0
+            with self._lock:
+                e = self._t[name]
+                e[0] += w
+                e[1] += c
+                e[2] += 1
+
+    def report(self) -> dict:
+        with self._lock:
+            return {k: {"wall_s": v[0], "cpu_s": v[1], "calls": v[2]} for k, v in sorted(self._t.items())}
 
 
 def chunk_elems() -> int:
@@ -126,6 +156,7 @@ class LoopbackServer:
         done_rx = [0]  # receivers finished (an empty frame has no chunks)
         ready = [threading.Event() for _ in range(J)]
         stamps = {}
+        clock = StageClock()
 
         def receive(i):
             try:
@@ -142,19 +173,22 @@ class LoopbackServer:
                     k, e0 = nbytes // 8, off // 8
                     if verify_digest:
                         dig[0] ^= W.xor_digest(ring[i][b].numpy()[:k])
-                    with torch.cuda.stream(streams[i]):
-                        devb[i][e0:e0 + k].copy_(ring[i][b][:k], non_blocking=True)
-                        events[b] = torch.cuda.Event()
-                        events[b].record(streams[i])
+                    with clock("server: H2D enqueue (pinned ring -> GPU)"):
+                        with torch.cuda.stream(streams[i]):
+                            devb[i][e0:e0 + k].copy_(ring[i][b][:k], non_blocking=True)
+                            events[b] = torch.cuda.Event()
+                            events[b].record(streams[i])
                     with cond:
                         j = e0 // ce
                         ev_in[i][j] = events[b]
                         arrived[j] += 1
                         cond.notify_all()
                     if events[1 - b] is not None:  # the other buffer is received into next
-                        events[1 - b].synchronize()
+                        with clock("server: wait for the ring buffer's H2D"):
+                            events[1 - b].synchronize()
 
-                W.recv_payload_chunked(conn, h, ring[i], on_chunk)
+                with clock("server: receive thread total (socket recv_into the pinned ring + the above)"):
+                    W.recv_payload_chunked(conn, h, ring[i], on_chunk)
                 if verify_digest and h.digest != dig[0]:
                     raise W.WireError(f"client {i}: payload digest mismatch")
                 with cond:
@@ -171,12 +205,14 @@ class LoopbackServer:
                 conn.sendall(W.pack_header(W.RESULT, W.F64, 0, rnd, n))
                 host = res_host.numpy()
                 for j, (lo, hi) in enumerate(bounds):
-                    if not ready[j].wait(timeout):
-                        raise TimeoutError(f"result chunk {j} not ready")
+                    with clock("server: send thread waits for a result chunk"):
+                        if not ready[j].wait(timeout):
+                            raise TimeoutError(f"result chunk {j} not ready")
                     if errors:
                         return
                     if hi > lo:
-                        conn.sendall(memoryview(host[lo:hi]).cast("B"))
+                        with clock("server: broadcast send (pinned result -> socket)"):
+                            conn.sendall(memoryview(host[lo:hi]).cast("B"))
             except BaseException as e:  # noqa: BLE001
                 with cond:
                     errors.append(e)
@@ -191,7 +227,7 @@ class LoopbackServer:
         try:
             div = None
             for j, (lo, hi) in enumerate(bounds):
-                with cond:
+                with clock("server: wait for chunk j of every client"), cond:
                     if not cond.wait_for(lambda: errors or arrived[j] == C or done_rx[0] == C, timeout):
                         raise TimeoutError(f"chunk {j} not received from every client")
                     if errors:
@@ -213,11 +249,13 @@ class LoopbackServer:
                         res_host[lo:hi].copy_(dec[lo:hi], non_blocking=True)
                     e = torch.cuda.Event()
                     e.record(agg)
-                e.synchronize()
+                with clock("server: sum + decode + D2H of the chunk (GPU)"):
+                    e.synchronize()
                 ready[j].set()
                 # copy the chunk out of the pinned buffer while it is broadcast
                 # and later chunks arrive (no 8n-byte copy after the round)
-                out[lo:hi] = res_np[lo:hi]
+                with clock("server: copy-out (pinned result -> caller's array, memcpy)"):
+                    out[lo:hi] = res_np[lo:hi]
             stamps["recv_done"] = time.perf_counter()
             for t in rx + tx:
                 t.join(timeout)
@@ -241,7 +279,7 @@ class LoopbackServer:
         return out, {"first_chunk_all_s": stamps["first_chunk_all"] - t0,
                      "recv_sum_decode_s": stamps["recv_done"] - t0,
                      "broadcast_tail_s": t_end - stamps["recv_done"],
-                     "round_s": t_end - t0, "chunks": J}
+                     "round_s": t_end - t0, "chunks": J, "stages": clock.report()}
 
     def close(self):
         for c in self.conns:
@@ -312,14 +350,17 @@ class LoopbackClient:
         dev = dx.device
         ce = hx[0].numel()
         xf = np.asarray(x, dtype=np.float32).reshape(-1)
+        clock = StageClock()
         t0 = time.perf_counter()
         ev = [None, None]
         with torch.cuda.stream(cs):
             for j, lo in enumerate(range(0, n, ce)):
                 b, k = j & 1, min(ce, n - lo)
                 if ev[b] is not None:
-                    ev[b].synchronize()
-                hx[b].numpy()[:k] = xf[lo:lo + k]
+                    with clock("client: wait for the staging buffer's H2D"):
+                        ev[b].synchronize()
+                with clock("client: stage in (numpy -> pinned, memcpy)"):
+                    hx[b].numpy()[:k] = xf[lo:lo + k]
                 dx[lo:lo + k].copy_(hx[b][:k], non_blocking=True)
                 ev[b] = torch.cuda.Event()
                 ev[b].record(cs)
@@ -331,7 +372,8 @@ class LoopbackClient:
             else:
                 K.mask_dp(dx, dm, self.masker.streams(), dp.params(dp.sumsq([dx]), n), weight=w,
                           fxp_bits=self.fxp_bits, digest=dig, flags=flags)
-        cs.synchronize()
+        with clock("client: last H2D + mask kernel (GPU)"):
+            cs.synchronize()
         extra = {}
         if int(flags.item()) & L.SA_FLAG_PRG_REJECT:
             # numpy's Generator.integers rejected a raw 0 on some stream: move
@@ -364,15 +406,20 @@ class LoopbackClient:
                 ev[b].record(cs)
                 if pending is not None:  # send the previous chunk while this one copies
                     pb, pk = pending
-                    ev[pb].synchronize()
-                    self.sock.sendall(memoryview(hm[pb].numpy()[:pk]).cast("B"))
+                    with clock("client: wait for a chunk's D2H"):
+                        ev[pb].synchronize()
+                    with clock("client: send (pinned masked vector -> socket)"):
+                        self.sock.sendall(memoryview(hm[pb].numpy()[:pk]).cast("B"))
                 pending = (b, k)
             if pending is not None:
                 pb, pk = pending
-                ev[pb].synchronize()
-                self.sock.sendall(memoryview(hm[pb].numpy()[:pk]).cast("B"))
+                with clock("client: wait for a chunk's D2H"):
+                    ev[pb].synchronize()
+                with clock("client: send (pinned masked vector -> socket)"):
+                    self.sock.sendall(memoryview(hm[pb].numpy()[:pk]).cast("B"))
         t2 = time.perf_counter()
-        return {"h2d_mask_s": t1 - t0, "d2h_send_s": t2 - t1}
+        self.last_stages = clock.report()
+        return {"h2d_mask_s": t1 - t0, "d2h_send_s": t2 - t1, "stages": self.last_stages}
 
     def result(self, n: int | None = None, into: np.ndarray | None = None) -> np.ndarray:
         """The server's float64 aggregate (``n`` elements when given: a larger
@@ -387,7 +434,9 @@ class LoopbackClient:
             return W.as_array(h, mv).copy()
         if into.dtype != np.float64 or not into.flags.c_contiguous:
             raise ValueError("result buffer must be a contiguous float64 array")
+        w0, c0 = time.perf_counter(), time.thread_time()
         h, _ = W.recv_frame(self.sock, into, expect_kind=W.RESULT)
+        self.last_result_recv = {"wall_s": time.perf_counter() - w0, "cpu_s": time.thread_time() - c0}
         if h.dtype != W.F64 or (n is not None and h.count != int(n)):
             raise W.WireError(f"RESULT frame of {h.count} elements (dtype {h.dtype}), want {n} float64")
         return into[:h.count]
@@ -426,6 +475,8 @@ def client_process(parties: list, port: int, n: int, rounds: int, gpu: int, fxp_
                 if r:  # the previous result's checksum, after this round's submit
                     stats[-1]["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))
                 cl.result(n, into=res)
+                st["stages"]["client: result recv (socket -> numpy, incl. waiting for the server)"] = dict(
+                    cl.last_result_recv, calls=1)
                 stats.append(st)
             if stats:
                 stats[-1]["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))

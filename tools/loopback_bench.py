@@ -17,6 +17,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def _median_stages(reports):
+    import numpy as np
+
+    names = sorted({k for r in reports for k in r})
+    return {k: {f: float(np.median([r[k][f] for r in reports if k in r])) for f in ("wall_s", "cpu_s", "calls")}
+            for k in names}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--clients", type=int, default=8)
@@ -50,7 +58,12 @@ def main():
         "clients": args.clients, "elems_per_client": args.elems, "rounds": args.rounds,
         "period_s": period, "grad_elems_per_s": args.clients * args.elems / period,
         "round_s_median": rs,
-        "server": {k: float(np.median([t[k] for t in steady])) for k in steady[0] if k != "t_start"},
+        "server": {k: float(np.median([t[k] for t in steady])) for k in steady[0] if k not in ("t_start", "stages")},
+        # host-side profile (sfl_amd.loopback.StageClock): wall and thread-CPU
+        # seconds per named copy / wait, summed over the threads that ran it,
+        # median over the steady rounds (server) or over clients x rounds
+        "server_stages": _median_stages([t["stages"] for t in steady]),
+        "client_stages": _median_stages([s["stages"] for s in cl]),
         "client_h2d_mask_s_median": float(np.median([s["h2d_mask_s"] for s in cl])),
         "client_d2h_send_s_median": float(np.median([s["d2h_send_s"] for s in cl])),
         "parties_per_process": args.parties_per_process,
