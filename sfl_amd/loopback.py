@@ -19,6 +19,14 @@ RayFed actor transport of the reference (``sfl/distributed/op_strategy.py:131-14
 This is the path that "starts and ends in host memory" (BASELINE north
 star): the per-round rate here includes H2D, D2H and the loopback copies.
 The GPU kernels are the product path; nothing here falls back to the CPU.
+
+Host buffers that leave through a socket (every client's masked vector, the
+server's float64 result) are ``SharedHostBuffer``s: memfd-backed pages that
+are HIP-registered, so the D2H copy lands in them directly, and that are
+sent with ``os.sendfile`` -- the kernel hands the page references to the
+socket instead of copying them in, so a byte crossing 127.0.0.1 is copied
+once (into the receiver) instead of twice.  tools/socket_floor.py measures
+the transport with and without it.
 """
 
 from __future__ import annotations
@@ -65,6 +73,115 @@ class StageClock:
     def report(self) -> dict:
         with self._lock:
             return {k: {"wall_s": v[0], "cpu_s": v[1], "calls": v[2]} for k, v in sorted(self._t.items())}
+
+
+# Knobs for same-box A/B measurements of the host path (tools/loopback_bench.py
+# --ab); the defaults are the product's choices.
+#   SFL_LOOPBACK_SEND=sendfile|copy   sendfile() from the memfd pages, or sendall() (a copy into the kernel)
+#   SFL_LOOPBACK_WAIT=poll|spin       wait for a GPU event by polling with short sleeps, or in hipEventSynchronize
+def _send_mode() -> str:
+    return os.environ.get("SFL_LOOPBACK_SEND", "sendfile")
+
+
+def wait_event(e) -> None:
+    """Wait for a recorded GPU event.  hipEventSynchronize spins a CPU core
+    for the whole wait; the loopback party runs ~20 threads per process
+    against the box's CPU share, so a wait polls with ~50 us sleeps instead
+    and leaves the core to the socket copies."""
+    if os.environ.get("SFL_LOOPBACK_WAIT", "poll") == "spin":
+        e.synchronize()
+        return
+    while not e.query():
+        time.sleep(50e-6)
+
+
+_HIP = None
+
+
+def _hip():
+    global _HIP
+    if _HIP is None:
+        import ctypes
+
+        _HIP = ctypes.CDLL("libamdhip64.so")
+    return _HIP
+
+
+class SharedHostBuffer:
+    """``nbytes`` of memfd-backed host memory, mapped, faulted in and
+    HIP-registered (hipHostRegister): device copies land in it directly (torch
+    sees it as pinned), and ``send(sock, lo, hi)`` ships a byte range with
+    ``os.sendfile`` -- page references handed to the socket, no send-side
+    copy.  The pages must not change until the peer has read them; the
+    round protocol guarantees that (a party writes a buffer again only after
+    every peer answered the frame that carried it)."""
+
+    def __init__(self, nbytes: int, dtype=np.float64):
+        import ctypes
+        import mmap
+
+        self.nbytes = max(int(nbytes), 8)
+        self.fd = os.memfd_create("sfl_sa_wire", os.MFD_CLOEXEC)
+        try:
+            os.ftruncate(self.fd, self.nbytes)
+            self._mm = mmap.mmap(self.fd, self.nbytes)
+        except BaseException:
+            os.close(self.fd)
+            raise
+        self.array = np.frombuffer(self._mm, dtype=dtype)
+        self.array.view(np.uint8)[:] = 0  # fault every page in before registering
+        self._ptr = self.array.ctypes.data
+        rc = _hip().hipHostRegister(ctypes.c_void_p(self._ptr), ctypes.c_size_t(self.nbytes), ctypes.c_uint(0))
+        if rc != 0:
+            self._close_map()
+            raise RuntimeError(f"hipHostRegister of a {self.nbytes}-byte memfd buffer failed (hipError {rc})")
+        self._registered = True
+
+    def tensor(self):
+        import torch
+
+        return torch.from_numpy(self.array)
+
+    def send(self, sock: socket.socket, lo: int, hi: int) -> None:
+        """Send bytes [lo, hi) of the buffer (socket.sendfile: os.sendfile
+        plus the wait for a full socket buffer that a socket with a timeout,
+        i.e. a non-blocking descriptor, needs)."""
+        if hi <= lo:
+            return
+        if _send_mode() == "copy":
+            sock.sendall(memoryview(self.array).cast("B")[lo:hi])
+            return
+        f = open(self.fd, "rb", buffering=0, closefd=False)  # a file object on the memfd (no new open)
+        try:
+            sent = sock.sendfile(f, lo, hi - lo)
+        finally:
+            f.close()
+        if sent != hi - lo:
+            raise W.WireError(f"sendfile sent {sent} of {hi - lo} bytes (peer closed?)")
+
+    def _close_map(self):
+        self.array = None
+        try:
+            self._mm.close()
+        except BufferError:  # a view of the pages is still alive: the mapping goes with it
+            pass
+        os.close(self.fd)
+        self.fd = -1
+
+    def close(self):
+        if getattr(self, "_registered", False):
+            import ctypes
+
+            _hip().hipHostUnregister(ctypes.c_void_p(self._ptr))
+            self._registered = False
+        if getattr(self, "fd", -1) >= 0:
+            self._close_map()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
 
 
 def chunk_elems() -> int:
@@ -119,14 +236,18 @@ class LoopbackServer:
             ring = [[torch.empty(ce, dtype=torch.int64).pin_memory() for _ in range(2)] for _ in self.conns]
             devb = [torch.empty(n, dtype=torch.int64, device=dev) for _ in self.conns]
             streams = [torch.cuda.Stream(dev) for _ in self.conns]
+            # the float64 result: D2H straight into memfd pages the broadcast sendfile()s
             agg = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.float64, device=dev),
-                   torch.empty(n, dtype=torch.float64).pin_memory(), torch.cuda.Stream(dev))
+                   SharedHostBuffer(8 * n, np.float64), torch.cuda.Stream(dev))
             self._bufs = (n, ring, devb, streams, agg)
         return self._bufs[1:]
 
     def round(self, n: int, rnd: int, *, average: bool = False, verify_digest: bool = False,
-              keep_masked: bool = False, timeout: float = 600.0):
+              keep_masked: bool = False, timeout: float = 600.0, copy_out: bool = True):
         """One aggregation round over n-element vectors -> (float64 result, timings).
+
+        ``copy_out=False`` returns the server's own result buffer (the pages the
+        broadcast sent) instead of a copy: valid until the next round().
 
         Pipelined per chunk (chunk_elems() elements): every connection's frame
         streams through a ring of two pinned buffers and each chunk is copied
@@ -142,7 +263,8 @@ class LoopbackServer:
 
         from . import kernels as K
 
-        ring, devb, streams, (s_sum, dec, res_host, agg) = self._buffers(n)
+        ring, devb, streams, (s_sum, dec, res_shb, agg) = self._buffers(n)
+        res_host = res_shb.tensor()
         C = len(self.conns)
         ce = ring[0][0].numel()
         bounds = [(lo, min(n, lo + ce)) for lo in range(0, n, ce)] or [(0, 0)]
@@ -185,7 +307,7 @@ class LoopbackServer:
                         cond.notify_all()
                     if events[1 - b] is not None:  # the other buffer is received into next
                         with clock("server: wait for the ring buffer's H2D"):
-                            events[1 - b].synchronize()
+                            wait_event(events[1 - b])
 
                 with clock("server: receive thread total (socket recv_into the pinned ring + the above)"):
                     W.recv_payload_chunked(conn, h, ring[i], on_chunk)
@@ -203,7 +325,6 @@ class LoopbackServer:
             try:
                 conn = self.conns[i]
                 conn.sendall(W.pack_header(W.RESULT, W.F64, 0, rnd, n))
-                host = res_host.numpy()
                 for j, (lo, hi) in enumerate(bounds):
                     with clock("server: send thread waits for a result chunk"):
                         if not ready[j].wait(timeout):
@@ -211,15 +332,15 @@ class LoopbackServer:
                     if errors:
                         return
                     if hi > lo:
-                        with clock("server: broadcast send (pinned result -> socket)"):
-                            conn.sendall(memoryview(host[lo:hi]).cast("B"))
+                        with clock("server: broadcast sendfile (memfd result pages -> socket, no copy)"):
+                            res_shb.send(conn, 8 * lo, 8 * hi)
             except BaseException as e:  # noqa: BLE001
                 with cond:
                     errors.append(e)
                     cond.notify_all()
 
-        out = np.empty(n, dtype=np.float64)  # the caller's copy, filled chunk by chunk below
-        res_np = res_host.numpy()
+        res_np = res_shb.array[:n]
+        out = np.empty(n, dtype=np.float64) if copy_out else res_np  # the caller's copy, filled chunk by chunk
         rx = [threading.Thread(target=receive, args=(i,), daemon=True) for i in range(C)]
         tx = [threading.Thread(target=send, args=(i,), daemon=True) for i in range(C)]
         for t in rx + tx:
@@ -250,12 +371,13 @@ class LoopbackServer:
                     e = torch.cuda.Event()
                     e.record(agg)
                 with clock("server: sum + decode + D2H of the chunk (GPU)"):
-                    e.synchronize()
+                    wait_event(e)
                 ready[j].set()
-                # copy the chunk out of the pinned buffer while it is broadcast
+                # copy the chunk out of the result pages while it is broadcast
                 # and later chunks arrive (no 8n-byte copy after the round)
-                with clock("server: copy-out (pinned result -> caller's array, memcpy)"):
-                    out[lo:hi] = res_np[lo:hi]
+                if copy_out:
+                    with clock("server: copy-out (result pages -> caller's array, memcpy)"):
+                        out[lo:hi] = res_np[lo:hi]
             stamps["recv_done"] = time.perf_counter()
             for t in rx + tx:
                 t.join(timeout)
@@ -289,6 +411,9 @@ class LoopbackServer:
             except OSError:
                 pass
         self.sock.close()
+        if self._bufs is not None:
+            self._bufs[4][2].close()
+            self._bufs = None
 
 
 class LoopbackClient:
@@ -305,6 +430,7 @@ class LoopbackClient:
         self.sock = socket.create_connection((host, port), timeout=300)
         self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         self._bufs = None
+        self._rx = None  # the result receiver of the round in flight (submit(result_into=...))
 
     def handshake(self):
         hello = {"party": self.party, "index": self.index, "public_key": self.masker.public_key}
@@ -329,24 +455,58 @@ class LoopbackClient:
         if self._bufs is None or self._bufs[0] != n:
             dev = torch.device("cuda", self.gpu)
             ce = min(n, chunk_elems())
+            if self._bufs is not None:
+                self._bufs[2].close()
+            # the masked vector: D2H straight into memfd pages that are sendfile()d
             self._bufs = (n, [torch.empty(ce, dtype=torch.float32).pin_memory() for _ in range(2)],
-                          [torch.empty(ce, dtype=torch.int64).pin_memory() for _ in range(2)],
+                          SharedHostBuffer(8 * n, np.int64),
                           torch.empty(n, dtype=torch.float32, device=dev),
                           torch.empty(n, dtype=torch.int64, device=dev), torch.cuda.Stream(dev))
         return self._bufs[1:]
 
-    def submit(self, x: np.ndarray, rnd: int, weight=None, dp=None) -> dict:
+    def _receive_result(self, n, into, box):
+        try:
+            w0, c0 = time.perf_counter(), time.thread_time()
+            h, _ = W.recv_frame(self.sock, into, expect_kind=W.RESULT)
+            if h.dtype != W.F64 or h.count != int(n):
+                raise W.WireError(f"RESULT frame of {h.count} elements (dtype {h.dtype}), want {n} float64")
+            box["h"] = h
+            self.last_result_recv = {"wall_s": time.perf_counter() - w0, "cpu_s": time.thread_time() - c0}
+        except BaseException as e:  # noqa: BLE001 - re-raised by result()
+            box["error"] = e
+
+    def submit(self, x: np.ndarray, rnd: int, weight=None, dp=None, result_into: np.ndarray | None = None) -> dict:
         """Mask ``x`` (host float32) for round ``rnd`` and send it.  With a
         ``GaussianModelDP`` ``dp``, its clip + noise runs inside the masking
-        kernel (``sa_mask_dp``) on the device copy of ``x``.  Host <-> device
-        copies stream through two pinned chunk buffers each way."""
+        kernel (``sa_mask_dp``) on the device copy of ``x``.  ``x`` streams to
+        the device through two pinned chunk buffers; the masked vector comes
+        back chunk by chunk into memfd pages that are sendfile()d as each
+        chunk lands.
+
+        ``result_into`` (float64, n elements): the round's RESULT frame is
+        received into it by a thread started now, while this party is still
+        sending -- the server broadcasts chunk j as soon as it has chunk j of
+        every party, and a party that read only after sending everything
+        would leave both directions of its connection full at once (on the
+        GPU box's kernel that stalls sendfile()d transfers, tools/socket_floor.py
+        --client-sequential).  ``result()`` then joins it."""
         import torch
 
         from . import _lib as L
         from . import kernels as K
 
         n = x.size
-        hx, hm, dx, dm, cs = self._buffers(n)
+        if self._rx is not None:
+            raise RuntimeError("the previous round's result was not collected (result())")
+        if result_into is not None:
+            if result_into.dtype != np.float64 or not result_into.flags.c_contiguous or result_into.size < n:
+                raise ValueError("result_into must be a contiguous float64 array of at least n elements")
+            box = {}
+            t = threading.Thread(target=self._receive_result, args=(n, result_into[:n], box), daemon=True)
+            t.start()
+            self._rx = (t, box, result_into[:n], n)
+        hx, hmb, dx, dm, cs = self._buffers(n)
+        hm = hmb.tensor()
         dev = dx.device
         ce = hx[0].numel()
         xf = np.asarray(x, dtype=np.float32).reshape(-1)
@@ -358,7 +518,7 @@ class LoopbackClient:
                 b, k = j & 1, min(ce, n - lo)
                 if ev[b] is not None:
                     with clock("client: wait for the staging buffer's H2D"):
-                        ev[b].synchronize()
+                        wait_event(ev[b])
                 with clock("client: stage in (numpy -> pinned, memcpy)"):
                     hx[b].numpy()[:k] = xf[lo:lo + k]
                 dx[lo:lo + k].copy_(hx[b][:k], non_blocking=True)
@@ -396,27 +556,21 @@ class LoopbackClient:
         W.send_frame(self.sock, META, json.dumps({"weight": weight}).encode(), sender=self.index, rnd=rnd)
         self.sock.sendall(W.pack_header(W.MASKED, W.U64, self.index, rnd, n,
                                         int(dig.cpu().numpy().view(np.uint64)[0])))
-        ev = [None, None]
-        pending = None
+        # every chunk's D2H enqueued at once (each lands in its own pages);
+        # a chunk is sent as soon as its copy has finished
+        chunks = []
         with torch.cuda.stream(cs):
-            for j, lo in enumerate(range(0, n, ce)):
-                b, k = j & 1, min(ce, n - lo)
-                hm[b][:k].copy_(dm[lo:lo + k], non_blocking=True)
-                ev[b] = torch.cuda.Event()
-                ev[b].record(cs)
-                if pending is not None:  # send the previous chunk while this one copies
-                    pb, pk = pending
-                    with clock("client: wait for a chunk's D2H"):
-                        ev[pb].synchronize()
-                    with clock("client: send (pinned masked vector -> socket)"):
-                        self.sock.sendall(memoryview(hm[pb].numpy()[:pk]).cast("B"))
-                pending = (b, k)
-            if pending is not None:
-                pb, pk = pending
-                with clock("client: wait for a chunk's D2H"):
-                    ev[pb].synchronize()
-                with clock("client: send (pinned masked vector -> socket)"):
-                    self.sock.sendall(memoryview(hm[pb].numpy()[:pk]).cast("B"))
+            for lo in range(0, n, ce):
+                hi = min(n, lo + ce)
+                hm[lo:hi].copy_(dm[lo:hi], non_blocking=True)
+                e = torch.cuda.Event()
+                e.record(cs)
+                chunks.append((lo, hi, e))
+        for lo, hi, e in chunks:
+            with clock("client: wait for a chunk's D2H"):
+                wait_event(e)
+            with clock("client: sendfile (memfd masked-vector pages -> socket, no copy)"):
+                hmb.send(self.sock, 8 * lo, 8 * hi)
         t2 = time.perf_counter()
         self.last_stages = clock.report()
         return {"h2d_mask_s": t1 - t0, "d2h_send_s": t2 - t1, "stages": self.last_stages}
@@ -427,6 +581,15 @@ class LoopbackClient:
         payload is received straight into the returned array -- ``into``
         (float64, reused across rounds by a caller that consumes each result
         before the next) or a fresh one -- with no intermediate copy."""
+        if self._rx is not None:  # received concurrently with submit(result_into=...)
+            t, box, buf, rn = self._rx
+            self._rx = None
+            t.join()
+            if "error" in box:
+                raise box["error"]
+            if n is not None and int(n) != rn:
+                raise W.WireError(f"RESULT of {rn} elements, want {n}")
+            return buf
         if into is None and n is not None:
             into = np.empty(int(n), dtype=np.float64)
         if into is None:
@@ -446,6 +609,9 @@ class LoopbackClient:
             self.sock.close()
         except OSError:
             pass
+        if self._bufs is not None:
+            self._bufs[2].close()
+            self._bufs = None
 
 
 # ---------------------------------------------------------------------------
@@ -463,23 +629,31 @@ def client_process(parties: list, port: int, n: int, rounds: int, gpu: int, fxp_
     its own socket and thread."""
     import threading
 
+    dump_after = float(os.environ.get("SFL_LOOPBACK_DUMP_AFTER", "0"))
+    if dump_after > 0:  # diagnostics: every thread's stack if the process is still here then
+        import faulthandler
+
+        faulthandler.dump_traceback_later(dump_after, exit=False)
+
     def run(party, index, seeds, weight):
         try:
             xs = [synthetic_gradient(index, n, r) for r in range(rounds)]  # generated outside the rounds
             cl = LoopbackClient(party, index, port, gpu=gpu, fxp_bits=fxp_bits, seeds=seeds)
             cl.handshake()
             stats = []
-            res = np.empty(n, dtype=np.float64)  # one receive buffer for every round
+            # two receive buffers, alternating: round r's result arrives while
+            # round r-1's is checksummed
+            res = [np.empty(n, dtype=np.float64) for _ in range(2)]
             for r in range(rounds):
-                st = cl.submit(xs[r], r, weight)
+                st = cl.submit(xs[r], r, weight, result_into=res[r & 1])
                 if r:  # the previous result's checksum, after this round's submit
-                    stats[-1]["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))
-                cl.result(n, into=res)
-                st["stages"]["client: result recv (socket -> numpy, incl. waiting for the server)"] = dict(
+                    stats[-1]["result_xor"] = int(np.bitwise_xor.reduce(res[(r - 1) & 1].view(np.uint64)))
+                cl.result(n)
+                st["stages"]["client: result recv thread (socket -> numpy, from the start of submit)"] = dict(
                     cl.last_result_recv, calls=1)
                 stats.append(st)
             if stats:
-                stats[-1]["result_xor"] = int(np.bitwise_xor.reduce(res.view(np.uint64)))
+                stats[-1]["result_xor"] = int(np.bitwise_xor.reduce(res[(rounds - 1) & 1].view(np.uint64)))
             W.recv_header(cl.sock, expect_kind=W.BYE)
             cl.close()
             out_q.put((index, "ok", stats))
@@ -495,10 +669,14 @@ def client_process(parties: list, port: int, n: int, rounds: int, gpu: int, fxp_
 
 def run_loopback(names: list[str], n: int, rounds: int = 1, *, seeds: dict | None = None, weights=None,
                  average: bool = False, gpu: int = 0, fxp_bits: int = 18, keep_masked: bool = False,
-                 verify_digest: bool = False, timeout: float = 600.0, parties_per_process: int = 1):
+                 verify_digest: bool = False, timeout: float = 600.0, parties_per_process: int = 1,
+                 keep_results: bool = True):
     """Spawn the client parties (``parties_per_process`` per OS process), run
     ``rounds`` rounds with this process as the server.  Returns (results per
-    round, server timings, client stats, received masked vectors)."""
+    round, server timings, client stats, received masked vectors).
+    ``keep_results=False``: the server keeps no copy of each round's result
+    (results holds None per round; every client checksums what it received,
+    ``stats[i][r]["result_xor"]``)."""
     import multiprocessing as mp
 
     ctx = mp.get_context("spawn")
@@ -519,9 +697,10 @@ def run_loopback(names: list[str], n: int, rounds: int = 1, *, seeds: dict | Non
         srv.accept(timeout=timeout)
         for r in range(rounds):
             t_start = time.perf_counter()
-            out, t = srv.round(n, r, average=average, keep_masked=keep_masked, verify_digest=verify_digest)
+            out, t = srv.round(n, r, average=average, keep_masked=keep_masked, verify_digest=verify_digest,
+                               copy_out=keep_results)
             t["t_start"] = t_start  # successive starts give the steady-state period (copy-out included)
-            results.append(out)
+            results.append(out if keep_results else None)
             timings.append(t)
             if keep_masked:
                 masked.append(srv.last_masked)

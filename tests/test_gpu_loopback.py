@@ -95,3 +95,26 @@ def test_loopback_client_reproduces_numpy_rejection():
         assert np.array_equal(res[r], o.decode(ssum)), r
         for c in range(len(names)):
             assert np.array_equal(masked[r][c], m[c]), (r, c)
+
+
+def test_loopback_sendfile_chunks_without_server_copy(monkeypatch):
+    """The sendfile transport over many chunks (masked vectors D2H into
+    memfd pages chunk by chunk, sendfile'd as each lands; the result D2H'd
+    into the server's memfd pages and broadcast from them), with no server
+    copy of the result (keep_results=False): every client received the
+    oracle's float64 result, round after round, with the streams advancing."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.loopback import run_loopback, synthetic_gradient
+
+    monkeypatch.setenv("SFL_LOOPBACK_CHUNK_ELEMS", "8192")  # 9 chunks; the spawned clients inherit it
+    names = ["p0", "p1", "p2", "p3"]
+    n, rounds = 70_001, 3
+    seeds = o.seeds_for(names)
+    res, _, stats, _ = run_loopback(names, n, rounds, seeds=seeds, keep_results=False, timeout=300)
+    assert res == [None] * rounds
+    for r in range(rounds):
+        xs = [synthetic_gradient(c, n, r) for c in range(len(names))]
+        exp = o.secure_sum(xs, names, seeds=seeds, offset=r * n)[0]
+        want = int(np.bitwise_xor.reduce(exp.view(np.uint64)))
+        assert [stats[c][r]["result_xor"] for c in range(len(names))] == [want] * len(names), r

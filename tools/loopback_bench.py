@@ -32,44 +32,77 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--parties-per-process", type=int, default=1,
                     help="client parties hosted per OS process (config 5: 32 clients as 8 x 4)")
+    ap.add_argument("--ab", type=int, default=0,
+                    help="A/B passes over the host-path knobs (SFL_LOOPBACK_SEND x SFL_LOOPBACK_WAIT), one line "
+                         "per run")
+    ap.add_argument("--dump-after", type=float, default=0.0,
+                    help="diagnostics: dump every thread's stack (server and client processes) after this many "
+                         "seconds")
     args = ap.parse_args()
     import numpy as np
+
+    if args.dump_after > 0:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(args.dump_after, exit=False)
+        os.environ["SFL_LOOPBACK_DUMP_AFTER"] = str(args.dump_after)
 
     from sfl_amd.loopback import run_loopback
 
     names = [f"client{c}" for c in range(args.clients)]
     seeds = {a: {b: (0x5ECA66 << 32) | (min(i, j) << 16) | max(i, j) for j, b in enumerate(names) if b != a}
              for i, a in enumerate(names)}
-    res, timings, stats, _ = run_loopback(names, args.elems, args.rounds, seeds=seeds, timeout=900,
-                                          parties_per_process=args.parties_per_process)
-    steady = timings[1:] if len(timings) > 1 else timings
-    rs = float(np.median([t["round_s"] for t in steady]))
-    # the rate: wall time from the start of round 1 (round 0 warms up) to the
-    # end of the last round, per round -- it counts the parties' turnaround
-    # between rounds as well as the server's rounds; one round: its time
-    if len(timings) > 1:
-        span = timings[-1]["t_start"] + timings[-1]["round_s"] - timings[1]["t_start"]
-        period = span / (len(timings) - 1)
-    else:
-        period = rs
-    cl = [s for per in stats.values() for s in per[1:] or per]
-    out = {
-        "metric": "host-resident grad elems/s (loopback sockets, H2D/D2H inclusive)",
-        "clients": args.clients, "elems_per_client": args.elems, "rounds": args.rounds,
-        "period_s": period, "grad_elems_per_s": args.clients * args.elems / period,
-        "round_s_median": rs,
-        "server": {k: float(np.median([t[k] for t in steady])) for k in steady[0] if k not in ("t_start", "stages")},
-        # host-side profile (sfl_amd.loopback.StageClock): wall and thread-CPU
-        # seconds per named copy / wait, summed over the threads that ran it,
-        # median over the steady rounds (server) or over clients x rounds
-        "server_stages": _median_stages([t["stages"] for t in steady]),
-        "client_stages": _median_stages([s["stages"] for s in cl]),
-        "client_h2d_mask_s_median": float(np.median([s["h2d_mask_s"] for s in cl])),
-        "client_d2h_send_s_median": float(np.median([s["d2h_send_s"] for s in cl])),
-        "parties_per_process": args.parties_per_process,
-        "wire_bytes_per_round": args.clients * args.elems * 8,
-    }
-    print(json.dumps(out))
+
+    def one_run():
+        res, timings, stats, _ = run_loopback(names, args.elems, args.rounds, seeds=seeds, timeout=900,
+                                              parties_per_process=args.parties_per_process, keep_results=False)
+        # no server-side copy of the results: every client must have received the same bytes
+        xors = [{s[r]["result_xor"] for s in stats.values()} for r in range(args.rounds)]
+        if any(len(x) != 1 for x in xors):
+            raise SystemExit(f"clients received different results: {xors}")
+        steady = timings[1:] if len(timings) > 1 else timings
+        rs = float(np.median([t["round_s"] for t in steady]))
+        # the rate: wall time from the start of round 1 (round 0 warms up) to the
+        # end of the last round, per round -- it counts the parties' turnaround
+        # between rounds as well as the server's rounds; one round: its time
+        if len(timings) > 1:
+            span = timings[-1]["t_start"] + timings[-1]["round_s"] - timings[1]["t_start"]
+            period = span / (len(timings) - 1)
+        else:
+            period = rs
+        cl = [s for per in stats.values() for s in per[1:] or per]
+        return {
+            "metric": "host-resident grad elems/s (loopback sockets, H2D/D2H inclusive)",
+            "clients": args.clients, "elems_per_client": args.elems, "rounds": args.rounds,
+            "period_s": period, "grad_elems_per_s": args.clients * args.elems / period,
+            "round_s_median": rs,
+            "server": {k: float(np.median([t[k] for t in steady])) for k in steady[0]
+                       if k not in ("t_start", "stages")},
+            # host-side profile (sfl_amd.loopback.StageClock): wall and thread-CPU
+            # seconds per named copy / wait, summed over the threads that ran it,
+            # median over the steady rounds (server) or over clients x rounds
+            "server_stages": _median_stages([t["stages"] for t in steady]),
+            "client_stages": _median_stages([s["stages"] for s in cl]),
+            "client_h2d_mask_s_median": float(np.median([s["h2d_mask_s"] for s in cl])),
+            "client_d2h_send_s_median": float(np.median([s["d2h_send_s"] for s in cl])),
+            "parties_per_process": args.parties_per_process,
+            "wire_bytes_per_round": args.clients * args.elems * 8,
+            "send": os.environ.get("SFL_LOOPBACK_SEND", "sendfile"),
+            "wait": os.environ.get("SFL_LOOPBACK_WAIT", "poll"),
+            "results_agree_across_clients": True,
+        }
+
+    if not args.ab:
+        print(json.dumps(one_run()), flush=True)
+        return
+    # same-box A/B of the host-path choices, interleaved passes (boxes differ
+    # by +-25 % on this host-bound path, so only same-box runs compare)
+    for p in range(args.ab):
+        for send, wait in (("sendfile", "poll"), ("copy", "spin"), ("copy", "poll"), ("sendfile", "spin")):
+            os.environ["SFL_LOOPBACK_SEND"], os.environ["SFL_LOOPBACK_WAIT"] = send, wait
+            r = one_run()
+            r["ab_pass"] = p
+            print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":

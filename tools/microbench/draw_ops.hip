@@ -42,13 +42,15 @@ enum {
   kSubCo,     // v_sub_co_u32_e64 v, s[..], v, v
   kSubb,      // v_subb_co_u32_e64 v, s[..], v, v, s[..]
   kAdd32,     // v_add_u32_e32 (the full-rate reference)
+  kCmp32,     // v_cmp_gt_i32_e32 vcc, 0, v
+  kCndmask32, // v_cndmask_b32_e32 v, v, v, vcc
   kNumOps
 };
 static const char* kNames[kNumOps] = {
     "v_mad_u64_u32 (sgpr addend)", "v_mad_u64_u32 (vgpr addend)", "v_mul_lo_u32", "v_add_co_u32_e64",
     "v_addc_co_u32_e64", "v_bitop3_b32", "v_cmp_gt_i32_e64", "v_lshrrev_b32", "v_alignbit_b32",
     "v_cndmask_b32_e64", "v_min3_u32", "v_lshl_add_u64", "v_sub_co_u32_e64", "v_subb_co_u32_e64",
-    "v_add_u32_e32"};
+    "v_add_u32_e32", "v_cmp_gt_i32_e32", "v_cndmask_b32_e32"};
 
 template <int OP>
 __global__ void __launch_bounds__(256) k_op(uint64_t* out, unsigned long long* clk, int iters, uint64_t seed) {
@@ -121,6 +123,15 @@ __global__ void __launch_bounds__(256) k_op(uint64_t* out, unsigned long long* c
     } else if constexpr (OP == kSubb) {
 #define X(i) asm volatile("v_subb_co_u32_e64 %0, s[40:41], %0, %1, s[42:43]" : "+v"(LO(i)) : "v"(bl) : "s40", "s41");
       asm volatile("s_mov_b64 s[42:43], 0" ::: "s42", "s43");
+      R8(X) R8(X)
+#undef X
+    } else if constexpr (OP == kCmp32) {
+#define X(i) asm volatile("v_cmp_gt_i32_e32 vcc, 0, %0" : : "v"(LO(i)) : "vcc");
+      R8(X) R8(X)
+#undef X
+    } else if constexpr (OP == kCndmask32) {
+#define X(i) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(LO(i)) : "v"(HI(i)) : "vcc");
+      asm volatile("s_mov_b64 vcc, 0x5555" ::: "vcc");
       R8(X) R8(X)
 #undef X
     } else {

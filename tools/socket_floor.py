@@ -35,6 +35,15 @@ CHUNK = 64 << 20  # the loopback runtime's staging chunk (8M u64)
 
 
 def _send(sock, buf: memoryview, fd: int | None, nbytes: int):
+    if fd is not None and sock.gettimeout() is not None:  # socket.sendfile: poll + os.sendfile
+        f = open(fd, "rb", buffering=0, closefd=False)
+        off = 0
+        while off < nbytes:
+            k = min(CHUNK, nbytes - off)
+            assert sock.sendfile(f, off, k) == k
+            off += k
+        f.close()
+        return
     if fd is None:
         off = 0
         while off < nbytes:
@@ -64,9 +73,10 @@ def _memfd(nbytes: int):
     return fd, mm
 
 
-def client(port: int, nbytes: int, rounds: int, sendfile: bool, overlap: bool, q):
+def client(port: int, nbytes: int, rounds: int, sendfile: bool, overlap: bool, timeout, q, client_overlap=True):
+    """One client: sends its masked vector, receives the result (concurrently with --overlap)."""
     try:
-        s = socket.create_connection(("127.0.0.1", port))
+        s = socket.create_connection(("127.0.0.1", port), timeout=timeout)
         s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         if sendfile:
             fd, mm = _memfd(nbytes)
@@ -75,7 +85,7 @@ def client(port: int, nbytes: int, rounds: int, sendfile: bool, overlap: bool, q
             fd, out = None, memoryview(np.full(nbytes, 7, dtype=np.uint8))
         res = memoryview(np.empty(nbytes, dtype=np.uint8))
         for _ in range(rounds):
-            if overlap:
+            if overlap and client_overlap:
                 t = threading.Thread(target=_recv, args=(s, res, nbytes))
                 t.start()
                 _send(s, out, fd, nbytes)
@@ -94,24 +104,34 @@ def main():
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--elems", type=int, default=100_000_000)
     ap.add_argument("--rounds", type=int, default=4)
-    ap.add_argument("--sendfile", action="store_true")
+    ap.add_argument("--sendfile", action="store_true", help="both directions")
+    ap.add_argument("--sendfile-side", choices=("both", "clients", "server"), default="both",
+                    help="with --sendfile: which senders use it")
     ap.add_argument("--overlap", action="store_true")
+    ap.add_argument("--client-sequential", action="store_true",
+                    help="with --overlap: clients read the result only after sending everything (the loopback "
+                         "runtime's client), while the server already sends")
+    ap.add_argument("--timeout", type=float, default=None,
+                    help="sockets with a timeout (non-blocking descriptors; sendfile through socket.sendfile)")
     args = ap.parse_args()
     C, nbytes = args.clients, 8 * args.elems
     srv = socket.create_server(("127.0.0.1", 0))
     port = srv.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=client, args=(port, nbytes, args.rounds, args.sendfile, args.overlap, q)) for _ in range(C)]
+    procs = [ctx.Process(target=client, args=(port, nbytes, args.rounds, args.sendfile and args.sendfile_side != "server",
+                                                   args.overlap, args.timeout, q,
+                                                   not args.client_sequential)) for _ in range(C)]
     for p in procs:
         p.start()
     conns = []
     for _ in range(C):
         c, _ = srv.accept()
+        c.settimeout(args.timeout)
         c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         conns.append(c)
     rx = [memoryview(np.empty(nbytes, dtype=np.uint8)) for _ in range(C)]
-    if args.sendfile:
+    if args.sendfile and args.sendfile_side != "clients":
         fd, mm = _memfd(nbytes)
         res = memoryview(mm)
     else:
@@ -145,8 +165,8 @@ def main():
     tx_s = float(np.median([b for _, b in steady]))
     round_s = float(np.median([a + b for a, b in steady]))
     print(json.dumps({"what": "loopback transport floor (no GPU): C masked u64 vectors in, the float64 result "
-                              "back to every client", "send": "os.sendfile from a memfd" if args.sendfile
-                      else "sendall from user memory", "overlap": args.overlap, "clients": C, "elems": args.elems, "rounds": args.rounds,
+                              "back to every client", "send": f"os.sendfile from a memfd ({args.sendfile_side})" if args.sendfile
+                      else "sendall from user memory", "client_sequential": args.client_sequential, "overlap": args.overlap, "socket_timeout": args.timeout, "clients": C, "elems": args.elems, "rounds": args.rounds,
                       "gather_s": rx_s, "after_gather_s": tx_s, "round_s": round_s,
                       "wire_GBps": 2 * C * nbytes / round_s / 1e9,
                       "grad_elems_per_s": C * args.elems / round_s, "cpus": os.cpu_count(),
