@@ -56,6 +56,16 @@ import sys
 # tools/check_pair01.py on the ISA.  --no-pair01 emits the earlier form
 # (limbs in four 32-bit operands, the new limb 0 moved in from scratch).
 PAIR01 = "--no-pair01" not in sys.argv
+# --rot64: XSL-RR's 64-bit rotation by r = s3 >> 26 as two 64-bit shifts and
+# an OR (x >> r | x << (64 - r) & 63, exact for r = 0 too: x | x) instead of
+# two v_alignbit (rotating by r & 31) + a v_cmp on bit 31 of s3 + two
+# v_cndmask swapping the halves when r >= 32.  The same instruction count,
+# 5.6 fewer cycles per draw by the per-form issue costs
+# (tools/microbench/draw_ops.hip), but measured neutral in the kernel
+# (profiles/r03/ab_rot64_kb.jsonl: every per-rank shape within +-1.5 %), so
+# the default stays the alignbit form.  Both are pinned to numpy on the CPU
+# by tests/test_draw_emulation.py.
+ROT64 = "--rot64" in sys.argv
 
 # one draw: (asm, sgpr_writes, sgpr_reads); {..} fields are renamed per stream
 DRAW = [
@@ -91,6 +101,28 @@ DRAW = [
 ]
 
 
+ROT64_STEPS = [  # replaces {cmp} .. {cnd_hi} of DRAW (the rotation), zero test and accumulate kept in place
+    ("v_lshrrev_b32_e32 v{v2}, 26, %[{s3}]", set(), set()),
+    ("v_bitop3_b32 v{v3}, v{v0}, v{v1}, %[{m}] bitop3:0x7e", set(), set()),
+    ("v_sub_u32_e32 v{v8}, 64, v{v2}", set(), set()),
+    ("v_lshrrev_b64 v[{v4}:{v5}], v{v2}, v[{v0}:{v1}]", set(), set()),
+    ("ZMIN", set(), set()),
+    ("v_lshlrev_b64 v[{v6}:{v7}], v{v8}, v[{v0}:{v1}]", set(), set()),
+    ("v_or_b32_e32 v{v6}, v{v6}, v{v4}", set(), set()),
+    ("VSUBLO", {"k2"}, set()),
+    ("v_or_b32_e32 v{v7}, v{v7}, v{v5}", set(), set()),
+]
+
+
+def draw_steps():
+    """DRAW with the rotation in the form ROT64 selects."""
+    if not ROT64:
+        return DRAW
+    i0 = DRAW.index(("{cmp}", {"sw"}, set()))
+    i1 = DRAW.index(("{cnd_hi}", set(), {"sw"}))
+    return DRAW[:i0] + ROT64_STEPS + DRAW[i1 + 1:]
+
+
 def stream(tag, base, vmode, acc_u, acc_v):
     """vmode: None (no second client), "s" (subtract) or "a" (add)."""
     f = {"s0": f"s0{tag}", "s1": f"s1{tag}", "s2": f"s2{tag}", "s3": f"s3{tag}",
@@ -107,12 +139,12 @@ def stream(tag, base, vmode, acc_u, acc_v):
         f["cnd_lo"] = f"v_cndmask_b32_e64 v{base + 6}, v{base + 4}, v{base + 5}, %[swb]"
         f["cnd_hi"] = f"v_cndmask_b32_e64 v{base + 7}, v{base + 5}, v{base + 4}, %[swb]"
     out = []
-    draw = DRAW
+    draw = draw_steps()
     if PAIR01:
         f["p01"] = f"p01{tag}"
         e0 = None
         draw = []
-        for asm, w, r in DRAW:
+        for asm, w, r in draw_steps():
             if asm.startswith("v_mad_u64_u32 v[{v0}:{v1}]"):
                 e0 = (asm.replace("v[{v0}:{v1}]", "%[{p01}]"), w, r)
                 continue

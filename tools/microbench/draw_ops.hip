@@ -44,13 +44,18 @@ enum {
   kAdd32,     // v_add_u32_e32 (the full-rate reference)
   kCmp32,     // v_cmp_gt_i32_e32 vcc, 0, v
   kCndmask32, // v_cndmask_b32_e32 v, v, v, vcc
+  kOr32,      // v_or_b32_e32 (the 64-bit-shift rotation's halves)
+  kSubK,      // v_sub_u32_e32 v, 64, v (its 64 - r)
+  kLshr64,    // v_lshrrev_b64 v[..], v, v[..]
+  kLshl64,    // v_lshlrev_b64 v[..], v, v[..]
   kNumOps
 };
 static const char* kNames[kNumOps] = {
     "v_mad_u64_u32 (sgpr addend)", "v_mad_u64_u32 (vgpr addend)", "v_mul_lo_u32", "v_add_co_u32_e64",
     "v_addc_co_u32_e64", "v_bitop3_b32", "v_cmp_gt_i32_e64", "v_lshrrev_b32", "v_alignbit_b32",
     "v_cndmask_b32_e64", "v_min3_u32", "v_lshl_add_u64", "v_sub_co_u32_e64", "v_subb_co_u32_e64",
-    "v_add_u32_e32", "v_cmp_gt_i32_e32", "v_cndmask_b32_e32"};
+    "v_add_u32_e32", "v_cmp_gt_i32_e32", "v_cndmask_b32_e32", "v_or_b32_e32", "v_sub_u32_e32 (64 - v)",
+    "v_lshrrev_b64", "v_lshlrev_b64"};
 
 template <int OP>
 __global__ void __launch_bounds__(256) k_op(uint64_t* out, unsigned long long* clk, int iters, uint64_t seed) {
@@ -132,6 +137,22 @@ __global__ void __launch_bounds__(256) k_op(uint64_t* out, unsigned long long* c
     } else if constexpr (OP == kCndmask32) {
 #define X(i) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(LO(i)) : "v"(HI(i)) : "vcc");
       asm volatile("s_mov_b64 vcc, 0x5555" ::: "vcc");
+      R8(X) R8(X)
+#undef X
+    } else if constexpr (OP == kOr32) {
+#define X(i) asm volatile("v_or_b32_e32 %0, %0, %1" : "+v"(LO(i)) : "v"(HI(i)));
+      R8(X) R8(X)
+#undef X
+    } else if constexpr (OP == kSubK) {
+#define X(i) asm volatile("v_sub_u32_e32 %0, 64, %0" : "+v"(LO(i)));
+      R8(X) R8(X)
+#undef X
+    } else if constexpr (OP == kLshr64) {
+#define X(i) asm volatile("v_lshrrev_b64 %0, %1, %0" : "+v"(a##i) : "v"(bl));
+      R8(X) R8(X)
+#undef X
+    } else if constexpr (OP == kLshl64) {
+#define X(i) asm volatile("v_lshlrev_b64 %0, %1, %0" : "+v"(a##i) : "v"(bl));
       R8(X) R8(X)
 #undef X
     } else {
