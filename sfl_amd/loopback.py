@@ -22,11 +22,12 @@ The GPU kernels are the product path; nothing here falls back to the CPU.
 
 Host buffers that leave through a socket (every client's masked vector, the
 server's float64 result) are ``SharedHostBuffer``s: memfd-backed pages that
-are HIP-registered, so the D2H copy lands in them directly, and that are
-sent with ``os.sendfile`` -- the kernel hands the page references to the
-socket instead of copying them in, so a byte crossing 127.0.0.1 is copied
-once (into the receiver) instead of twice.  tools/socket_floor.py measures
-the transport with and without it.
+are HIP-registered, so the D2H copy lands in them directly.  They are sent
+with ``sendall`` (a copy into the kernel); ``SFL_LOOPBACK_SEND=sendfile``
+hands the page references to the socket instead -- no send-side copy, but
+measured no faster at 8 x 100M and slower at 32 x 256M (DESIGN.md §7,
+tools/socket_floor.py for the transport alone).  Clients receive the result
+while they send, and GPU waits poll instead of spinning a core.
 """
 
 from __future__ import annotations
@@ -77,10 +78,14 @@ class StageClock:
 
 # Knobs for same-box A/B measurements of the host path (tools/loopback_bench.py
 # --ab); the defaults are the product's choices.
-#   SFL_LOOPBACK_SEND=sendfile|copy   sendfile() from the memfd pages, or sendall() (a copy into the kernel)
+#   SFL_LOOPBACK_SEND=copy|sendfile   sendall() (a copy into the kernel), or sendfile() from the memfd pages
+#                                     (no send-side copy, but page-granular kernel work: measured no faster
+#                                     at 8 x 100M and 26 % slower at 32 x 256M, profiles/r03/loopback_*_ab.jsonl)
 #   SFL_LOOPBACK_WAIT=poll|spin       wait for a GPU event by polling with short sleeps, or in hipEventSynchronize
+#   SFL_LOOPBACK_CLIENT_RX=concurrent|after   a client reads the result while it sends, or after (round 2;
+#                                     with SEND=sendfile that can stall on the box's kernel: copy only)
 def _send_mode() -> str:
-    return os.environ.get("SFL_LOOPBACK_SEND", "sendfile")
+    return os.environ.get("SFL_LOOPBACK_SEND", "copy")
 
 
 def wait_event(e) -> None:
@@ -110,9 +115,10 @@ def _hip():
 class SharedHostBuffer:
     """``nbytes`` of memfd-backed host memory, mapped, faulted in and
     HIP-registered (hipHostRegister): device copies land in it directly (torch
-    sees it as pinned), and ``send(sock, lo, hi)`` ships a byte range with
-    ``os.sendfile`` -- page references handed to the socket, no send-side
-    copy.  The pages must not change until the peer has read them; the
+    sees it as pinned), and ``send(sock, lo, hi)`` ships a byte range --
+    with ``sendall``, or with ``os.sendfile`` (page references handed to the
+    socket, no send-side copy) under SFL_LOOPBACK_SEND=sendfile.  With
+    sendfile the pages must not change until the peer has read them; the
     round protocol guarantees that (a party writes a buffer again only after
     every peer answered the frame that carried it)."""
 
@@ -236,7 +242,7 @@ class LoopbackServer:
             ring = [[torch.empty(ce, dtype=torch.int64).pin_memory() for _ in range(2)] for _ in self.conns]
             devb = [torch.empty(n, dtype=torch.int64, device=dev) for _ in self.conns]
             streams = [torch.cuda.Stream(dev) for _ in self.conns]
-            # the float64 result: D2H straight into memfd pages the broadcast sendfile()s
+            # the float64 result: D2H straight into the registered pages the broadcast sends
             agg = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.float64, device=dev),
                    SharedHostBuffer(8 * n, np.float64), torch.cuda.Stream(dev))
             self._bufs = (n, ring, devb, streams, agg)
@@ -332,7 +338,7 @@ class LoopbackServer:
                     if errors:
                         return
                     if hi > lo:
-                        with clock("server: broadcast sendfile (memfd result pages -> socket, no copy)"):
+                        with clock("server: broadcast send (result pages -> socket)"):
                             res_shb.send(conn, 8 * lo, 8 * hi)
             except BaseException as e:  # noqa: BLE001
                 with cond:
@@ -457,7 +463,7 @@ class LoopbackClient:
             ce = min(n, chunk_elems())
             if self._bufs is not None:
                 self._bufs[2].close()
-            # the masked vector: D2H straight into memfd pages that are sendfile()d
+            # the masked vector: D2H straight into registered pages, sent chunk by chunk
             self._bufs = (n, [torch.empty(ce, dtype=torch.float32).pin_memory() for _ in range(2)],
                           SharedHostBuffer(8 * n, np.int64),
                           torch.empty(n, dtype=torch.float32, device=dev),
@@ -465,12 +471,25 @@ class LoopbackClient:
         return self._bufs[1:]
 
     def _receive_result(self, n, into, box):
+        """The RESULT frame, chunk by chunk: into ``into`` (n elements) or,
+        when ``into`` is a list of two chunk buffers, through that ring (the
+        caller keeps only the checksum); the XOR of its 64-bit words is
+        folded in as each chunk lands (``box["xor"]``)."""
         try:
             w0, c0 = time.perf_counter(), time.thread_time()
-            h, _ = W.recv_frame(self.sock, into, expect_kind=W.RESULT)
+            h = W.recv_header(self.sock, expect_kind=W.RESULT)
             if h.dtype != W.F64 or h.count != int(n):
                 raise W.WireError(f"RESULT frame of {h.count} elements (dtype {h.dtype}), want {n} float64")
-            box["h"] = h
+            ring = isinstance(into, list)
+            ce = into[0].size if ring else chunk_elems()
+            x, j = 0, 0
+            for lo in range(0, n, ce):
+                k = min(ce, n - lo)
+                buf = into[j & 1][:k] if ring else into[lo:lo + k]
+                W.recv_exact(self.sock, memoryview(buf).cast("B"))
+                x ^= int(np.bitwise_xor.reduce(buf.view(np.uint64))) if k else 0
+                j += 1
+            box["h"], box["xor"] = h, x
             self.last_result_recv = {"wall_s": time.perf_counter() - w0, "cpu_s": time.thread_time() - c0}
         except BaseException as e:  # noqa: BLE001 - re-raised by result()
             box["error"] = e
@@ -480,16 +499,18 @@ class LoopbackClient:
         ``GaussianModelDP`` ``dp``, its clip + noise runs inside the masking
         kernel (``sa_mask_dp``) on the device copy of ``x``.  ``x`` streams to
         the device through two pinned chunk buffers; the masked vector comes
-        back chunk by chunk into memfd pages that are sendfile()d as each
-        chunk lands.
+        back chunk by chunk into registered memfd pages, each chunk sent as it
+        lands.
 
-        ``result_into`` (float64, n elements): the round's RESULT frame is
+        ``result_into`` (float64, n elements; or a list of two float64 chunk
+        buffers when only the checksum is wanted): the round's RESULT frame is
         received into it by a thread started now, while this party is still
         sending -- the server broadcasts chunk j as soon as it has chunk j of
         every party, and a party that read only after sending everything
         would leave both directions of its connection full at once (on the
         GPU box's kernel that stalls sendfile()d transfers, tools/socket_floor.py
-        --client-sequential).  ``result()`` then joins it."""
+        --client-sequential).  ``result()`` then joins it; ``last_result_xor``
+        holds the XOR of the result's 64-bit words."""
         import torch
 
         from . import _lib as L
@@ -499,12 +520,22 @@ class LoopbackClient:
         if self._rx is not None:
             raise RuntimeError("the previous round's result was not collected (result())")
         if result_into is not None:
-            if result_into.dtype != np.float64 or not result_into.flags.c_contiguous or result_into.size < n:
-                raise ValueError("result_into must be a contiguous float64 array of at least n elements")
+            bufs = result_into if isinstance(result_into, list) else [result_into]
+            for b in bufs:
+                if b.dtype != np.float64 or not b.flags.c_contiguous:
+                    raise ValueError("result_into: contiguous float64 arrays")
+            if isinstance(result_into, list):
+                if len(result_into) != 2 or min(b.size for b in result_into) < 1:
+                    raise ValueError("result_into: a ring of two chunk buffers")
+                target, keep = result_into, None
+            else:
+                if result_into.size < n:
+                    raise ValueError("result_into must hold at least n elements")
+                target = keep = result_into[:n]
             box = {}
-            t = threading.Thread(target=self._receive_result, args=(n, result_into[:n], box), daemon=True)
+            t = threading.Thread(target=self._receive_result, args=(n, target, box), daemon=True)
             t.start()
-            self._rx = (t, box, result_into[:n], n)
+            self._rx = (t, box, keep, n)
         hx, hmb, dx, dm, cs = self._buffers(n)
         hm = hmb.tensor()
         dev = dx.device
@@ -569,7 +600,7 @@ class LoopbackClient:
         for lo, hi, e in chunks:
             with clock("client: wait for a chunk's D2H"):
                 wait_event(e)
-            with clock("client: sendfile (memfd masked-vector pages -> socket, no copy)"):
+            with clock("client: send (masked-vector pages -> socket)"):
                 hmb.send(self.sock, 8 * lo, 8 * hi)
         t2 = time.perf_counter()
         self.last_stages = clock.report()
@@ -589,19 +620,36 @@ class LoopbackClient:
                 raise box["error"]
             if n is not None and int(n) != rn:
                 raise W.WireError(f"RESULT of {rn} elements, want {n}")
+            self.last_result_xor = box["xor"]
             return buf
         if into is None and n is not None:
             into = np.empty(int(n), dtype=np.float64)
         if into is None:
             h, mv = W.recv_frame(self.sock, expect_kind=W.RESULT)
             return W.as_array(h, mv).copy()
+        if isinstance(into, list):  # a ring of two chunk buffers: the checksum only
+            if n is None:
+                raise ValueError("a result ring needs n")
+            box = {}
+            self._receive_result(int(n), into, box)
+            if "error" in box:
+                raise box["error"]
+            self.last_result_xor = box["xor"]
+            return None
         if into.dtype != np.float64 or not into.flags.c_contiguous:
             raise ValueError("result buffer must be a contiguous float64 array")
+        if n is not None:
+            box = {}
+            self._receive_result(int(n), into[:int(n)], box)
+            if "error" in box:
+                raise box["error"]
+            self.last_result_xor = box["xor"]
+            return into[:int(n)]
         w0, c0 = time.perf_counter(), time.thread_time()
         h, _ = W.recv_frame(self.sock, into, expect_kind=W.RESULT)
         self.last_result_recv = {"wall_s": time.perf_counter() - w0, "cpu_s": time.thread_time() - c0}
-        if h.dtype != W.F64 or (n is not None and h.count != int(n)):
-            raise W.WireError(f"RESULT frame of {h.count} elements (dtype {h.dtype}), want {n} float64")
+        if h.dtype != W.F64:
+            raise W.WireError(f"RESULT frame of dtype {h.dtype}, want float64")
         return into[:h.count]
 
     def close(self):
@@ -623,10 +671,14 @@ def synthetic_gradient(c: int, n: int, rnd: int = 0) -> np.ndarray:
     return (g.standard_normal(n, dtype=np.float32) * np.float32(1e-2)).astype(np.float32)
 
 
-def client_process(parties: list, port: int, n: int, rounds: int, gpu: int, fxp_bits: int, out_q) -> None:
+def client_process(parties: list, port: int, n: int, rounds: int, gpu: int, fxp_bits: int, out_q,
+                   keep_results: bool = True) -> None:
     """Entry point of one spawned process hosting one or more client parties
     (``parties``: (name, index, pair seeds or None, weight) tuples), each on
-    its own socket and thread."""
+    its own socket and thread.  Every party records the XOR of each round's
+    result; ``keep_results=False`` receives the results through a ring of two
+    chunk buffers instead of a whole-vector array (config 5's 32 parties x
+    256M elements would otherwise hold 64 GB of results)."""
     import threading
 
     dump_after = float(os.environ.get("SFL_LOOPBACK_DUMP_AFTER", "0"))
@@ -641,19 +693,23 @@ def client_process(parties: list, port: int, n: int, rounds: int, gpu: int, fxp_
             cl = LoopbackClient(party, index, port, gpu=gpu, fxp_bits=fxp_bits, seeds=seeds)
             cl.handshake()
             stats = []
-            # two receive buffers, alternating: round r's result arrives while
-            # round r-1's is checksummed
-            res = [np.empty(n, dtype=np.float64) for _ in range(2)]
+            # one result array for every round (checksummed chunk by chunk as it
+            # arrives), or a ring of two chunks when only the checksum is kept
+            ce = max(1, min(n, chunk_elems()))
+            res = np.empty(n, dtype=np.float64) if keep_results else [np.empty(ce, dtype=np.float64)
+                                                                       for _ in range(2)]
+            after = os.environ.get("SFL_LOOPBACK_CLIENT_RX", "concurrent") == "after"
             for r in range(rounds):
-                st = cl.submit(xs[r], r, weight, result_into=res[r & 1])
-                if r:  # the previous result's checksum, after this round's submit
-                    stats[-1]["result_xor"] = int(np.bitwise_xor.reduce(res[(r - 1) & 1].view(np.uint64)))
-                cl.result(n)
+                if after:  # A/B only (round 2's client): read the result once everything is sent
+                    st = cl.submit(xs[r], r, weight)
+                    cl.result(n, into=res)
+                else:
+                    st = cl.submit(xs[r], r, weight, result_into=res)
+                    cl.result(n)
+                st["result_xor"] = cl.last_result_xor
                 st["stages"]["client: result recv thread (socket -> numpy, from the start of submit)"] = dict(
                     cl.last_result_recv, calls=1)
                 stats.append(st)
-            if stats:
-                stats[-1]["result_xor"] = int(np.bitwise_xor.reduce(res[(rounds - 1) & 1].view(np.uint64)))
             W.recv_header(cl.sock, expect_kind=W.BYE)
             cl.close()
             out_q.put((index, "ok", stats))
@@ -674,9 +730,9 @@ def run_loopback(names: list[str], n: int, rounds: int = 1, *, seeds: dict | Non
     """Spawn the client parties (``parties_per_process`` per OS process), run
     ``rounds`` rounds with this process as the server.  Returns (results per
     round, server timings, client stats, received masked vectors).
-    ``keep_results=False``: the server keeps no copy of each round's result
-    (results holds None per round; every client checksums what it received,
-    ``stats[i][r]["result_xor"]``)."""
+    ``keep_results=False``: neither the server nor the clients keep each
+    round's result (results holds None per round); every client checksums
+    what it received either way (``stats[i][r]["result_xor"]``)."""
     import multiprocessing as mp
 
     ctx = mp.get_context("spawn")
@@ -689,7 +745,8 @@ def run_loopback(names: list[str], n: int, rounds: int = 1, *, seeds: dict | Non
         specs.append((p, i, ps, None if weights is None else weights[i]))
     k = max(1, int(parties_per_process))
     for g in range(0, len(specs), k):
-        pr = ctx.Process(target=client_process, args=(specs[g:g + k], srv.port, n, rounds, gpu, fxp_bits, q))
+        pr = ctx.Process(target=client_process, args=(specs[g:g + k], srv.port, n, rounds, gpu, fxp_bits, q,
+                                                      keep_results))
         pr.start()
         procs.append(pr)
     results, timings, masked = [], [], []

@@ -100,6 +100,11 @@ def unpack_header(b: bytes) -> Header:
     return Header(kind, dtype, sender, rnd, count, nbytes, digest)
 
 
+def recv_exact(sock: socket.socket, view: memoryview) -> None:
+    """Fill ``view`` from the socket (raises WireError on a closed connection)."""
+    _recv_exact(sock, view)
+
+
 def _recv_exact(sock: socket.socket, view: memoryview) -> None:
     got = 0
     n = len(view)

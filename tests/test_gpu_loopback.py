@@ -97,17 +97,21 @@ def test_loopback_client_reproduces_numpy_rejection():
             assert np.array_equal(masked[r][c], m[c]), (r, c)
 
 
-def test_loopback_sendfile_chunks_without_server_copy(monkeypatch):
-    """The sendfile transport over many chunks (masked vectors D2H into
-    memfd pages chunk by chunk, sendfile'd as each lands; the result D2H'd
-    into the server's memfd pages and broadcast from them), with no server
-    copy of the result (keep_results=False): every client received the
-    oracle's float64 result, round after round, with the streams advancing."""
+@pytest.mark.parametrize("send", ["copy", "sendfile"])
+def test_loopback_chunks_without_result_copies(monkeypatch, send):
+    """Both send modes over many chunks (masked vectors D2H into registered
+    memfd pages chunk by chunk, each sent as it lands; the result D2H'd into
+    the server's pages and broadcast from them), with no copy of the result
+    kept by the server or the clients (keep_results=False: the clients
+    receive it through a ring of two chunks and checksum it as it lands):
+    every client received the oracle's float64 result, round after round,
+    with the streams advancing."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from sfl_amd.loopback import run_loopback, synthetic_gradient
 
-    monkeypatch.setenv("SFL_LOOPBACK_CHUNK_ELEMS", "8192")  # 9 chunks; the spawned clients inherit it
+    monkeypatch.setenv("SFL_LOOPBACK_SEND", send)  # the spawned clients inherit both
+    monkeypatch.setenv("SFL_LOOPBACK_CHUNK_ELEMS", "8192")  # 9 chunks
     names = ["p0", "p1", "p2", "p3"]
     n, rounds = 70_001, 3
     seeds = o.seeds_for(names)

@@ -1,5 +1,6 @@
-"""The loopback runtime's sendfile transport (sfl_amd.loopback.SharedHostBuffer)
-on the CPU: memfd pages sent with socket.sendfile over a socket with a
+"""The loopback runtime's send path (sfl_amd.loopback.SharedHostBuffer) on
+the CPU, in both modes (sendall, and socket.sendfile of the memfd pages):
+byte ranges sent over a socket with a
 timeout (a non-blocking descriptor) whose buffer fills while the receiver
 sleeps -- every byte arrives, in order, in several ranges.  (HIP registration
 of the pages is exercised on the GPU by tests/test_gpu_loopback.py.)"""
@@ -10,6 +11,7 @@ import threading
 import time
 
 import numpy as np
+import pytest
 
 from sfl_amd import loopback as lb
 
@@ -25,7 +27,9 @@ class _Unregistered(lb.SharedHostBuffer):
         self._registered = False
 
 
-def test_sendfile_ranges_through_a_full_socket_buffer():
+@pytest.mark.parametrize("send", ["copy", "sendfile"])
+def test_send_ranges_through_a_full_socket_buffer(monkeypatch, send):
+    monkeypatch.setenv("SFL_LOOPBACK_SEND", send)
     n = 96 << 20
     buf = _Unregistered(n)
     srv = socket.create_server(("127.0.0.1", 0))

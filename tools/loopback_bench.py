@@ -87,20 +87,25 @@ def main():
             "client_d2h_send_s_median": float(np.median([s["d2h_send_s"] for s in cl])),
             "parties_per_process": args.parties_per_process,
             "wire_bytes_per_round": args.clients * args.elems * 8,
-            "send": os.environ.get("SFL_LOOPBACK_SEND", "sendfile"),
+            "send": os.environ.get("SFL_LOOPBACK_SEND", "copy"),
             "wait": os.environ.get("SFL_LOOPBACK_WAIT", "poll"),
             "results_agree_across_clients": True,
         }
 
     if not args.ab:
-        print(json.dumps(one_run()), flush=True)
+        r = one_run()
+        r["client_rx"] = os.environ.get("SFL_LOOPBACK_CLIENT_RX", "concurrent")
+        print(json.dumps(r), flush=True)
         return
     # same-box A/B of the host-path choices, interleaved passes (boxes differ
     # by +-25 % on this host-bound path, so only same-box runs compare)
     for p in range(args.ab):
-        for send, wait in (("sendfile", "poll"), ("copy", "spin"), ("copy", "poll"), ("sendfile", "spin")):
+        for send, wait, rx in (("sendfile", "poll", "concurrent"), ("copy", "spin", "after"),
+                               ("copy", "poll", "concurrent"), ("copy", "spin", "concurrent")):
             os.environ["SFL_LOOPBACK_SEND"], os.environ["SFL_LOOPBACK_WAIT"] = send, wait
+            os.environ["SFL_LOOPBACK_CLIENT_RX"] = rx
             r = one_run()
+            r["client_rx"] = rx
             r["ab_pass"] = p
             print(json.dumps(r), flush=True)
 
