@@ -451,6 +451,53 @@ def collective_text(v: Variant) -> str:
     return "ncclReduce(uint64, sum) in place to rank 0"
 
 
+class GlooStandinComm:
+    """--rehearse-one-gpu only: RcclComm's contract (reduce_u64,
+    reduce_scatter_u64, gather_f64) through gloo host round trips, so N rank
+    processes can run every design's code path on ONE GPU (RCCL refuses two
+    ranks on one device: "Duplicate GPU detected").  Called on the comm
+    stream like RcclComm; ``send.cpu()`` waits for the chunk's launch.  Its
+    timings are host round trips, not xGMI: a rehearsal checks the N > 1
+    control flow, never the rate."""
+
+    def __init__(self, rank: int, world: int):
+        self.rank, self.world = rank, world
+
+    def reduce_u64(self, send, recv, root: int = 0):
+        import torch.distributed as dist
+
+        host = send.cpu()
+        dist.reduce(host, dst=root, op=dist.ReduceOp.SUM)  # int64 addition wraps like uint64
+        if self.rank == root:
+            (recv if recv is not None else send).copy_(host)
+        return recv
+
+    def reduce_scatter_u64(self, send, recv):
+        import torch.distributed as dist
+
+        if send.numel() != recv.numel() * self.world:
+            raise ValueError("reduce_scatter: shard sizes")
+        host = send.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM)
+        k = recv.numel()
+        recv.copy_(host[self.rank * k:(self.rank + 1) * k])
+        return recv
+
+    def gather_f64(self, send, recv, root: int = 0):
+        import torch
+        import torch.distributed as dist
+
+        host = send.cpu()
+        parts = [torch.empty_like(host) for _ in range(self.world)] if self.rank == root else None
+        dist.gather(host, parts, dst=root)
+        if self.rank == root:
+            recv.copy_(torch.cat(parts))
+        return recv
+
+    def close(self):
+        pass
+
+
 def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
     """Time `steps` steps (after `warmup`) of design `v` on this rank: the
     masking launches on the compute stream, the design's exchange on the
@@ -540,7 +587,8 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     kern_ms = sum(a.elapsed_time(b) for a, b in kev) / steps  # masking kernel time per step
     xchg_ms = sum(a.elapsed_time(b) for a, b in xev) / steps  # exchange time per step (comm stream)
     if multi:
-        t = torch.tensor([elapsed, kern_ms, xchg_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms, xchg_ms], dtype=torch.float64,
+                         device="cpu" if ctx.get("rehearse") else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms, xchg_ms = float(t[0]), float(t[1]), float(t[2])
     flagged = bool(int(flags.item()))
@@ -627,6 +675,10 @@ def main():
                     help="also fold every client's masked values into an XOR digest (test checksum)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher rehearsal without a GPU: ranks join a gloo group, rank 0 prints one line")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, a gloo process group and the "
+                         "collectives through gloo host round trips (RCCL refuses two ranks on one GPU); runs "
+                         "every design's code path, its timings are not the product's")
     ap.add_argument("--watchdog-seconds", type=float, default=480.0,
                     help="a rank still running after this long dumps every thread's stack (faulthandler) and "
                          "exits (a hung collective cannot be interrupted from Python; torchrun then stops the "
@@ -665,7 +717,8 @@ def main():
         return
     multi = world > 1 or args.dist
     # same-box draw-loop ceilings, also before this process initialises the GPU
-    ceil = draw_loop_ceilings(local_rank if world > 1 else None)
+    rehearse = args.rehearse_one_gpu
+    ceil = {} if rehearse else draw_loop_ceilings(local_rank if world > 1 else None)
 
     import torch
     import torch.distributed as dist
@@ -673,16 +726,20 @@ def main():
     from sfl_amd import _lib
     from sfl_amd.parallel_sum import RcclComm
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gpu = 0 if rehearse else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     _lib.lib()
     comm = None
-    if multi:
+    if multi and rehearse:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        comm = GlooStandinComm(rank, world)
+    elif multi:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         comm = RcclComm(rank, world, local_rank)
 
     C, N = args.clients, args.elems
-    ctx = {"args": args, "world": world, "rank": rank, "dev": dev, "comm": comm,
+    ctx = {"args": args, "world": world, "rank": rank, "dev": dev, "comm": comm, "rehearse": rehearse,
            "names": [f"client{c}" for c in range(C)]}
     head = headline_variant(args, multi)
     r = run_design(ctx, head, args.steps, args.warmup, keep=args.extra and world == 1)
@@ -751,6 +808,9 @@ def main():
              "xchg_ms": x["exchange"]["ms_per_step"], "bytes_per_rank_per_step": x["exchange"]["bytes_per_rank_per_step"],
              "algbw_GBps": x["exchange"]["algbw_GBps"], "busbw_GBps": x["exchange"]["busbw_GBps"],
              "collective": x["exchange"]["collective"]} for x in variants]
+    if rehearse:
+        out["rehearsal"] = ("--rehearse-one-gpu: every rank on cuda:0, collectives through gloo host round "
+                            "trips; the N > 1 control flow, not the product's rate")
     if args.extra and world == 1:
         from sfl_amd import kernels as K
 

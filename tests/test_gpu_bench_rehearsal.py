@@ -1,0 +1,51 @@
+"""The driver's N > 1 bench, rehearsed with real rank processes on the one
+GPU of the test box (`bench.py --gpus W --rehearse-one-gpu`): the
+self-launcher, W torchrun ranks, every design's code path in run_design
+(client sharding with the pipelined sharded server, its gather, the reduce
+to rank 0, element sharding with and without the gather) and the max-over-
+ranks timing, with the collectives through gloo host round trips because
+RCCL refuses two ranks on one GPU ("Duplicate GPU detected",
+tools/debug/rccl_two_ranks_one_gpu.py).  RCCL itself runs at world 1 in
+tests/test_gpu_rccl.py; the data path of every rank is checked against the
+oracle in tests/test_gpu_dist_pipeline.py and test_gpu_world_emulation.py."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_n_ranks_every_design(world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
+                        "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
+                        "--cpu-baseline-seconds", "0", "--watchdog-seconds", "100"],
+                       capture_output=True, text=True, timeout=115, env=env, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == world and "rehearsal" in line and line["config"]["design"] == "sharded"
+    per = 8 // world
+    assert line["config"]["clients_per_gpu"] == per
+    assert line["roofline"]["kernel"].startswith(f"k_clients<float, float, {per}, {8 - per}, ")
+    assert line["exchange"]["chunks"] == 8
+    names = [v["name"] for v in line["exchange_variants"]]
+    assert sorted(names) == sorted(["sharded", "sharded+gather", "reduce", "elements", "elements+gather"])
+    for v in line["exchange_variants"]:
+        assert v["value"] > 0 and v["kernel_ms_per_step"] > 0, v
+        if v["name"].startswith("elements"):
+            assert v["kernel"].startswith("k_clients<float, float, 8, 0, ")
+        else:
+            assert v["xchg_ms"] > 0 and v["bytes_per_rank_per_step"] > 0
