@@ -670,7 +670,8 @@ def main():
     ap.add_argument("--variants", default="all",
                     help="N>1: the other exchange designs timed after the headline in the same process group "
                          f"('all' = {','.join(VARIANTS)}; a comma list; 'none')")
-    ap.add_argument("--variant-steps", type=int, default=200, help="timed steps per extra design")
+    ap.add_argument("--variant-steps", type=int, default=None,
+                    help="timed steps per extra design (default: min(200, --steps))")
     ap.add_argument("--digests", action="store_true",
                     help="also fold every client's masked values into an XOR digest (test checksum)")
     ap.add_argument("--dry-run", action="store_true",
@@ -684,6 +685,8 @@ def main():
                          "exits (a hung collective cannot be interrupted from Python; torchrun then stops the "
                          "other ranks); below the driver's 600 s lease; 0 disables")
     args = ap.parse_args()
+    if args.variant_steps is None:
+        args.variant_steps = max(1, min(200, args.steps))
     for v in (args.variants.split(",") if args.variants not in ("all", "none") else []):
         if v and v not in VARIANTS:
             ap.error(f"--variants: unknown design {v!r} (choose from {', '.join(VARIANTS)})")
