@@ -118,3 +118,54 @@ def test_gaussian_model_dp_class_vs_oracle(each_layer):
     exp0 = D.gaussian_model_dp(layers, 0.0, 8, 2.0)
     for g, e in zip(got0, exp0):
         assert np.array_equal(g, e)
+
+
+def test_loopback_client_dp_round_vs_oracle():
+    """LoopbackClient.submit(dp=...) with in-process parties over 127.0.0.1:
+    every client perturbs its device copy (GaussianModelDP: clip to the
+    global norm + Philox noise) and masks it; the server's decoded sum equals
+    the oracle's sum of the perturbed vectors bit for bit (the noise taken
+    from the standalone perturb kernel, which test_fused_mask_dp_equals_
+    perturb_then_mask pins to the fused kernel)."""
+    import threading
+
+    from sfl_amd.loopback import LoopbackClient, LoopbackServer
+    from sfl_amd.security.privacy import GaussianModelDP
+
+    K = _K()
+    names, n = ["p0", "p1", "p2"], 30_011
+    seeds = o.seeds_for(names)
+    rng = np.random.default_rng(9)
+    xs = [(rng.standard_normal(n) * 0.05).astype(np.float32) for _ in names]
+    srv = LoopbackServer(len(names))
+    res = {}
+
+    def client(i):
+        cl = LoopbackClient(names[i], i, srv.port, seeds={v: seeds[names[i]][v] for v in names if v != names[i]})
+        cl.handshake()
+        dp = GaussianModelDP(noise_multiplier=0.5, num_clients=3, l2_norm_clip=0.8, seed=100 + i)
+        out = np.empty(n, dtype=np.float64)
+        cl.submit(xs[i], 0, dp=dp, result_into=out)
+        res[i] = (cl.result(n), cl.last_result_xor)
+        cl.close()
+
+    ts = [threading.Thread(target=client, args=(i,)) for i in range(len(names))]
+    for t in ts:
+        t.start()
+    srv.accept(timeout=60)
+    got, _ = srv.round(n, 0)
+    for t in ts:
+        t.join(60)
+    srv.close()
+    # the expected perturbed inputs, from the same DP parameters
+    xp = []
+    for i, x in enumerate(xs):
+        dp = GaussianModelDP(noise_multiplier=0.5, num_clients=3, l2_norm_clip=0.8, seed=100 + i)
+        d = torch.from_numpy(x).to(DEV)
+        xp.append(K.dp_perturb(d, torch.empty_like(d), dp.params(dp.sumsq([d]), n)).cpu().numpy())
+    exp = o.secure_sum(xp, names, seeds=seeds)[0]
+    assert np.array_equal(got, exp)
+    for i in range(len(names)):
+        assert np.array_equal(res[i][0], exp)
+        assert res[i][1] == int(np.bitwise_xor.reduce(exp.view(np.uint64)))
+    assert float(np.abs(exp - np.sum(xs, axis=0)).max()) > 1e-4  # the noise is there
