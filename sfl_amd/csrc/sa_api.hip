@@ -10,6 +10,7 @@
 #include "../../include/sfl_sa.h"
 #include "pcg128.h"
 #include "sa_internal.h"
+#include "sa_philox.h"
 
 namespace sa {
 
@@ -290,6 +291,7 @@ int sa_mask_impl(const void* x, int x_type, int compute_type, uint64_t n, double
       a.dp_clip = dp->l2_norm_clip;
       a.dp_sigma = dp->noise_std;
       a.dp_updates = dp->num_updates;
+      a.dp_inv = exact_recip_pow2(dp->num_updates);
       a.dp_sumsq = dp->sumsq;
       a.dp_sumsq_layer = dp->sumsq_layer;
       a.dp_key = dp->key;

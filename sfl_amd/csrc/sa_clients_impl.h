@@ -814,11 +814,12 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
     const bool cont = kGeneral && ka->continue_mode;
     if constexpr (kGeneral && std::is_same<XT, float>::value && std::is_same<CT, float>::value) {
       if (ka->dp_on && !cont) {  // fused DP pre-step (sa_mask_dp)
-        const Normal4 z = gauss4(ka->dp_key, ka->dp_block0 + (i >> 2));
-        const int h = (int)(i & 2);
+        // the lane's two elements are Box-Muller pair (i & 2) / 2 of their
+        // Philox block: only that pair is formed
+        const Normal2 z = gauss2(ka->dp_key, ka->dp_block0 + (i >> 2), (int)((i >> 1) & 1));
 #pragma unroll
         for (int k = 0; k < kE; k++)
-          xv[0].v[k] = dp_apply(xv[0].v[k], dp_s, h ? z.z[2 + k] : z.z[k], ka->dp_sigma, ka->dp_updates);
+          xv[0].v[k] = dp_apply(xv[0].v[k], dp_s, z.z[k], ka->dp_sigma, ka->dp_updates, ka->dp_inv);
       }
     }
     const QScale qs{ka->scale_f, ka->scale_d, ka->fxp_bits};

@@ -50,7 +50,7 @@ struct DpArgs {
   uint64_t n;
   const double* sumsq;
   const double* sumsq_layer;
-  float clip, sigma, updates;
+  float clip, sigma, updates, inv;  // inv: exact_recip_pow2(updates) or 0
   uint64_t key, block0;
 };
 
@@ -65,13 +65,13 @@ __global__ void __launch_bounds__(256) k_dp_perturb(const DpArgs a) {
     if (e + 4 <= a.n) {
       const float4 v = reinterpret_cast<const float4*>(a.x)[b];
       float4 o;
-      o.x = dp_apply(v.x, scale, z.z[0], a.sigma, a.updates);
-      o.y = dp_apply(v.y, scale, z.z[1], a.sigma, a.updates);
-      o.z = dp_apply(v.z, scale, z.z[2], a.sigma, a.updates);
-      o.w = dp_apply(v.w, scale, z.z[3], a.sigma, a.updates);
+      o.x = dp_apply(v.x, scale, z.z[0], a.sigma, a.updates, a.inv);
+      o.y = dp_apply(v.y, scale, z.z[1], a.sigma, a.updates, a.inv);
+      o.z = dp_apply(v.z, scale, z.z[2], a.sigma, a.updates, a.inv);
+      o.w = dp_apply(v.w, scale, z.z[3], a.sigma, a.updates, a.inv);
       reinterpret_cast<float4*>(a.out)[b] = o;
     } else {
-      for (int k = 0; e + k < a.n; k++) a.out[e + k] = dp_apply(a.x[e + k], scale, z.z[k], a.sigma, a.updates);
+      for (int k = 0; e + k < a.n; k++) a.out[e + k] = dp_apply(a.x[e + k], scale, z.z[k], a.sigma, a.updates, a.inv);
     }
   }
 }
@@ -115,8 +115,8 @@ extern "C" int sa_dp_perturb_f32(const float* x, uint64_t n, const sa_dp* dp, fl
   }
   if (!dp_ok(dp, "sa_dp_perturb_f32")) return SA_ERR_ARG;
   if (n == 0) return SA_OK;
-  DpArgs a{x, out, n, dp->sumsq, dp->sumsq_layer, dp->l2_norm_clip, dp->noise_std, dp->num_updates, dp->key,
-           dp->counter0 / 4};
+  DpArgs a{x,  out, n, dp->sumsq, dp->sumsq_layer, dp->l2_norm_clip, dp->noise_std, dp->num_updates,
+           exact_recip_pow2(dp->num_updates), dp->key, dp->counter0 / 4};
   const int maxb = occupancy_blocks((const void*)&k_dp_perturb);
   if (maxb <= 0) return SA_ERR_HIP;
   const uint64_t want = ((n + 3) / 4 + 255) / 256;

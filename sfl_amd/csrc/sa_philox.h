@@ -8,6 +8,7 @@
 // bit for bit.
 #pragma once
 #include <stdint.h>
+#include <string.h>
 
 namespace sa {
 
@@ -37,34 +38,75 @@ SA_PHX_HD inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 }
 
 #if defined(__HIPCC__)
-// 4 standard normals of counter block `blk` under `key`.  Never inlined: the
-// libm calls inside (logf, sincospif) are otherwise optimised together with
-// the caller, and contraction / scheduling decisions that differ between the
-// fused masking kernel and the standalone perturb kernel changed the last
-// bit of some normals.  As a called function every kernel runs the same
-// instruction sequence.
-__device__ __noinline__ Normal4 gauss4(uint64_t key, uint64_t blk) {
-  uint32_t c[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u};
-  philox4x32_10(c, (uint32_t)key, (uint32_t)(key >> 32));
-  Normal4 o;
-#pragma unroll
-  for (int j = 0; j < 2; j++) {
-    const float u1 = (float)((c[2 * j] >> 8) + 1u) * 0x1p-24f;  // (0, 1]
-    const float u2 = (float)(c[2 * j + 1] >> 8) * 0x1p-24f;     // [0, 1)
-    const float rad = sqrtf(-2.0f * logf(u1));
-    float s, co;
-    sincospif(2.0f * u2, &s, &co);
-    o.z[2 * j] = rad * co;
-    o.z[2 * j + 1] = rad * s;
-  }
+struct Normal2 {
+  float z[2];
+};
+
+// Box-Muller of one pair of Philox words -> 2 standard normals.
+__device__ __forceinline__ Normal2 box_muller(uint32_t w0, uint32_t w1) {
+  const float u1 = (float)((w0 >> 8) + 1u) * 0x1p-24f;  // (0, 1]
+  const float u2 = (float)(w1 >> 8) * 0x1p-24f;         // [0, 1)
+  const float rad = sqrtf(-2.0f * logf(u1));
+  float s, co;
+  sincospif(2.0f * u2, &s, &co);
+  Normal2 o;
+  o.z[0] = rad * co;
+  o.z[1] = rad * s;
   return o;
+}
+
+__device__ __forceinline__ void philox_block(uint64_t key, uint64_t blk, uint32_t c[4]) {
+  c[0] = (uint32_t)blk;
+  c[1] = (uint32_t)(blk >> 32);
+  c[2] = c[3] = 0u;
+  philox4x32_10(c, (uint32_t)key, (uint32_t)(key >> 32));
+}
+
+// The two entry points below are never inlined.  Inlined, the libm code in
+// Box-Muller (logf, sincospif) is contracted together with the caller's
+// arithmetic (rad * co with the noise scaling), and the fused masking kernel
+// and the standalone perturb kernel then differed in the last bit of some
+// normals; returned from a call, every normal is rounded the same way.  Out
+// of line also keeps the Philox rounds' registers out of the masking kernel
+// (sa_mask_dp).  tests/test_gpu_dp.py checks the two paths bit for bit.
+
+// Box-Muller pair j (normals 2j, 2j+1) of counter block `blk` under `key`:
+// the fused masking kernel needs one pair per lane.
+__device__ __noinline__ Normal2 gauss2(uint64_t key, uint64_t blk, int j) {
+  uint32_t c[4];
+  philox_block(key, blk, c);
+  return j ? box_muller(c[2], c[3]) : box_muller(c[0], c[1]);
+}
+
+// All 4 standard normals of counter block `blk` (one Philox block).
+__device__ __noinline__ Normal4 gauss4(uint64_t key, uint64_t blk) {
+  uint32_t c[4];
+  philox_block(key, blk, c);
+  const Normal2 a = box_muller(c[0], c[1]), b = box_muller(c[2], c[3]);
+  return Normal4{{a.z[0], a.z[1], b.z[0], b.z[1]}};
+}
+
+// 1/u when u is a positive normal power of two whose reciprocal is normal
+// (then z·(1/u) rounded once IS z/u rounded once: the exact values are
+// equal), else 0 -- the launchers pass it so dp_apply multiplies instead of
+// dividing for the common num_updates = 2^k.
+__host__ __device__ inline float exact_recip_pow2(float u) {
+  uint32_t b;
+  memcpy(&b, &u, sizeof(b));
+  const uint32_t e = (b >> 23) & 0xFFu;
+  if ((b & 0x807FFFFFu) || e == 0 || e >= 253) return 0.0f;
+  const uint32_t r = (254u - e) << 23;
+  float f;
+  memcpy(&f, &r, sizeof(f));
+  return f;
 }
 
 // x' = x * scale + (z * sigma) / num_updates, float32 in the reference's
 // operation order (mechanism_fl.py:112-127: clip, astype(float32) noise,
-// noise / num_updates, np.add).
-__device__ __forceinline__ float dp_apply(float x, float scale, float z, float sigma, float updates) {
-  return __fadd_rn(__fmul_rn(x, scale), __fdiv_rn(__fmul_rn(z, sigma), updates));
+// noise / num_updates, np.add); inv = exact_recip_pow2(updates) or 0.
+__device__ __forceinline__ float dp_apply(float x, float scale, float z, float sigma, float updates, float inv) {
+  const float zs = __fmul_rn(z, sigma);
+  return __fadd_rn(__fmul_rn(x, scale), inv != 0.0f ? __fmul_rn(zs, inv) : __fdiv_rn(zs, updates));
 }
 
 // scale = min(1, clip / norm) in float32 (mechanism_fl.py:107); with a layer

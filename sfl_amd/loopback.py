@@ -496,8 +496,8 @@ class LoopbackClient:
 
     def submit(self, x: np.ndarray, rnd: int, weight=None, dp=None, result_into: np.ndarray | None = None) -> dict:
         """Mask ``x`` (host float32) for round ``rnd`` and send it.  With a
-        ``GaussianModelDP`` ``dp``, its clip + noise is applied to the device
-        copy of ``x`` first (``sa_dp_perturb_f32`` in place).  ``x`` streams to
+        ``GaussianModelDP`` ``dp``, its clip + noise runs inside the masking
+        kernel (``sa_mask_dp``) on the device copy of ``x``.  ``x`` streams to
         the device through two pinned chunk buffers; the masked vector comes
         back chunk by chunk into registered memfd pages, each chunk sent as it
         lands.
@@ -558,13 +558,11 @@ class LoopbackClient:
             dig = torch.zeros(1, dtype=torch.int64, device=dev)
             flags = torch.zeros(1, dtype=torch.int32, device=dev)
             w = 1.0 if weight is None else weight
-            if dp is not None:
-                # clip + noise in place on the device copy, then the lean
-                # masking kernel: bit-identical to the fused sa_mask_dp and
-                # 9 % faster on MI355X (both halves are VALU-bound, so fusing
-                # saves only HBM bytes that do not bind; tools/dp_bench.py)
-                K.dp_perturb(dx, dx, dp.params(dp.sumsq([dx]), n))
-            K.mask(dx, dm, self.masker.streams(), weight=w, fxp_bits=self.fxp_bits, digest=dig, flags=flags)
+            if dp is None:
+                K.mask(dx, dm, self.masker.streams(), weight=w, fxp_bits=self.fxp_bits, digest=dig, flags=flags)
+            else:  # clip + noise inside the masking kernel (sa_mask_dp; tools/dp_bench.py)
+                K.mask_dp(dx, dm, self.masker.streams(), dp.params(dp.sumsq([dx]), n), weight=w,
+                          fxp_bits=self.fxp_bits, digest=dig, flags=flags)
         with clock("client: last H2D + mask kernel (GPU)"):
             cs.synchronize()
         extra = {}

@@ -55,21 +55,22 @@ def test_perturb_clip_exact_without_noise(clip):
     assert np.array_equal(y.cpu().numpy(), x.cpu().numpy() * scale)
 
 
-def test_perturb_noise_matches_oracle_stream():
+@pytest.mark.parametrize("updates", [4, 3])
+def test_perturb_noise_matches_oracle_stream(updates):
     K = _K()
     n, key, ctr = 100_003, 0xDEADBEEF12345678, 4 * 1000
     x = torch.zeros(n, device=DEV)
     s = _sumsq(torch.ones(4, device=DEV))
-    dp = K.make_dp(s, l2_norm_clip=1.0, noise_std=1.5, num_updates=4, key=key, counter0=ctr)
+    dp = K.make_dp(s, l2_norm_clip=1.0, noise_std=1.5, num_updates=updates, key=key, counter0=ctr)
     y = K.dp_perturb(x, torch.empty_like(x), dp).cpu().numpy()
     z = D.gauss(key, ctr, n)
-    exp = D.perturb(np.zeros(n, np.float32), 1.0, z, 1.5, 4)
+    exp = D.perturb(np.zeros(n, np.float32), 1.0, z, 1.5, updates)
     assert np.allclose(y, exp, rtol=2e-5, atol=2e-6)
-    assert abs(y.mean()) < 0.01 and abs(y.std() - 1.5 / 4) < 0.01
+    assert abs(y.mean()) < 0.01 and abs(y.std() - 1.5 / updates) < 0.01
 
 
-@pytest.mark.parametrize("nstreams", [0, 3, 17])
-def test_fused_mask_dp_equals_perturb_then_mask(nstreams):
+@pytest.mark.parametrize("nstreams,updates", [(0, 8), (3, 8), (17, 8), (3, 3), (7, 6)])
+def test_fused_mask_dp_equals_perturb_then_mask(nstreams, updates):
     K, L = _K(), None
     from sfl_amd import _lib as L
 
@@ -78,7 +79,8 @@ def test_fused_mask_dp_equals_perturb_then_mask(nstreams):
     s = _sumsq(x)
     seeds = [o.pair_seed(0, j + 1) for j in range(nstreams)]
     streams = [(L.pcg64_from_seed(sd), 1 if j % 2 else -1, j) for j, sd in enumerate(seeds)]
-    mk = lambda: K.make_dp(s, l2_norm_clip=0.3, noise_std=0.01, num_updates=8, key=77, counter0=40)  # noqa: E731
+    # num_updates a power of two: the kernels multiply by the exact reciprocal; else IEEE division
+    mk = lambda: K.make_dp(s, l2_norm_clip=0.3, noise_std=0.01, num_updates=updates, key=77, counter0=40)  # noqa: E731
     xp = K.dp_perturb(x, torch.empty_like(x), mk())
     m1 = torch.empty(n, dtype=torch.int64, device=DEV)
     d1 = torch.zeros(1, dtype=torch.int64, device=DEV)
