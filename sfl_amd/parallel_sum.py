@@ -7,10 +7,13 @@ ONE fused launch (``sa_fused_clients``) over its L = C/W local clients:
 internal pair streams are expanded once and applied to both clients, each
 local client additionally applies its C - L cross-rank streams (the peer's
 half of those pairs runs on the peer's rank).  The only exchange is the
-uint64 masked partial sum, reduced to rank 0 (the server) by ``ncclReduce``
-(``sa_comm_reduce_u64``) — bit-exact for any RCCL algorithm because uint64
-addition is associative mod 2^64.  This replaces the RayFed ``.to(server)``
-transfer plus the server ``np.sum`` (sfl/distributed/op_strategy.py:131-141,
+uint64 masked partial sum: reduce-scattered so that every rank is the
+server of one shard and decodes it (``sa_comm_reduce_scatter_u64``, the
+bench's headline design, optionally followed by a float64 gather to the
+root), or reduced to rank 0 by ``ncclReduce`` (``sa_comm_reduce_u64``) —
+bit-exact for any RCCL algorithm because uint64 addition is associative
+mod 2^64.  This replaces the RayFed ``.to(server)`` transfer plus the
+server ``np.sum`` (sfl/distributed/op_strategy.py:131-141,
 sfl/security/aggregation/sparse_plain_aggregator.py:86-94).
 
 The shard planning here is pure host logic (tested with gloo on CPU); the
