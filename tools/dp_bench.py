@@ -13,7 +13,7 @@ against the masking it rides on, one client of --elems float32 elements:
 
 Median of --reps launches per pass (HIP events), the cases interleaved over
 --passes after a clock warm-up; one JSON line per case (median of the passes).
-usage: python tools/dp_bench.py [--elems 100000000] [--streams 7] [--reps 20]
+usage: python tools/dp_bench.py [--elems 100000000] [--streams 7] [--reps 20] [--passes 3]
 """
 import argparse
 import json
@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--streams", type=int, default=7)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--passes", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=30, help="lean masking launches before the first case")
     args = ap.parse_args()
     import torch
 
@@ -52,7 +53,7 @@ def main():
     streams = [(L.pcg64_from_seed(pair_seed(0, v + 1)), 1 if v % 2 else -1, v) for v in range(args.streams)]
 
     def time(fn):
-        for _ in range(5):
+        for _ in range(min(5, args.reps)):
             fn()
         ts = []
         for _ in range(args.reps):
@@ -75,7 +76,7 @@ def main():
     ]
     # warm the clocks, then interleave the cases over passes (the first
     # launches after idle run at lower clocks)
-    for _ in range(30):
+    for _ in range(args.warmup):
         K.mask(x, out, streams)
     res = {name: [] for name, _, _ in cases}
     for _ in range(args.passes):

@@ -8,7 +8,8 @@
 #      tools/kernel_bench.py over every per-rank shape (8 clients over 1, 2, 4, 8
 #      GPUs at 100M element positions) + the bipartite launch + the k_sum_u64
 #      calibration launch whose bytes are known, and on tools/server_bench.py
-#      (k_sum_u64, k_decode, k_sum_f64); the SQ issue census (tools/pmc_sq.sh)
+#      (k_sum_u64, k_decode, k_sum_f64) and tools/dp_bench.py (the DP
+#      pre-step kernels); the SQ issue census (tools/pmc_sq.sh)
 #   4. microbenchmarks: per-instruction issue cost of the draw (draw_ops),
 #      HBM streaming shapes (stream_rate)
 # Copy what should be judged into profiles/<round>/ afterwards
@@ -32,6 +33,13 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_server_write -o run -- \
   python3 tools/server_bench.py --reps 3 > gpurun_out/pmc_server_write.log 2>&1
 tools/pmc_sq.sh 8:1,8:8 > /dev/null
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_dp -o run -- \
+  python3 tools/dp_bench.py --reps 10 --passes 1 > gpurun_out/dp_bench_prof.jsonl 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_dp_fetch -o run -- \
+  python3 tools/dp_bench.py --reps 2 --passes 1 --warmup 0 > gpurun_out/pmc_dp_fetch.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_dp_write -o run -- \
+  python3 tools/dp_bench.py --reps 2 --passes 1 --warmup 0 > gpurun_out/pmc_dp_write.log 2>&1
+timeout -k 10 200 python tools/dp_bench.py > gpurun_out/dp_bench.jsonl 2>&1
 timeout -k 10 120 python -u tools/kernel_bench.py --rounds 5 > gpurun_out/kb_shapes.jsonl
 timeout -k 10 120 tools/microbench/draw_ops > gpurun_out/draw_ops.jsonl
 timeout -k 10 200 tools/microbench/stream_rate > gpurun_out/stream_rate.jsonl

@@ -14,6 +14,10 @@ cp gpurun_out/pmc_fetch/run_counter_collection.csv $P/pmc_fetch_size.csv
 cp gpurun_out/pmc_write/run_counter_collection.csv $P/pmc_write_size.csv
 cp gpurun_out/pmc_server_fetch/run_counter_collection.csv $P/pmc_server_fetch_size.csv
 cp gpurun_out/pmc_server_write/run_counter_collection.csv $P/pmc_server_write_size.csv
+cp gpurun_out/prof_dp/run_kernel_stats.csv $P/dp_kernel_stats.csv
+cp gpurun_out/pmc_dp_fetch/run_counter_collection.csv $P/pmc_dp_fetch_size.csv
+cp gpurun_out/pmc_dp_write/run_counter_collection.csv $P/pmc_dp_write_size.csv
+grep '^{' gpurun_out/dp_bench.jsonl > $P/dp_bench.jsonl
 python3 - "$P" <<'PY'
 import csv, sys
 P = sys.argv[1]
