@@ -16,9 +16,10 @@ GPU, config 3 at N=8); each rank runs the fused masking over its clients
 of the uint64 partial sums over xGMI.  `value` is measured on the sharded
 server (ncclReduceScatter in place, every rank decodes its
 shard of the masked sum); the same process group then times every other
-design (`exchange_variants`: the shards also gathered to rank 0, ncclReduce
-of the partial sums to rank 0, element sharding with and without the
-gather), so one run reports them all.  Total work is fixed as N grows:
+design (`exchange_variants`: the shards also gathered to rank 0, the
+sharded server over direct shard transfers, ncclReduce of the partial sums
+to rank 0, element sharding with and without the gather), so one run
+reports them all.  Total work is fixed as N grows:
 "scaling": "strong".  `python bench.py --gpus N` starts its N rank
 processes itself (torch.distributed.run as a child process with a c10d
 rendezvous on 127.0.0.1 port 0, before this process touches the GPU); under
@@ -254,17 +255,20 @@ def kernel_variant(L: int, X: int, digests: bool) -> int:
 #                    ncclReduceScatter'ed in place, each rank decodes its shard
 #                    (the sharded server) -- the default
 #   sharded+gather   ... and the float64 shards gathered to rank 0
+#   direct           the sharded server with the reduce-scatter done as direct
+#                    shard transfers (grouped ncclSend/Recv: each shard crosses
+#                    one xGMI link) + a local k_sum_u64 of the W shards
 #   reduce           client sharding, ncclReduce of the partial sums to rank 0
 #   elements         element sharding: every rank masks 1/N of EVERY client's
 #                    elements, no exchange for the sum (not config 3: a
 #                    client's raw gradient on every GPU), decodes its slice
 #   elements+gather  ... and the float64 slices gathered to rank 0
-VARIANTS = ("sharded", "sharded+gather", "reduce", "elements", "elements+gather")
+VARIANTS = ("sharded", "sharded+gather", "direct", "reduce", "elements", "elements+gather")
 
 
 class Variant:
     def __init__(self, name: str):
-        if name not in VARIANTS and name != "local":
+        if name not in VARIANTS and name not in ("local", "direct+gather"):
             raise ValueError(f"unknown exchange variant {name!r}")
         self.name = name
         self.shard = "elements" if name.startswith("elements") else "clients"
@@ -280,7 +284,7 @@ def headline_variant(args, multi: bool) -> Variant:
     if args.shard == "elements":
         return Variant("elements+gather" if args.gather else "elements")
     ex = args.exchange or "sharded"
-    return Variant("sharded+gather" if ex == "sharded" and args.gather else ex)
+    return Variant(f"{ex}+gather" if ex in ("sharded", "direct") and args.gather else ex)
 
 
 def other_variants(args, head: Variant) -> list[Variant]:
@@ -434,9 +438,11 @@ def workload(args, world: int, v: Variant) -> str:
     return (f"{C} clients x {N} fp32 grad elems over {world} GPUs, fxp {args.fxp_bits}, ring 2^64; per rank: "
             f"{L} local client(s), {pairs} internal pair + {L * X} cross streams "
             f"(k_clients<float,float,{L},{X}>), pipelined " +
-            ("ncclReduceScatter(uint64) of the partial sum, each rank decoding its shard (sharded server)"
-             + (" and gathering the float64 shards to rank 0" if v.gather else "")
-             if v.exchange == "sharded" else "ncclReduce(uint64) of the partial sum to rank 0"))
+            {"sharded": "ncclReduceScatter(uint64) of the partial sum, each rank decoding its shard (sharded server)",
+             "direct": "direct shard transfers (ncclSend/Recv, uint64) of the partial sum, each rank summing "
+                       "and decoding its shard (sharded server)",
+             }.get(v.exchange, "ncclReduce(uint64) of the partial sum to rank 0")
+            + (" and gathering the float64 shards to rank 0" if v.gather else ""))
 
 
 def collective_text(v: Variant) -> str:
@@ -448,12 +454,17 @@ def collective_text(v: Variant) -> str:
         return ("sharded server: ncclReduceScatter(uint64, sum) in place, every rank decodes its shard "
                 "(k_decode on the comm stream)" + (", float64 shards gathered to rank 0 (ncclSend/Recv)"
                                                    if v.gather else ""))
+    if v.exchange == "direct":
+        return ("sharded server, direct: every shard sent to its server rank over one link (grouped "
+                "ncclSend/Recv, uint64), the rank sums the world shards (k_sum_u64) and decodes them "
+                "(k_decode), both on the comm stream" + (", float64 shards gathered to rank 0 (ncclSend/Recv)"
+                                                        if v.gather else ""))
     return "ncclReduce(uint64, sum) in place to rank 0"
 
 
 class GlooStandinComm:
     """--rehearse-one-gpu only: RcclComm's contract (reduce_u64,
-    reduce_scatter_u64, gather_f64) through gloo host round trips, so N rank
+    reduce_scatter_u64, alltoall_u64, gather_f64) through gloo host round trips, so N rank
     processes can run every design's code path on ONE GPU (RCCL refuses two
     ranks on one device: "Duplicate GPU detected").  Called on the comm
     stream like RcclComm; ``send.cpu()`` waits for the chunk's launch.  Its
@@ -481,6 +492,19 @@ class GlooStandinComm:
         dist.all_reduce(host, op=dist.ReduceOp.SUM)
         k = recv.numel()
         recv.copy_(host[self.rank * k:(self.rank + 1) * k])
+        return recv
+
+    def alltoall_u64(self, send, recv):
+        import torch
+        import torch.distributed as dist
+
+        host = send.cpu()
+        parts = [torch.empty_like(host) for _ in range(self.world)]
+        dist.all_gather(parts, host)
+        k = host.numel() // self.world
+        for p in range(self.world):
+            if p != self.rank:
+                recv[p * k:(p + 1) * k].copy_(parts[p][self.rank * k:(self.rank + 1) * k])
         return recv
 
     def gather_f64(self, send, recv, root: int = 0):
@@ -524,9 +548,9 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
         del x
     total = warmup + steps
     chunks = args.chunks if args.chunks is not None else (8 if world > 1 and not by_elems else 1)
-    sharded = v.exchange == "sharded"
+    sharded = v.exchange in ("sharded", "direct")
     pipe = PipelinedMaskedSum(None if by_elems else comm, dev, n_loc, chunks,
-                              exchange="sharded" if sharded else "reduce")
+                              exchange=v.exchange if sharded else "reduce")
     # every step is a new round: streams start i*N draws in, chunk j at +lo_j
     gens = [[plan_generators(plan, pair_seed, offset=i * N + e0 + lo) for lo, _ in pipe.bounds]
             for i in range(total)]
@@ -657,10 +681,11 @@ def main():
                          "(rehearsal of the N>1 path on one GPU)")
     ap.add_argument("--chunks", type=int, default=None,
                     help="masking/exchange pipeline depth (default 8 for N>1, 1 at N=1)")
-    ap.add_argument("--exchange", choices=("reduce", "sharded"), default=None,
+    ap.add_argument("--exchange", choices=("reduce", "sharded", "direct"), default=None,
                     help="N>1 headline exchange: the sharded server of SURVEY.md 8(e) (default: "
-                         "ncclReduceScatter, every rank decodes its shard), or ncclReduce of the partial sums "
-                         "to rank 0")
+                         "ncclReduceScatter, every rank decodes its shard), the same server with direct shard "
+                         "transfers (grouped ncclSend/Recv) and a local k_sum_u64, or ncclReduce of the partial "
+                         "sums to rank 0")
     ap.add_argument("--gather", action="store_true",
                     help="with --exchange sharded or --shard elements: also gather the decoded float64 shards "
                          "to rank 0")

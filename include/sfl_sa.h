@@ -281,6 +281,14 @@ int sa_comm_allreduce_u64(void* comm, const uint64_t* send, uint64_t* recv, uint
  * over the ranks. */
 int sa_comm_reduce_scatter_u64(void* comm, const uint64_t* send, uint64_t* recv, uint64_t count,
                                void* stream);
+/* The sharded server's exchange as direct transfers (each shard crosses one
+ * point-to-point xGMI link): for every rank p != r, rank r's recv[p*count,
+ * (p+1)*count) = rank p's send[r*count, (r+1)*count) (grouped ncclSend /
+ * ncclRecv); recv's slot r is not written.  The caller sums the shards with
+ * sa_sum_u64 (its own shard from send): the same result and wire bytes as
+ * sa_comm_reduce_scatter_u64, without RCCL's reduce schedule. */
+int sa_comm_alltoall_u64(void* comm, const uint64_t* send, uint64_t* recv, uint64_t count,
+                         void* stream);
 /* The decoded float64 shards to the server: on root, recv[r*count, (r+1)*count)
  * = rank r's send (grouped ncclSend/ncclRecv); recv may be NULL off root. */
 int sa_comm_gather_f64(void* comm, const double* send, double* recv, uint64_t count, int root,

@@ -87,6 +87,41 @@ extern "C" int sa_comm_reduce_scatter_u64(void* comm, const uint64_t* send, uint
   return SA_OK;
 }
 
+// The sharded server's exchange as direct transfers over the point-to-point
+// xGMI links: rank r sends shard p of `send` (count elements at send +
+// p*count) to rank p and receives rank p's shard r into recv + p*count, for
+// every p != r, in one grouped ncclSend/ncclRecv round; recv's slot r is not
+// written (the caller's own shard stays in send).  The caller then sums the
+// world shards (sa_sum_u64).  The same bytes as sa_comm_reduce_scatter_u64,
+// each shard crossing exactly one link, instead of RCCL's reduce-scatter
+// schedule (rings or trees of partial sums).
+extern "C" int sa_comm_alltoall_u64(void* comm, const uint64_t* send, uint64_t* recv, uint64_t count,
+                                    void* stream) {
+  if (!comm || !send || !recv) {
+    sa_set_error("sa_comm_alltoall_u64: bad arguments");
+    return SA_ERR_ARG;
+  }
+  ncclComm_t c = (ncclComm_t)comm;
+  int rank = 0, nranks = 0;
+  SA_NCCL_CHECK(ncclCommUserRank(c, &rank));
+  SA_NCCL_CHECK(ncclCommCount(c, &nranks));
+  if (count == 0 || nranks == 1) return SA_OK;
+  hipStream_t s = (hipStream_t)stream;
+  SA_NCCL_CHECK(ncclGroupStart());
+  for (int k = 1; k < nranks; ++k) {  // peers in ring order from this rank: every link busy at once
+    const int to = (rank + k) % nranks, from = (rank - k + nranks) % nranks;
+    ncclResult_t e = ncclSend(send + (size_t)to * count, (size_t)count, ncclUint64, to, c, s);
+    if (e == ncclSuccess) e = ncclRecv(recv + (size_t)from * count, (size_t)count, ncclUint64, from, c, s);
+    if (e != ncclSuccess) {
+      ncclGroupEnd();
+      sa_set_error("sa_comm_alltoall_u64: send/recv with rank %d/%d failed: %s", to, from, ncclGetErrorString(e));
+      return SA_ERR_RCCL;
+    }
+  }
+  SA_NCCL_CHECK(ncclGroupEnd());
+  return SA_OK;
+}
+
 // float64 shards to the server: root's recv[r*count, (r+1)*count) = rank r's
 // send (one grouped ncclSend/ncclRecv round; root's own shard is a device copy
 // unless it is already in place).  recv is only read on root (may be NULL

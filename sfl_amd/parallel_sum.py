@@ -124,6 +124,19 @@ class RcclComm:
                                                    recv.numel(), C.c_void_p(stream)), "sa_comm_reduce_scatter_u64")
         return recv
 
+    def alltoall_u64(self, send, recv):
+        """For every rank p != this one: ``recv``'s p-th of ``world`` equal
+        slots = rank p's shard (this rank's slot) of ``send``; this rank's own
+        slot of ``recv`` is not written (its shard stays in ``send``)."""
+        import torch
+
+        if send.numel() != recv.numel() or send.numel() % self.world:
+            raise ValueError(f"alltoall: {send.numel()} / {recv.numel()} elements do not split into {self.world} slots")
+        stream = torch.cuda.current_stream(send.device).cuda_stream
+        L.check(L.lib().sa_comm_alltoall_u64(self._h, C.c_void_p(send.data_ptr()), C.c_void_p(recv.data_ptr()),
+                                             send.numel() // self.world, C.c_void_p(stream)), "sa_comm_alltoall_u64")
+        return recv
+
     def gather_f64(self, send, recv, root: int = 0):
         """Root's ``recv`` (``world`` x ``send.numel()``) = every rank's float64 shard in rank order."""
         import torch
@@ -209,15 +222,19 @@ class PipelinedMaskedSum:
     place (rank r receives the masked sum of its shard, ``shard_layout``),
     every rank decodes its shard into ``dec`` on the comm stream, and with
     ``gather=True`` the float64 shards are gathered into the root's ``dec``.
+    ``exchange="direct"``: the same sharded server with the reduce-scatter
+    done as direct shard transfers (``alltoall_u64``: each shard crosses one
+    link into a staging buffer) and a local ``sum_u64`` of the ``world``
+    shards into this rank's shard of the partial sum.
     Partial-sum and ``dec`` buffers hold ``self.buffer_len`` elements (n plus
     < world of padding that is reduced and decoded but never read)."""
 
     def __init__(self, comm: RcclComm | None, device, n: int, chunks: int, exchange: str = "reduce"):
         import torch
 
-        if exchange not in ("reduce", "sharded"):
-            raise ValueError(f"exchange must be 'reduce' or 'sharded', not {exchange!r}")
-        if exchange == "sharded" and comm is None:
+        if exchange not in ("reduce", "sharded", "direct"):
+            raise ValueError(f"exchange must be 'reduce', 'sharded' or 'direct', not {exchange!r}")
+        if exchange != "reduce" and comm is None:
             raise ValueError("the sharded server needs a communicator")
         self.comm = comm
         self.device = device
@@ -227,9 +244,14 @@ class PipelinedMaskedSum:
         # sharded: chunk starts on multiples of 1024 * world, so only the last
         # chunk's shards can run past its end (into padding, never into the
         # next chunk that the compute stream may be masking)
-        self.bounds = chunk_bounds(n, chunks, align=1024 * world if exchange == "sharded" else 1024)
-        self.shards = shard_layout(self.bounds, world) if exchange == "sharded" else None
-        self.buffer_len = padded_len(self.bounds, world) if exchange == "sharded" else n
+        sharded = exchange != "reduce"
+        self.bounds = chunk_bounds(n, chunks, align=1024 * world if sharded else 1024)
+        self.shards = shard_layout(self.bounds, world) if sharded else None
+        self.buffer_len = padded_len(self.bounds, world) if sharded else n
+        # direct: the other ranks' shards of one chunk land here (the comm
+        # stream runs one chunk's exchange at a time, so one chunk's worth)
+        self.staging = (torch.empty(world * max(k for _, k in self.shards), dtype=torch.int64, device=device)
+                        if exchange == "direct" and world > 1 else None)
         self.comm_stream = torch.cuda.Stream(device) if comm is not None else None
         self.events = [torch.cuda.Event() for _ in self.bounds]
         # reduce of chunk j done (comm stream): the next round's chunk-j launch
@@ -256,7 +278,7 @@ class PipelinedMaskedSum:
 
         if len(chunk_gens) != len(self.bounds):
             raise ValueError(f"{len(chunk_gens)} generator sets for {len(self.bounds)} chunks")
-        sharded = self.exchange == "sharded"
+        sharded = self.exchange != "reduce"
         if sharded:
             if recv is not None:
                 raise ValueError("the sharded server reduces in place (recv=None)")
@@ -285,9 +307,15 @@ class PipelinedMaskedSum:
                         exchange_events[-1][0].record(self.comm_stream)
                     if sharded:
                         lo_s, k = self.shards[j]
-                        mine = lo_s + self.comm.rank * k
-                        shard = self.comm.reduce_scatter_u64(sum_buf[lo_s:lo_s + k * self.comm.world],
-                                                             sum_buf[mine:mine + k])
+                        W, r = self.comm.world, self.comm.rank
+                        mine = lo_s + r * k
+                        shard = sum_buf[mine:mine + k]
+                        if self.exchange == "sharded":
+                            self.comm.reduce_scatter_u64(sum_buf[lo_s:lo_s + k * W], shard)
+                        elif W > 1:  # direct: own shard first (sum_u64's out may alias in[0])
+                            st = self.staging[:k * W]
+                            self.comm.alltoall_u64(sum_buf[lo_s:lo_s + k * W], st)
+                            K.sum_u64([shard] + [st[p * k:(p + 1) * k] for p in range(W) if p != r], shard)
                         K.decode(shard, dec[mine:mine + k], fxp_bits=fxp_bits, divisor=divisor)
                         if gather:
                             self.comm.gather_f64(dec[mine:mine + k], dec[lo_s:lo_s + k * self.comm.world]

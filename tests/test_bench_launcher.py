@@ -76,6 +76,7 @@ def test_world_one_runs_in_process():
 @pytest.mark.parametrize("opts,expect", [
     (["--exchange", "sharded", "--gather"], "ncclReduceScatter(uint64) of the partial sum"),
     (["--exchange", "reduce"], "ncclReduce(uint64) of the partial sum to rank 0"),
+    (["--exchange", "direct"], "direct shard transfers (ncclSend/Recv, uint64) of the partial sum"),
     (["--shard", "elements"], "element-sharded: every rank masks its 1/2 of every client's elements"),
 ])
 def test_exchange_options_reach_every_rank(opts, expect):

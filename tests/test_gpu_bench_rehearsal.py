@@ -42,7 +42,7 @@ def test_bench_n_ranks_every_design(world):
     assert line["roofline"]["kernel"].startswith(f"k_clients<float, float, {per}, {8 - per}, ")
     assert line["exchange"]["chunks"] == 8
     names = [v["name"] for v in line["exchange_variants"]]
-    assert sorted(names) == sorted(["sharded", "sharded+gather", "reduce", "elements", "elements+gather"])
+    assert sorted(names) == sorted(["sharded", "sharded+gather", "direct", "reduce", "elements", "elements+gather"])
     for v in line["exchange_variants"]:
         assert v["value"] > 0 and v["kernel_ms_per_step"] > 0, v
         if v["name"].startswith("elements"):

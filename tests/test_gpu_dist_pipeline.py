@@ -132,6 +132,19 @@ class GlooShardedServer:
         recv.copy_(host[self.rank * k:(self.rank + 1) * k], non_blocking=False)
         return recv
 
+    def alltoall_u64(self, send, recv):
+        import torch
+        import torch.distributed as dist
+
+        host = send.cpu()
+        parts = [torch.empty_like(host) for _ in range(self.world)]
+        dist.all_gather(parts, host)
+        k = host.numel() // self.world
+        for p in range(self.world):
+            if p != self.rank:
+                recv[p * k:(p + 1) * k].copy_(parts[p][self.rank * k:(self.rank + 1) * k], non_blocking=False)
+        return recv
+
     def gather_f64(self, send, recv, root: int = 0):
         import torch
         import torch.distributed as dist
@@ -144,7 +157,7 @@ class GlooShardedServer:
         return recv
 
 
-def _worker_sharded(rank, world, init, n, chunks, offset, q):
+def _worker_sharded(rank, world, init, n, chunks, offset, exchange, q):
     import torch
     import torch.distributed as dist
 
@@ -161,7 +174,7 @@ def _worker_sharded(rank, world, init, n, chunks, offset, q):
         xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
         dev = torch.device("cuda", 0)
         plan = plan_rank(names, world, rank)
-        pipe = PipelinedMaskedSum(GlooShardedServer(rank, world), dev, n, chunks, exchange="sharded")
+        pipe = PipelinedMaskedSum(GlooShardedServer(rank, world), dev, n, chunks, exchange=exchange)
         gens = [plan_generators(plan, seed_of, offset=offset + lo) for lo, _ in pipe.bounds]
         part = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
         dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev)
@@ -180,14 +193,17 @@ def _worker_sharded(rank, world, init, n, chunks, offset, q):
         q.put((rank, repr(e), False))
 
 
+@pytest.mark.parametrize("exchange", ["sharded", "direct"])
 @pytest.mark.parametrize("world,chunks", [(2, 3), (4, 2), (8, 8)])
-def test_ranks_sharded_server(world, chunks):
-    """exchange="sharded" with W real ranks: every rank's shard of the masked
-    sum and its float64 decode equal the oracle's on that range, and the
-    root's gathered decode equals the oracle's whole decoded sum."""
+def test_ranks_sharded_server(world, chunks, exchange):
+    """exchange="sharded" (reduce-scatter) or "direct" (shard transfers +
+    a local sum_u64 through the staging buffer) with W real ranks: every
+    rank's shard of the masked sum and its float64 decode equal the oracle's
+    on that range, and the root's gathered decode equals the oracle's whole
+    decoded sum."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    res = _run_ranks(_worker_sharded, world, (70_001, chunks, 3 * 10**9 + 1))
+    res = _run_ranks(_worker_sharded, world, (70_001, chunks, 3 * 10**9 + 1, exchange))
     for rank, shard_ok, full_ok in res:
         assert shard_ok is True, (rank, shard_ok)
         assert full_ok, f"rank {rank}: gathered decode differs from the oracle"

@@ -133,8 +133,19 @@ def test_rccl_world1_reduce_scatter_and_gather(comm):
     assert torch.equal(g, f)
 
 
+def test_rccl_world1_alltoall_leaves_own_slot(comm):
+    """sa_comm_alltoall_u64 at world 1: no peer, so nothing moves and the
+    receive buffer's own slot is left untouched."""
+    send = torch.arange(4099, dtype=torch.int64, device="cuda")
+    recv = torch.full_like(send, -7)
+    comm.alltoall_u64(send, recv)
+    torch.cuda.synchronize()
+    assert bool((recv == -7).all())
+
+
+@pytest.mark.parametrize("exchange", ["sharded", "direct"])
 @pytest.mark.parametrize("chunks", [1, 3])
-def test_sharded_server_pipeline_world1(comm, chunks):
+def test_sharded_server_pipeline_world1(comm, chunks, exchange):
     """exchange="sharded" at world 1 (the whole vector is rank 0's shard):
     8 co-located clients, every chunk reduce-scattered, decoded on the comm
     stream and gathered, two rounds back to back (join=False); the decoded
@@ -147,7 +158,7 @@ def test_sharded_server_pipeline_world1(comm, chunks):
     seeds = o.seeds_for(names)
     plan = plan_rank(names, 1, 0)
     dev = torch.device("cuda", 0)
-    pipe = PipelinedMaskedSum(comm, dev, n, chunks, exchange="sharded")
+    pipe = PipelinedMaskedSum(comm, dev, n, chunks, exchange=exchange)
     assert pipe.buffer_len >= n
     seed_of = lambda u, v: seeds[names[u]][names[v]]  # noqa: E731
     s = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
@@ -165,7 +176,7 @@ def test_sharded_server_pipeline_world1(comm, chunks):
         assert np.array_equal(decs[r][:n].cpu().numpy(), exps[r]), r
 
 
-@pytest.mark.parametrize("exchange", ["reduce", "sharded"])
+@pytest.mark.parametrize("exchange", ["reduce", "sharded", "direct"])
 def test_pipelined_world1_at_1m_matches_oracle_server_sum(comm, exchange):
     """bench.py --gpus 1 --dist's data path at n = 1,000,003: 8 co-located
     clients, the bench's 8-chunk pipeline through RcclComm (ncclReduce in
@@ -188,7 +199,7 @@ def test_pipelined_world1_at_1m_matches_oracle_server_sum(comm, exchange):
     seed_of = lambda u, v: seeds[names[u]][names[v]]  # noqa: E731
     gens = [plan_generators(plan, seed_of, offset=rnd * n + lo) for lo, _ in pipe.bounds]
     s = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
-    dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev) if exchange == "sharded" else None
+    dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev) if exchange != "reduce" else None
     flags = torch.zeros(1, dtype=torch.int32, device=dev)
     pipe.run([torch.from_numpy(x).to(dev) for x in xs], [1.0] * C, gens, plan.n_cross, s, None, flags=flags,
              dec=dec)
@@ -200,6 +211,13 @@ def test_pipelined_world1_at_1m_matches_oracle_server_sum(comm, exchange):
 
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def bench_variants():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    return bench.VARIANTS
 
 
 @pytest.mark.parametrize("opts", [["--exchange", "reduce"], ["--exchange", "sharded", "--gather"]])
@@ -226,6 +244,6 @@ def test_bench_self_launched_dist_world1(opts):
     want = "reduce" if opts[1] == "reduce" else "sharded+gather"
     assert line["config"]["design"] == want
     names = [v["name"] for v in line["exchange_variants"]]
-    assert names[0] == want and len(names) == 5
+    assert names[0] == want and len(names) == len(bench_variants())
     assert all(v["value"] > 0 and v["kernel_ms_per_step"] > 0 for v in line["exchange_variants"])
     assert line["roofline"]["kernel"].startswith("k_clients<float, float, 8, 0, 4>")
