@@ -173,3 +173,22 @@ def test_tuning_builds_report_a_refused_abi_version(tmp_path):
         cmd = ["g++", "-std=c++17", "-shared", "-fPIC", "-O1", src, "-o", str(so)] + ([define] if define else [])
         subprocess.run(cmd, check=True, capture_output=True)
         assert ctypes.CDLL(str(so)).sa_abi_version() == want, define
+
+
+def test_integration_table_cites_the_header_lines():
+    """INTEGRATION.md's export table gives each entry point's line in
+    include/sfl_sa.h: every ``name`` (line) pair must point at that
+    declaration, and every declared entry point must be in the table."""
+    hdr = open(os.path.join(ROOT, "include", "sfl_sa.h")).read().splitlines()
+    table = [ln for ln in open(os.path.join(ROOT, "INTEGRATION.md")).read().splitlines()
+             if ln.startswith("| `sa_")]
+    cited = {}
+    for row in table:
+        for name, line in re.findall(r"`(sa_\w+)` \((\d+)\)", row.split("|")[1]):
+            cited[name] = int(line)
+    for name, line in cited.items():
+        assert re.search(r"\b%s\(" % name, hdr[line - 1]), f"{name}: line {line} is {hdr[line - 1]!r}"
+    declared = {m for ln in hdr for m in re.findall(r"^\w[\w\s\*]*\b(sa_\w+)\(", ln)}
+    text = " ".join(r.split("|")[1] for r in table)
+    missing = [d for d in declared if d not in text and "_" + d.split("_", 2)[-1] not in text]
+    assert not missing, f"entry points missing from INTEGRATION.md's table: {missing}"
