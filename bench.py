@@ -14,8 +14,10 @@ N>1: one process per GPU, clients sharded in contiguous blocks (8/N per
 GPU, config 3 at N=8); each rank runs the fused masking over its clients
 (internal pairs + cross streams), pipelined in chunks against the exchange
 of the uint64 partial sums over xGMI.  `value` is measured on the sharded
-server (ncclReduceScatter in place, every rank decodes its
-shard of the masked sum); the same process group then times every other
+server (every rank receives and decodes its shard of the
+masked sum), its exchange done by ncclReduceScatter in place or by direct
+shard transfers + a local sum, whichever a short probe of both finds
+faster on this node (`exchange_probe`); the same process group then times every other
 design (`exchange_variants`: the shards also gathered to rank 0, the
 sharded server over direct shard transfers, ncclReduce of the partial sums
 to rank 0, element sharding with and without the gather), so one run
@@ -522,6 +524,23 @@ class GlooStandinComm:
         pass
 
 
+def probe_exchange(ctx, args):
+    """The sharded server has two implementations of its one exchange step
+    (the same shards, bytes and result): RCCL's reduce-scatter, or direct
+    shard transfers + a local sum.  Which is faster depends on RCCL's
+    schedule on this node's xGMI mesh, so without an explicit --exchange the
+    headline takes the faster of a short probe of both (--probe-steps each,
+    max over ranks, so every rank picks the same) and the line says so."""
+    args_gather = "+gather" if args.gather else ""
+    cands = [Variant(ex + args_gather) for ex in ("sharded", "direct")]
+    timed = [run_design(ctx, v, args.probe_steps, 3)["ms_per_step"] for v in cands]
+    best = 0 if timed[0] <= timed[1] else 1
+    return cands[best], {"steps": args.probe_steps, "warmup": 3, "chosen": cands[best].name,
+                         "ms_per_step": {v.name: t for v, t in zip(cands, timed)},
+                         "note": "two implementations of the sharded server's exchange (same shards, bytes and "
+                                 "result); the headline is measured with --steps on the faster one"}
+
+
 def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
     """Time `steps` steps (after `warmup`) of design `v` on this rank: the
     masking launches on the compute stream, the design's exchange on the
@@ -697,6 +716,10 @@ def main():
                          f"('all' = {','.join(VARIANTS)}; a comma list; 'none')")
     ap.add_argument("--variant-steps", type=int, default=None,
                     help="timed steps per extra design (default: min(200, --steps))")
+    ap.add_argument("--probe-steps", type=int, default=20,
+                    help="N>1 sharded server without --exchange: time this many steps of each exchange "
+                         "implementation (reduce-scatter, direct transfers) first and take the faster for the "
+                         "headline (0: always the reduce-scatter)")
     ap.add_argument("--digests", action="store_true",
                     help="also fold every client's masked values into an XOR digest (test checksum)")
     ap.add_argument("--dry-run", action="store_true",
@@ -770,6 +793,9 @@ def main():
     ctx = {"args": args, "world": world, "rank": rank, "dev": dev, "comm": comm, "rehearse": rehearse,
            "names": [f"client{c}" for c in range(C)]}
     head = headline_variant(args, multi)
+    probe = None
+    if multi and args.exchange is None and head.shard == "clients" and args.probe_steps > 0:
+        head, probe = probe_exchange(ctx, args)
     r = run_design(ctx, head, args.steps, args.warmup, keep=args.extra and world == 1)
     if r["zero_draw_flag"]:
         print("warning: PRG zero-draw flag raised", file=sys.stderr)
@@ -827,6 +853,8 @@ def main():
     }
     if multi:
         out["exchange"] = r["exchange"]
+        if probe is not None:
+            out["exchange_probe"] = probe
         variants = [r]
         for v in other_variants(args, head):
             variants.append(run_design(ctx, v, args.variant_steps, min(5, args.warmup)))

@@ -30,13 +30,15 @@ def test_bench_n_ranks_every_design(world):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                         "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
-                        "--cpu-baseline-seconds", "0", "--watchdog-seconds", "100"],
+                        "--probe-steps", "2", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "100"],
                        capture_output=True, text=True, timeout=115, env=env, cwd=ROOT)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = lines[0]
-    assert line["n_gpus"] == world and "rehearsal" in line and line["config"]["design"] == "sharded"
+    assert line["n_gpus"] == world and "rehearsal" in line and line["config"]["design"] in ("sharded", "direct")
+    probe = line["exchange_probe"]
+    assert probe["chosen"] == line["config"]["design"] and sorted(probe["ms_per_step"]) == ["direct", "sharded"]
     per = 8 // world
     assert line["config"]["clients_per_gpu"] == per
     assert line["roofline"]["kernel"].startswith(f"k_clients<float, float, {per}, {8 - per}, ")
