@@ -12,7 +12,7 @@ Device work: ``sa_sumsq_f32`` (deterministic float64 norm), then
 ``sa_dp_perturb_f32`` (this class's ``__call__``: the perturbed arrays are
 materialised, as the reference returns them).  ``sa_mask_dp`` runs the
 same clip + noise inside the masking kernel, bit-identical; the loopback
-client uses it (3 % faster than perturb-then-mask on MI355X).
+client uses it (2–3 % faster than perturb-then-mask on MI355X).
 
 The noise is Philox4x32-10 + Box-Muller keyed by a 64-bit key and the
 element index (reproducible, parallel), not numpy's unseeded global
