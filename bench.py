@@ -222,6 +222,31 @@ def pmc_traffic(kernel: str, elems_per_launch: int, pmc_elems: int = PMC_ELEMS) 
     return None
 
 
+VALU_PEAK_WAVE_INSTR_PER_S = 1024 * 2.4e9 / 4  # 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles
+                                               # at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
+
+
+def pmc_valu(kernel: str, elems_per_launch: int, pmc_elems: int = PMC_ELEMS) -> dict | None:
+    """VALU wave instructions per launch of `kernel` from the committed SQ
+    census (tools/pmc_sq.sh: SQ_INSTS_VALU on tools/kernel_bench.py launches
+    of 100M element positions), matched on the full instantiation and scaled
+    to this run's launch size -- SURVEY.md 8(d)'s "achieved int-op rate"."""
+    import csv
+
+    want = kernel_key(kernel)
+    for d in PMC_DIRS:
+        path = os.path.join(d, "pmc_sq_census.csv")
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            v = [float(r["Counter_Value"]) for r in csv.DictReader(f)
+                 if r["Counter_Name"] == "SQ_INSTS_VALU" and kernel_key(r["Kernel_Name"]) == want]
+        if v:
+            return {"valu_wave_instr": sum(v) / len(v) * elems_per_launch / pmc_elems,
+                    "source": os.path.relpath(path, ROOT) + " (SQ_INSTS_VALU)", "scaled_from_elems": pmc_elems}
+    return None
+
+
 def traffic_field(pmc: dict | None, alg_bytes_per_launch: float):
     """roofline.traffic from the PMC bytes: never a figure below the
     algorithmic bytes without saying so (HBM traffic under the bytes the
@@ -805,6 +830,16 @@ def main():
     achieved = bytes_alg / (kern_ms / 1e3) / 1e9
     pmc = pmc_traffic(f"void sa::{r['kernel']}", n_loc // launches)
     traffic, traffic_detail = traffic_field(pmc, bytes_alg / launches)
+    census = pmc_valu(f"void sa::{r['kernel']}", n_loc // launches)
+    int_ops = None
+    if census is not None:  # VALU issue rate of the timed launches against the chip's issue peak
+        rate = census["valu_wave_instr"] * launches / (kern_ms / 1e3)
+        int_ops = {"valu_wave_instr_per_launch": census["valu_wave_instr"], "valu_wave_instr_per_s": rate,
+                   "valu_lane_ops_per_s": 64 * rate, "peak_valu_wave_instr_per_s": VALU_PEAK_WAVE_INSTR_PER_S,
+                   "frac": rate / VALU_PEAK_WAVE_INSTR_PER_S, "source": census["source"],
+                   "note": "instructions per launch from the committed SQ census, time from this run's launches; "
+                           "the peak is one wave64 VALU instruction per 4 cycles per SIMD at 2.4 GHz (the board "
+                           "holds ~2.33 GHz under its power limit, and VOP3 forms issue at 4.2-4.7 cycles)"}
     # VALU: the step's draws against the same-box draw loop at the same draw
     # kinds: ideal time = pair draws / pair ceiling + one-sided / one-sided ceiling
     pair_peak = ceil["pair"]["draws_per_s"] if "pair" in ceil else PCG_PAIR_DRAWS_2WAVE
@@ -849,7 +884,8 @@ def main():
                                               "constants from profiles/r01/draw_issue_microbench.txt (another "
                                               "box): the same-box measurement failed"),
                               "ideal_ms_per_step": ideal_s * 1e3,
-                              "frac": ideal_s / (kern_ms / 1e3)}},
+                              "frac": ideal_s / (kern_ms / 1e3),
+                              "issue": int_ops}},
     }
     if multi:
         out["exchange"] = r["exchange"]

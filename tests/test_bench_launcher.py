@@ -182,3 +182,19 @@ def test_pmc_traffic_keys_on_the_full_instantiation():
     # a figure below the algorithmic bytes is withheld, with a note
     t, detail = bench.traffic_field({"bytes": 2.8e9, "read": 2.0e9, "write": 0.8e9}, 4.0e9)
     assert t is None and "withheld" in detail["note"]
+
+
+def test_pmc_valu_reads_the_census_of_the_timed_kernel():
+    """roofline.valu.issue: VALU wave instructions per launch from the
+    committed SQ census of exactly the timed instantiation, scaled to the
+    launch size; ~27 per pair draw for the 8-client launch."""
+    import bench
+
+    n = 10 ** 8
+    v = bench.pmc_valu("void sa::k_clients<float, float, 8, 0, 4>", n)
+    assert v is not None
+    per_pair_draw = v["valu_wave_instr"] / (28 * n / 64)
+    assert 24 < per_pair_draw < 30, per_pair_draw
+    half = bench.pmc_valu("void sa::k_clients<float, float, 8, 0, 4>", n // 2)
+    assert abs(half["valu_wave_instr"] * 2 - v["valu_wave_instr"]) < 1
+    assert bench.pmc_valu("void sa::k_clients<float, float, 3, 5, 4>", n) is None
