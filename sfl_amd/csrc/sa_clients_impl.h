@@ -648,7 +648,9 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
     }
   }
 
-  uint32_t zmin = 0xFFFFFFFFu;  // 0 iff some raw PCG64 draw of this lane was 0
+  // 0 iff some raw PCG64 draw of this lane (or, for the paired draws, of its
+  // wave) was 0; the paired draws test per tile (sa_draw2.h, ZeroAcc)
+  uint32_t zmin = 0xFFFFFFFFu;
   SA_TS(ts1);
 
   // per-lane XOR digests of the clients' masked values: VGPRs, or for the
@@ -732,6 +734,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
     // ---- mask expansion, stream-outer, two streams per asm block where the
     // schedule pairs them; group g+1's constants are scalar-loaded during
     // group g's first draw
+    ZeroAcc zh = zero_acc_init();
     if constexpr (P > 0) {
       using SO = SchedOf<L, X, K>;  // the schedule (a static constexpr: usable in the lambdas)
       Inc ni[2], nj[2];  // next group's plain-step / tile-jump addends
@@ -786,7 +789,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
           } else {
             State& sb = st[G.qb];
 #define SA_DRAW2_PAIR(fn)                                                                                 \
-  fn<G.F>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], ib, m[1], zmin, \
+  fn<G.F>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], ib, m[1], zh,   \
           ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb], bua, bva, bub, bvb)
             if constexpr (G.va >= 0 && G.va_add && G.vb_add)
               SA_DRAW2_PAIR(pcg_draw2_pair_aa);
@@ -799,15 +802,17 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
 #undef SA_DRAW2_PAIR
             else if constexpr (G.ua == G.ub)
               pcg_draw2_one_same<G.F>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia,
-                                      m[0], ib, m[1], zmin, ak[G.ua], bua);
+                                      m[0], ib, m[1], zh, ak[G.ua], bua);
             else
               pcg_draw2_one<G.F>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0],
-                                 ib, m[1], zmin, ak[G.ua], ak[G.ub], bua, bub);
+                                 ib, m[1], zh, ak[G.ua], ak[G.ub], bua, bub);
           }
           if (k == 0 && g + 1 < SO::value.n && !(SA_ABLATE & 128)) fetch(g + 1);
         }
       }, std::make_integer_sequence<int, SO::value.n>{});
     }
+
+    if (__builtin_expect(zero_acc_hit(zh), 0)) zmin = 0;
 
     // ---- finish: add the quantized value (or the prior pass), digest, sums
     kargs_t* ka = fenced_args();

@@ -21,7 +21,7 @@ A = 0x2360ED051FC65DA44385DF649FCCF645
 
 # %[name] operands that are 64-bit values (VGPR pairs or SGPR pairs)
 WIDE = {"p01a", "p01b", "ua", "ub", "va", "vb", "bua", "bub", "bva", "bvb",
-        "c0a", "c1a", "c23a", "c0b", "c1b", "c23b"}
+        "c0a", "c1a", "c23a", "c0b", "c1b", "c23b", "mma", "mmb"}
 
 
 def _functions(text):
@@ -144,6 +144,13 @@ class Lane:
             self.write(ops[0], (r(ops[2]) << (r(ops[1]) & 63)) & M64)
         elif opc in ("v_or_b32_e32", "v_or_b32"):
             self.write(ops[0], r(ops[1]) | r(ops[2]))
+        elif opc == "v_xor_b32_e32":
+            self.write(ops[0], r(ops[1]) ^ r(ops[2]))
+        elif opc in ("v_cmp_eq_u64_e32", "v_cmp_eq_u64_e64"):
+            # this lane's bit of the compare mask (one lane: bit 0)
+            self.write(ops[0], 1 if r(ops[1]) == r(ops[2]) else 0)
+        elif opc == "s_or_b64":
+            self.write(ops[0], r(ops[1]) | r(ops[2]))
         elif opc == "v_min3_u32":
             self.write(ops[0], min(r(ops[1]), r(ops[2]), r(ops[3])))
         elif opc == "v_lshl_add_u64":
@@ -196,7 +203,7 @@ def _check(fn_lines, kind, sa, sb, ma, mb, acc, rng):
     ia, ib = sa[1], sb[1]
     a_limbs = [(A >> (32 * i)) & M32 for i in range(4)]
     env = {"a0": a_limbs[0], "a1": a_limbs[1], "a2": a_limbs[2], "a3": a_limbs[3],
-           "ma": ma, "mb": mb, "zmin": M32}
+           "ma": ma, "mb": mb, "mma": ma << 32 | ma, "mmb": mb << 32 | mb, "zmin": M32, "zh": 0}
     for t, (s, inc) in (("a", sa), ("b", sb)):
         env[f"p01{t}"] = s & M64
         env[f"s2{t}"] = (s >> 64) & M32
@@ -223,7 +230,10 @@ def _check(fn_lines, kind, sa, sb, ma, mb, acc, rng):
     for tag in "ab":
         got = lane.env[f"p01{tag}"] | lane.env[f"s2{tag}"] << 64 | lane.env[f"s3{tag}"] << 96
         assert got == exp_state[tag], (kind, tag)
-    assert (lane.env["zmin"] == 0) == zero, kind
+    if any("%[zh]" in ln for ln in fn_lines):  # shift-rotation form: SALU-OR-ed 64-bit compares
+        assert (lane.env["zh"] != 0) == zero, kind
+    else:  # alignbit / rot64 forms: the per-lane running minimum
+        assert (lane.env["zmin"] == 0) == zero, kind
     return lane.env, t
 
 
@@ -268,18 +278,22 @@ def test_one_sided_draw_blocks_equal_numpy_pcg64(name):
                 assert env["ub"] == (acc["ub"] + t["b"]) & M64
 
 
-def test_both_rotation_forms_of_the_generator():
-    """The committed header carries the alignbit rotation (the generator's
-    default); the generator's --rot64 form (two 64-bit shifts + OR, measured
-    neutral on MI355X) computes the same draws."""
+@pytest.mark.parametrize("flag", ["--alignbit", "--rot64"])
+def test_other_rotation_forms_of_the_generator(flag):
+    """The committed header carries the shift-rotation form (the generator's
+    default: two 64-bit shifts joined by one v_lshl_add_u64, the raw == 0 test
+    as a 64-bit compare OR-ed on the SALU); the generator's --alignbit form
+    (round 2: two v_alignbit + a swap on bit 31) and --rot64 form (shifts +
+    OR) compute the same draws."""
     import subprocess
     import sys
 
     text = open(os.path.join(ROOT, "sfl_amd", "csrc", "sa_draw2.h")).read()
-    assert "v_alignbit_b32" in text and "v_lshrrev_b64" not in text
-    alt = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_draw2.py"), "--rot64"],
+    assert "v_lshl_add_u64 v[6:7], v[6:7], 1, v[4:5]" in text and "v_alignbit_b32" not in text
+    assert '#define SA_DRAW2_FORM "rots"' in text
+    alt = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_draw2.py"), flag],
                          capture_output=True, text=True, check=True).stdout
-    assert "v_lshrrev_b64" in alt and "v_alignbit_b32" not in alt
+    assert ("v_alignbit_b32" in alt) == (flag == "--alignbit") and "v_cmp_eq_u64" not in alt
     funcs = _functions(alt)
     rng = np.random.default_rng(64)
     states = _states(rng)

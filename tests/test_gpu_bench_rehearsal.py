@@ -12,6 +12,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -28,11 +29,17 @@ def test_bench_n_ranks_every_design(world):
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
+    t0 = time.time()
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                         "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
                         "--probe-steps", "2", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "100"],
                        capture_output=True, text=True, timeout=115, env=env, cwd=ROOT)
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    if r.returncode != 0:  # the lines that say why (ranks interleave their output), then the tail
+        why = [ln for ln in r.stderr.splitlines()
+               if any(k in ln for k in ("Error", "error:", "Traceback", "watchdog", "still running", "exitcode"))]
+        pytest.fail(f"bench.py --gpus {world} --rehearse-one-gpu: rc {r.returncode} after {time.time() - t0:.0f} s\n"
+                    + "\n".join(why[:40]) + "\n--- stderr tail ---\n" + r.stderr[-2500:]
+                    + "\n--- stdout tail ---\n" + r.stdout[-1000:])
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = lines[0]

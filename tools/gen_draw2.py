@@ -66,6 +66,18 @@ PAIR01 = "--no-pair01" not in sys.argv
 # the default stays the alignbit form.  Both are pinned to numpy on the CPU
 # by tests/test_draw_emulation.py.
 ROT64 = "--rot64" in sys.argv
+# Default form (ROTS): XSL-RR's rotation as two 64-bit shifts whose parts are
+# ADDED by one v_lshl_add_u64 -- y = x >> r, z = x << (63 - r), t = (z << 1)
+# + y: the two parts have disjoint bits, so + is |, and for r = 0 the shift
+# by one more bit makes z's part vanish (t = x) -- 5 instructions (shift
+# amount, its complement, two shifts, the join) instead of the alignbit
+# form's 6 (shift amount, two v_alignbit, v_cmp, two v_cndmask); and the
+# raw == 0 test as ONE 64-bit compare of x with the sign mask pair (x == m:m
+# <=> raw == 0) into VCC / an SGPR pair, OR-ed into a wave-wide hit mask on
+# the SALU (which issues beside the other wave's VALU), instead of a v_bitop3
+# "all equal" per draw + a v_min3 per two draws: 1.5 VALU per draw fewer in
+# all.  --alignbit emits the round-2 form.
+ROTS = not ROT64 and "--alignbit" not in sys.argv
 
 # one draw: (asm, sgpr_writes, sgpr_reads); {..} fields are renamed per stream
 DRAW = [
@@ -114,8 +126,24 @@ ROT64_STEPS = [  # replaces {cmp} .. {cnd_hi} of DRAW (the rotation), zero test 
 ]
 
 
+ROTS_STEPS = [  # replaces {cmp} .. {cnd_hi} and the zero test of DRAW; accumulate kept in place
+    ("v_lshrrev_b32_e32 v{v2}, 26, %[{s3}]", set(), set()),
+    ("v_xor_b32_e32 v{v3}, 63, v{v2}", set(), set()),
+    ("{zcmp}", {"z"}, set()),
+    ("v_lshrrev_b64 v[{v4}:{v5}], v{v2}, v[{v0}:{v1}]", set(), set()),
+    ("v_lshlrev_b64 v[{v6}:{v7}], v{v3}, v[{v0}:{v1}]", set(), set()),
+    ("{zor}", set(), {"z"}),
+    ("v_lshl_add_u64 v[{v6}:{v7}], v[{v6}:{v7}], 1, v[{v4}:{v5}]", set(), set()),
+    ("VSUBLO", {"k2"}, set()),
+]
+
+
 def draw_steps():
-    """DRAW with the rotation in the form ROT64 selects."""
+    """DRAW with the rotation (and zero test) in the form the flags select."""
+    if ROTS:
+        i0 = DRAW.index(("{cmp}", {"sw"}, set()))
+        i1 = DRAW.index(("{cnd_hi}", set(), {"sw"}))
+        return DRAW[:i0] + ROTS_STEPS + DRAW[i1 + 1:]
     if not ROT64:
         return DRAW
     i0 = DRAW.index(("{cmp}", {"sw"}, set()))
@@ -130,6 +158,12 @@ def stream(tag, base, vmode, acc_u, acc_v):
          "c0": f"c0{tag}", "c1": f"c1{tag}", "c23": f"c23{tag}", "m": f"m{tag}", "u": acc_u}
     for i in range(10):
         f[f"v{i}"] = str(base + i)
+    if tag == "a":
+        f["zcmp"] = f"v_cmp_eq_u64_e32 vcc, %[mma], v[{base}:{base + 1}]"
+        f["zor"] = "s_or_b64 %[zh], %[zh], vcc"
+    else:
+        f["zcmp"] = f"v_cmp_eq_u64_e64 %[swb], %[mmb], v[{base}:{base + 1}]"
+        f["zor"] = "s_or_b64 %[zh], %[zh], %[swb]"
     if tag == "a":
         f["cmp"] = f"v_cmp_gt_i32_e32 vcc, 0, %[s3a]"
         f["cnd_lo"] = f"v_cndmask_b32_e32 v{base + 6}, v{base + 4}, v{base + 5}, vcc"
@@ -185,8 +219,9 @@ def interleave(a, b):
             seq.append(b[i])
     # the two raw==0 minimums become one v_min3 at B's ZMIN slot
     zs = [i for i, s in enumerate(seq) if s[0] == "ZMIN"]
-    seq[zs[1]] = ("v_min3_u32 %[zmin], %[zmin], v3, v13", set(), set())
-    del seq[zs[0]]
+    if zs:
+        seq[zs[1]] = ("v_min3_u32 %[zmin], %[zmin], v3, v13", set(), set())
+        del seq[zs[0]]
     # hazard check: reader index - last writer index >= 3, else pad with s_nop
     out = []
     last_w = {}
@@ -235,17 +270,20 @@ def block(vma, vmb, same_acc, f):
     u64 = ["ua"] + ([] if same_acc else ["ub"]) + [x for x, m in (("va", vma), ("vb", vmb)) if m == "a"]
     split = [x for x, m in (("va", vma), ("vb", vmb)) if m == "s"]
     accs = ["ua"] + (["va"] if vma else []) + ([] if same_acc else ["ub"] + (["vb"] if vmb else []))
+    zout = '[zh] "+s"(zh)' if ROTS else '[zmin] "+v"(zh)'
     outs = ['[s0a] "+v"(s0a)', '[s1a] "+v"(s1a)', '[s2a] "+v"(s2a)', '[s3a] "+v"(s3a)',
-            '[s0b] "+v"(s0b)', '[s1b] "+v"(s1b)', '[s2b] "+v"(s2b)', '[s3b] "+v"(s3b)', '[zmin] "+v"(zmin)']
+            '[s0b] "+v"(s0b)', '[s1b] "+v"(s1b)', '[s2b] "+v"(s2b)', '[s3b] "+v"(s3b)', zout]
     if PAIR01:
         outs = ['[p01a] "+v"(p01a)', '[s2a] "+v"(s2a)', '[s3a] "+v"(s3a)',
-                '[p01b] "+v"(p01b)', '[s2b] "+v"(s2b)', '[s3b] "+v"(s3b)', '[zmin] "+v"(zmin)']
+                '[p01b] "+v"(p01b)', '[s2b] "+v"(s2b)', '[s3b] "+v"(s3b)', zout]
     outs += [f'[{x}] "=&v"({x})' if first[x] else f'[{x}] "+v"({x})' for x in accs if x in u64]
     outs += [f'[{x}{h}] "+v"({x}{h})' for x in split for h in ("lo", "hi")]
     outs += [f'[{k}] "=&s"({k})' for k in ("k1a", "k2a", "k3a", "k1b", "k2b", "k3b", "swb")]
     ins = ['[a0] "v"(a0)', '[a1] "v"(a1)', '[a2] "v"(a2)', '[a3] "v"(a3)',
            '[c0a] "s"(ia.w0)', '[c1a] "s"(ia.w1)', '[c23a] "s"(ia.hi)', '[ma] "s"(ma)',
            '[c0b] "s"(ib.w0)', '[c1b] "s"(ib.w1)', '[c23b] "s"(ib.hi)', '[mb] "s"(mb)']
+    if ROTS:
+        ins += ['[mma] "s"(mma)', '[mmb] "s"(mmb)']
     ins += [f'[b{x}] "s"(b{x})' for x in accs if x in u64 and first[x]]
     if PAIR01:
         ins += ['[s0a] "v"(s0a)', '[s1a] "v"(s1a)', '[s0b] "v"(s0b)', '[s1b] "v"(s1b)']
@@ -266,10 +304,13 @@ def emit(name, vma, vmb, same_acc):
     params = st_params + [
               "uint32_t a0", "uint32_t a1", "uint32_t a2", "uint32_t a3",
               "const Inc& ia", "uint32_t ma", "const Inc& ib", "uint32_t mb",
-              "uint32_t& zmin"] + [f"uint64_t& {x}" for x in accs] + [f"uint64_t b{x}" for x in accs]
+              "ZeroAcc& zh"] + [f"uint64_t& {x}" for x in accs] + [f"uint64_t b{x}" for x in accs]
     lines.append("template <int F>")
     lines.append(f"__device__ __forceinline__ void {name}(" + ", ".join(params) + ") {")
     lines.append("  uint64_t k1a, k2a, k3a, k1b, k2b, k3b, swb;")
+    if ROTS:
+        lines.append("  // the sign masks as SGPR pairs (m:m) for the 64-bit raw == 0 compare")
+        lines.append("  const uint64_t mma = (uint64_t)ma << 32 | ma, mmb = (uint64_t)mb << 32 | mb;")
     for x in split:
         lines.append(f"  uint32_t {x}lo = (uint32_t){x}, {x}hi = (uint32_t)({x} >> 32);")
     for x in accs:
@@ -286,7 +327,9 @@ def emit(name, vma, vmb, same_acc):
             lines.append(f'        "{asm}\\n\\t"')
         lines.append("        : " + ", ".join(outs))
         lines.append("        : " + ", ".join(ins))
-        lines.append("        : " + ", ".join(['"vcc"'] + [f'"v{i}"' for i in range(20)]) + ");")
+        # ROTS: the SALU OR of the zero test writes SCC
+        clob = ['"vcc"'] + (['"scc"'] if ROTS else []) + [f'"v{i}"' for i in range(20)]
+        lines.append("        : " + ", ".join(clob) + ");")
     lines.append("  } else {")
     lines.append("    __builtin_trap();  // no such first-touch variant (the kernel's schedule never asks)")
     lines.append("  }")
@@ -310,6 +353,26 @@ def main():
     print("struct Inc {")
     print("  uint64_t w0, w1, hi;")
     print("};")
+    print()
+    form = "rots" if ROTS else ("rot64" if ROT64 else "alignbit")
+    print(f'#define SA_DRAW2_FORM "{form}"')
+    print()
+    print("// The paired draws' running raw == 0 test (numpy re-draws a raw 0), kept per")
+    print("// tile by the caller: zero_acc_init() before the tile's draws, zero_acc_hit()")
+    print("// after them.")
+    if ROTS:
+        print("// Here: the 64-bit compares OR-ed on the SALU into a wave-wide SGPR mask")
+        print("// (bit l: a draw of lane l was 0); zero_acc_hit is wave-uniform.  (Kept per")
+        print("// tile: a kernel-long SGPR accumulator fails to compile -- illegal VGPR to")
+        print("// SGPR copy -- in the kernels with VGPR digests.)")
+        print("typedef uint64_t ZeroAcc;")
+        print("__device__ __forceinline__ ZeroAcc zero_acc_init() { return 0; }")
+        print("__device__ __forceinline__ bool zero_acc_hit(ZeroAcc z) { return z != 0; }")
+    else:
+        print("// Here: a per-lane running minimum, 0 iff a draw of this lane was 0.")
+        print("typedef uint32_t ZeroAcc;")
+        print("__device__ __forceinline__ ZeroAcc zero_acc_init() { return 0xFFFFFFFFu; }")
+        print("__device__ __forceinline__ bool zero_acc_hit(ZeroAcc z) { return z == 0; }")
     print()
     for ma in "sa":
         for mb in "sa":

@@ -170,6 +170,7 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
   uint32_t zmin = 0xFFFFFFFFu;
   cptr_t cp = (cptr_t)gconst;
   for (int it = 0; it < iters; it++) {
+    ZeroAcc zh = zero_acc_init();  // the paired draws' zero test, per tile as in the kernel
     Inc ninc[2];
     uint64_t nm[2];
     auto fetch = [&](int g) {
@@ -205,7 +206,7 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
         } else {
           MbState& sb = st[G.qb];
 #define DRAW2(fn)                                                                                         \
-  fn<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_, zmin,     \
+  fn<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_, zh,       \
         ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb], 0, 0, 0, 0)
           if (G.va >= 0 && G.va_add && G.vb_add)
             DRAW2(pcg_draw2_pair_aa);
@@ -218,14 +219,15 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
 #undef DRAW2
           else if (G.ua == G.ub)
             pcg_draw2_one_same<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib,
-                                  fmb_, zmin, ak[G.ua], 0);
+                                  fmb_, zh, ak[G.ua], 0);
           else
             pcg_draw2_one<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_,
-                             zmin, ak[G.ua], ak[G.ub], 0, 0);
+                             zh, ak[G.ua], ak[G.ub], 0, 0);
         }
         if (k == 0 && g + 1 < S.n) fetch(g + 1);
       }
     }
+    if (zero_acc_hit(zh)) zmin = 0;
   }
   uint64_t acc = zmin;
 #pragma unroll
@@ -262,6 +264,7 @@ __global__ void __launch_bounds__(256, W) k_dualE(uint64_t* out, int iters, uint
   uint32_t zmin = 0xFFFFFFFFu;
   cptr_t cp = (cptr_t)gconst;
   for (int it = 0; it < iters; it++) {
+    ZeroAcc zh = zero_acc_init();  // the paired draws' zero test, per tile as in the kernel
     Inc ninc[2];
     uint64_t nm[2];
     auto fetch = [&](int g) {
@@ -297,7 +300,7 @@ __global__ void __launch_bounds__(256, W) k_dualE(uint64_t* out, int iters, uint
         } else {
           MbState& sb = st[G.qb];
 #define DRAW2(fn)                                                                                         \
-  fn<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_, zmin,     \
+  fn<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_, zh,       \
         ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb], 0, 0, 0, 0)
           if (G.va >= 0 && G.va_add && G.vb_add)
             DRAW2(pcg_draw2_pair_aa);
@@ -310,14 +313,15 @@ __global__ void __launch_bounds__(256, W) k_dualE(uint64_t* out, int iters, uint
 #undef DRAW2
           else if (G.ua == G.ub)
             pcg_draw2_one_same<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib,
-                                  fmb_, zmin, ak[G.ua], 0);
+                                  fmb_, zh, ak[G.ua], 0);
           else
             pcg_draw2_one<0>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, ib, fmb_,
-                             zmin, ak[G.ua], ak[G.ub], 0, 0);
+                             zh, ak[G.ua], ak[G.ub], 0, 0);
         }
         if (k == 0 && g + 1 < S.n) fetch(g + 1);
       }
     }
+    if (zero_acc_hit(zh)) zmin = 0;
   }
   uint64_t acc = zmin;
 #pragma unroll
