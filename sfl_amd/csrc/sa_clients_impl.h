@@ -290,10 +290,12 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
 //   carry-ins are the mads' own carry-outs -- 9 mads + 1 mul_lo + 4 adds +
 //   1 mov (the paired draws of sa_draw2.h, which do nearly all the work,
 //   keep limbs 0-1 in one VGPR pair written in place and need no mov).
-//   Then t = rotr(hi^lo^m,
-//   hi>>58) in 32-bit halves (v_bitop3 + v_alignbit + swap), the raw==0 test
-//   (hi == lo <=> xl == xh == m) folded into a running minimum, and the
-//   accumulation (below).
+//   Then x = hi^lo^m (two v_bitop3) and t = rotr(x, hi>>58) as two 64-bit
+//   shifts whose disjoint parts one v_lshl_add_u64 adds: y = x >> r,
+//   z = x << (63 - r), t = (z << 1) + y (r = 0: z << 1 vanishes, t = x); the
+//   raw==0 test (hi == lo <=> x == m:m) as one 64-bit compare whose lane
+//   mask the SALU ORs into `zs` (a per-tile SGPR pair), and the accumulation
+//   (below).  The same form as sa_draw2.h's paired draws (tools/gen_draw2.py).
 //
 // Carries live in three SGPR pairs, reused as they die (k1: a discarded
 // carry-out; k2: kO, c2, then the acc_v borrow; k3: discarded carry-outs, c1).
@@ -320,39 +322,40 @@ __device__ __forceinline__ uint32_t vreg(uint32_t x) {
   "s_nop 0\n\t"                                                                          \
   "v_addc_co_u32_e64 %[s3], %[k3], %[s3], 0, %[k2]\n\t"    /* r3 += c2 */               \
   "v_bitop3_b32 v1, %[s1], %[s3], %[m] bitop3:0x96\n\t"    /* xh */                     \
-  "v_cmp_gt_i32_e32 vcc, 0, %[s3]\n\t"                      /* rot >= 32: swap */        \
-  "v_lshrrev_b32_e32 v2, 26, %[s3]\n\t"                     /* rot (& 31 in alignbit) */ \
-  "v_bitop3_b32 v3, v0, v1, %[m] bitop3:0x7e\n\t"          /* 0 iff raw == 0 */         \
-  "v_alignbit_b32 v4, v1, v0, v2\n\t"                                                    \
-  "v_alignbit_b32 v5, v0, v1, v2\n\t"                                                    \
-  "v_min_u32_e32 %[zmin], %[zmin], v3\n\t"                                               \
-  "v_cndmask_b32_e32 v6, v4, v5, vcc\n\t"                   /* t lo */
+  "v_lshrrev_b32_e32 v2, 26, %[s3]\n\t"                     /* r */                      \
+  "v_xor_b32_e32 v3, 63, v2\n\t"                            /* 63 - r */                 \
+  "v_cmp_eq_u64_e32 vcc, %[mm], v[0:1]\n\t"                 /* raw == 0 */               \
+  "v_lshrrev_b64 v[4:5], v2, v[0:1]\n\t"                    /* y */                      \
+  "v_lshlrev_b64 v[6:7], v3, v[0:1]\n\t"                    /* z */                      \
+  "s_or_b64 %[zs], %[zs], vcc\n\t"                                                       \
+  "v_lshl_add_u64 v[6:7], v[6:7], 1, v[4:5]\n\t"           /* t */
 
 #define SA_PCG_DRAW_OUTS                                                                 \
-  [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [zmin] "+v"(zmin),          \
+  [s0] "+v"(s0), [s1] "+v"(s1), [s2] "+v"(s2), [s3] "+v"(s3), [zs] "+s"(zs),              \
       [u] "+v"(u), [k1] "=&s"(k1), [k2] "=&s"(k2), [k3] "=&s"(k3)
 // Operand classes: the multiplier limbs are wave-uniform VGPRs (set once per
 // launch), the stream constants SGPRs (scalar-loaded per stream and tile), so
 // every VOP3 reads at most one SGPR (the gfx9 constant-bus limit).
 #define SA_PCG_DRAW_INS                                                                  \
   [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c0] "s"(inc.w0),                    \
-      [c1] "s"(inc.w1), [c23] "s"(inc.hi), [m] "s"(m)
+      [c1] "s"(inc.w1), [c23] "s"(inc.hi), [m] "s"(m), [mm] "s"((uint64_t)m << 32 | m)
 #define SA_PCG_DRAW_CLOBBERS \
-  "vcc", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9"
+  "vcc", "scc", "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9"
 
 // acc_u += t with one v_lshl_add_u64 on the 64-bit accumulator (the issue cost
 // of one v_add_co, tools/microbench/op_rate.hip); the internal pair's second
 // client subtracts on 32-bit halves (pcg_draw_pair) or, when the kernel keeps
-// that client negated, also adds (pcg_draw_pair_a).
+// that client negated, also adds (pcg_draw_pair_a).  zs: the per-tile lane
+// mask of raw == 0 draws (an SGPR pair; 0 at the tile's start).
 __device__ __forceinline__ void pcg_draw_pair(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
                                               uint32_t a1, uint32_t a2, uint32_t a3, const Inc& inc,
-                                              uint32_t m, uint32_t& zmin, uint64_t& u, uint64_t& v) {
+                                              uint32_t m, uint64_t& zs, uint64_t& u, uint64_t& v) {
   uint64_t k1, k2, k3;
   uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
   asm volatile(SA_PCG_DRAW_ASM
                "v_sub_co_u32_e64 %[vlo], %[k2], %[vlo], v6\n\t"
-               "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"  // t hi
                "v_lshl_add_u64 %[u], v[6:7], 0, %[u]\n\t"
+               "s_nop 0\n\t"
                "v_subb_co_u32_e64 %[vhi], %[k2], %[vhi], v7, %[k2]"
                : SA_PCG_DRAW_OUTS, [vlo] "+v"(vlo), [vhi] "+v"(vhi)
                : SA_PCG_DRAW_INS
@@ -361,10 +364,9 @@ __device__ __forceinline__ void pcg_draw_pair(uint32_t& s0, uint32_t& s1, uint32
 }
 __device__ __forceinline__ void pcg_draw_pair_a(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
                                                 uint32_t a1, uint32_t a2, uint32_t a3, const Inc& inc,
-                                                uint32_t m, uint32_t& zmin, uint64_t& u, uint64_t& v) {
+                                                uint32_t m, uint64_t& zs, uint64_t& u, uint64_t& v) {
   uint64_t k1, k2, k3;
   asm volatile(SA_PCG_DRAW_ASM
-               "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"  // t hi
                "v_lshl_add_u64 %[u], v[6:7], 0, %[u]\n\t"
                "v_lshl_add_u64 %[v], v[6:7], 0, %[v]"
                : SA_PCG_DRAW_OUTS, [v] "+v"(v)
@@ -373,10 +375,9 @@ __device__ __forceinline__ void pcg_draw_pair_a(uint32_t& s0, uint32_t& s1, uint
 }
 __device__ __forceinline__ void pcg_draw_one(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
                                              uint32_t a1, uint32_t a2, uint32_t a3, const Inc& inc,
-                                             uint32_t m, uint32_t& zmin, uint64_t& u) {
+                                             uint32_t m, uint64_t& zs, uint64_t& u) {
   uint64_t k1, k2, k3;
   asm volatile(SA_PCG_DRAW_ASM
-               "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"  // t hi
                "v_lshl_add_u64 %[u], v[6:7], 0, %[u]"
                : SA_PCG_DRAW_OUTS
                : SA_PCG_DRAW_INS
@@ -734,7 +735,8 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
     // ---- mask expansion, stream-outer, two streams per asm block where the
     // schedule pairs them; group g+1's constants are scalar-loaded during
     // group g's first draw
-    ZeroAcc zh = zero_acc_init();
+    ZeroAcc zh = zero_acc_init();  // the paired draws' raw == 0 test (sa_draw2.h)
+    uint64_t zs = 0;               // the single draws' (SA_PCG_DRAW_ASM)
     if constexpr (P > 0) {
       using SO = SchedOf<L, X, K>;  // the schedule (a static constexpr: usable in the lambdas)
       Inc ni[2], nj[2];  // next group's plain-step / tile-jump addends
@@ -780,11 +782,11 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
           if constexpr (G.qb < 0) {  // singles never first-touch: their clients are preset
             uint32_t s0 = (uint32_t)sa.p01, s1 = (uint32_t)(sa.p01 >> 32);
             if constexpr (G.va >= 0 && G.va_add)
-              pcg_draw_pair_a(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua], ak[G.va]);
+              pcg_draw_pair_a(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zs, ak[G.ua], ak[G.va]);
             else if constexpr (G.va >= 0)
-              pcg_draw_pair(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua], ak[G.va]);
+              pcg_draw_pair(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zs, ak[G.ua], ak[G.va]);
             else
-              pcg_draw_one(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zmin, ak[G.ua]);
+              pcg_draw_one(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zs, ak[G.ua]);
             sa.p01 = ((uint64_t)s1 << 32) | s0;
           } else {
             State& sb = st[G.qb];
@@ -812,7 +814,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
       }, std::make_integer_sequence<int, SO::value.n>{});
     }
 
-    if (__builtin_expect(zero_acc_hit(zh), 0)) zmin = 0;
+    if (__builtin_expect(zero_acc_hit(zh) || zs != 0, 0)) zmin = 0;
 
     // ---- finish: add the quantized value (or the prior pass), digest, sums
     kargs_t* ka = fenced_args();

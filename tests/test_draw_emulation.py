@@ -21,7 +21,8 @@ A = 0x2360ED051FC65DA44385DF649FCCF645
 
 # %[name] operands that are 64-bit values (VGPR pairs or SGPR pairs)
 WIDE = {"p01a", "p01b", "ua", "ub", "va", "vb", "bua", "bub", "bva", "bvb",
-        "c0a", "c1a", "c23a", "c0b", "c1b", "c23b", "mma", "mmb"}
+        "c0a", "c1a", "c23a", "c0b", "c1b", "c23b", "mma", "mmb",
+        "u", "v", "mm", "c0", "c1", "c23"}  # the last six: the single draw (sa_clients_impl.h)
 
 
 def _functions(text):
@@ -144,6 +145,8 @@ class Lane:
             self.write(ops[0], (r(ops[2]) << (r(ops[1]) & 63)) & M64)
         elif opc in ("v_or_b32_e32", "v_or_b32"):
             self.write(ops[0], r(ops[1]) | r(ops[2]))
+        elif opc == "v_mov_b32_e32":
+            self.write(ops[0], r(ops[1]))
         elif opc == "v_xor_b32_e32":
             self.write(ops[0], r(ops[1]) ^ r(ops[2]))
         elif opc in ("v_cmp_eq_u64_e32", "v_cmp_eq_u64_e64"):
@@ -278,7 +281,7 @@ def test_one_sided_draw_blocks_equal_numpy_pcg64(name):
                 assert env["ub"] == (acc["ub"] + t["b"]) & M64
 
 
-@pytest.mark.parametrize("flag", ["--alignbit", "--rot64"])
+@pytest.mark.parametrize("flag", ["--alignbit", "--rot64", "--zmin"])
 def test_other_rotation_forms_of_the_generator(flag):
     """The committed header carries the shift-rotation form (the generator's
     default: two 64-bit shifts joined by one v_lshl_add_u64, the raw == 0 test
@@ -303,3 +306,49 @@ def test_other_rotation_forms_of_the_generator(flag):
             acc = {k: int(rng.integers(0, 1 << 63)) for k in ("ua", "ub", "va", "vb")}
             env, t = _check(lines, variant, sa, states[i - 1], M32 * (i & 1), 0, acc, rng)
             assert env["ua"] == (acc["ua"] + t["a"]) & M64
+
+
+def _single_draw_functions():
+    """name -> asm lines of the single-draw functions of sa_clients_impl.h
+    (the SA_PCG_DRAW_ASM macro + each function's own accumulate tail)."""
+    text = open(os.path.join(ROOT, "sfl_amd", "csrc", "sa_clients_impl.h")).read()
+    mac = text[text.index("#define SA_PCG_DRAW_ASM"):text.index("#define SA_PCG_DRAW_OUTS")]
+    head = re.findall(r'"(.*?)\\n\\t"', mac)
+    out = {}
+    for name in ("pcg_draw_pair", "pcg_draw_pair_a", "pcg_draw_one"):
+        m = re.search(r"void " + name + r"\(.*?asm volatile\(SA_PCG_DRAW_ASM(.*?)\n\s*:", text, re.S)
+        tail = [t.replace("\\n\\t", "") for t in re.findall(r'"(.*?)"', m.group(1))]
+        out[name] = head + tail
+    return out
+
+
+@pytest.mark.parametrize("name", ["pcg_draw_pair", "pcg_draw_pair_a", "pcg_draw_one"])
+def test_single_draw_equals_numpy_pcg64(name):
+    """The single draws (odd leftover streams) in the same shift-rotation form:
+    next state, accumulators (u adds; the partner subtracts, or adds when the
+    kernel keeps it negated) and the SGPR raw == 0 mask, vs numpy's PCG64."""
+    lines = _single_draw_functions()[name]
+    assert any("v_lshl_add_u64 v[6:7], v[6:7], 1, v[4:5]" in ln for ln in lines)
+    rng = np.random.default_rng(len(name) * 7)
+    a_limbs = [(A >> (32 * i)) & M32 for i in range(4)]
+    for s, inc in _states(rng):
+        for m in (0, M32):
+            u, v = int(rng.integers(0, 1 << 63)), int(rng.integers(0, 1 << 63))
+            env = {"a0": a_limbs[0], "a1": a_limbs[1], "a2": a_limbs[2], "a3": a_limbs[3], "m": m,
+                   "mm": m << 32 | m, "zs": 0, "u": u, "v": v, "vlo": v & M32, "vhi": v >> 32,
+                   "s0": s & M32, "s1": (s >> 32) & M32, "s2": (s >> 64) & M32, "s3": s >> 96,
+                   "c0": inc & M32, "c1": (inc >> 32) & M32, "c23": inc >> 64}
+            lane = Lane(env, rng)
+            for ln in lines:
+                lane.run(ln)
+            nxt = (s * A + inc) & M128
+            raw = _raw(nxt)
+            t = raw ^ (M64 if m else 0)
+            e = lane.env
+            assert e["s0"] | e["s1"] << 32 | e["s2"] << 64 | e["s3"] << 96 == nxt
+            assert (e["zs"] != 0) == (raw == 0)
+            assert e["u"] == (u + t) & M64
+            if name == "pcg_draw_pair":
+                assert e["vlo"] | e["vhi"] << 32 == (v - t) & M64
+            elif name == "pcg_draw_pair_a":
+                assert e["v"] == (v + t) & M64

@@ -78,6 +78,12 @@ ROT64 = "--rot64" in sys.argv
 # "all equal" per draw + a v_min3 per two draws: 1.5 VALU per draw fewer in
 # all.  --alignbit emits the round-2 form.
 ROTS = not ROT64 and "--alignbit" not in sys.argv
+# --zmin (with ROTS): the shift rotation, but the round-2 raw == 0 test (a
+# v_bitop3 "all equal" per draw + one v_min3 per two draws into a per-lane
+# running minimum) instead of the SALU-OR-ed 64-bit compares -- one VALU more
+# per two draws, no SALU: for A/B (tools/microbench/draw_ops: a compare +
+# s_or_b64 pair issues at 7.5 cycles, the compare alone at 4.5).
+ZMIN_FORM = ROTS and "--zmin" in sys.argv
 
 # one draw: (asm, sgpr_writes, sgpr_reads); {..} fields are renamed per stream
 DRAW = [
@@ -138,12 +144,24 @@ ROTS_STEPS = [  # replaces {cmp} .. {cnd_hi} and the zero test of DRAW; accumula
 ]
 
 
+ROTS_ZMIN_STEPS = [  # ROTS_STEPS with the per-lane minimum zero test
+    ("v_lshrrev_b32_e32 v{v2}, 26, %[{s3}]", set(), set()),
+    ("v_bitop3_b32 v{v8}, v{v0}, v{v1}, %[{m}] bitop3:0x7e", set(), set()),
+    ("v_xor_b32_e32 v{v3}, 63, v{v2}", set(), set()),
+    ("v_lshrrev_b64 v[{v4}:{v5}], v{v2}, v[{v0}:{v1}]", set(), set()),
+    ("ZMIN", set(), set()),
+    ("v_lshlrev_b64 v[{v6}:{v7}], v{v3}, v[{v0}:{v1}]", set(), set()),
+    ("v_lshl_add_u64 v[{v6}:{v7}], v[{v6}:{v7}], 1, v[{v4}:{v5}]", set(), set()),
+    ("VSUBLO", {"k2"}, set()),
+]
+
+
 def draw_steps():
     """DRAW with the rotation (and zero test) in the form the flags select."""
     if ROTS:
         i0 = DRAW.index(("{cmp}", {"sw"}, set()))
         i1 = DRAW.index(("{cnd_hi}", set(), {"sw"}))
-        return DRAW[:i0] + ROTS_STEPS + DRAW[i1 + 1:]
+        return DRAW[:i0] + (ROTS_ZMIN_STEPS if ZMIN_FORM else ROTS_STEPS) + DRAW[i1 + 1:]
     if not ROT64:
         return DRAW
     i0 = DRAW.index(("{cmp}", {"sw"}, set()))
@@ -220,7 +238,8 @@ def interleave(a, b):
     # the two raw==0 minimums become one v_min3 at B's ZMIN slot
     zs = [i for i, s in enumerate(seq) if s[0] == "ZMIN"]
     if zs:
-        seq[zs[1]] = ("v_min3_u32 %[zmin], %[zmin], v3, v13", set(), set())
+        z = (8, 18) if ZMIN_FORM else (3, 13)
+        seq[zs[1]] = (f"v_min3_u32 %[zmin], %[zmin], v{z[0]}, v{z[1]}", set(), set())
         del seq[zs[0]]
     # hazard check: reader index - last writer index >= 3, else pad with s_nop
     out = []
@@ -270,7 +289,7 @@ def block(vma, vmb, same_acc, f):
     u64 = ["ua"] + ([] if same_acc else ["ub"]) + [x for x, m in (("va", vma), ("vb", vmb)) if m == "a"]
     split = [x for x, m in (("va", vma), ("vb", vmb)) if m == "s"]
     accs = ["ua"] + (["va"] if vma else []) + ([] if same_acc else ["ub"] + (["vb"] if vmb else []))
-    zout = '[zh] "+s"(zh)' if ROTS else '[zmin] "+v"(zh)'
+    zout = '[zh] "+s"(zh)' if ROTS and not ZMIN_FORM else '[zmin] "+v"(zh)'
     outs = ['[s0a] "+v"(s0a)', '[s1a] "+v"(s1a)', '[s2a] "+v"(s2a)', '[s3a] "+v"(s3a)',
             '[s0b] "+v"(s0b)', '[s1b] "+v"(s1b)', '[s2b] "+v"(s2b)', '[s3b] "+v"(s3b)', zout]
     if PAIR01:
@@ -282,7 +301,7 @@ def block(vma, vmb, same_acc, f):
     ins = ['[a0] "v"(a0)', '[a1] "v"(a1)', '[a2] "v"(a2)', '[a3] "v"(a3)',
            '[c0a] "s"(ia.w0)', '[c1a] "s"(ia.w1)', '[c23a] "s"(ia.hi)', '[ma] "s"(ma)',
            '[c0b] "s"(ib.w0)', '[c1b] "s"(ib.w1)', '[c23b] "s"(ib.hi)', '[mb] "s"(mb)']
-    if ROTS:
+    if ROTS and not ZMIN_FORM:
         ins += ['[mma] "s"(mma)', '[mmb] "s"(mmb)']
     ins += [f'[b{x}] "s"(b{x})' for x in accs if x in u64 and first[x]]
     if PAIR01:
@@ -308,7 +327,7 @@ def emit(name, vma, vmb, same_acc):
     lines.append("template <int F>")
     lines.append(f"__device__ __forceinline__ void {name}(" + ", ".join(params) + ") {")
     lines.append("  uint64_t k1a, k2a, k3a, k1b, k2b, k3b, swb;")
-    if ROTS:
+    if ROTS and not ZMIN_FORM:
         lines.append("  // the sign masks as SGPR pairs (m:m) for the 64-bit raw == 0 compare")
         lines.append("  const uint64_t mma = (uint64_t)ma << 32 | ma, mmb = (uint64_t)mb << 32 | mb;")
     for x in split:
@@ -328,7 +347,7 @@ def emit(name, vma, vmb, same_acc):
         lines.append("        : " + ", ".join(outs))
         lines.append("        : " + ", ".join(ins))
         # ROTS: the SALU OR of the zero test writes SCC
-        clob = ['"vcc"'] + (['"scc"'] if ROTS else []) + [f'"v{i}"' for i in range(20)]
+        clob = ['"vcc"'] + (['"scc"'] if ROTS and not ZMIN_FORM else []) + [f'"v{i}"' for i in range(20)]
         lines.append("        : " + ", ".join(clob) + ");")
     lines.append("  } else {")
     lines.append("    __builtin_trap();  // no such first-touch variant (the kernel's schedule never asks)")
@@ -354,13 +373,13 @@ def main():
     print("  uint64_t w0, w1, hi;")
     print("};")
     print()
-    form = "rots" if ROTS else ("rot64" if ROT64 else "alignbit")
+    form = ("rots_zmin" if ZMIN_FORM else "rots") if ROTS else ("rot64" if ROT64 else "alignbit")
     print(f'#define SA_DRAW2_FORM "{form}"')
     print()
     print("// The paired draws' running raw == 0 test (numpy re-draws a raw 0), kept per")
     print("// tile by the caller: zero_acc_init() before the tile's draws, zero_acc_hit()")
     print("// after them.")
-    if ROTS:
+    if ROTS and not ZMIN_FORM:
         print("// Here: the 64-bit compares OR-ed on the SALU into a wave-wide SGPR mask")
         print("// (bit l: a draw of lane l was 0); zero_acc_hit is wave-uniform.  (Kept per")
         print("// tile: a kernel-long SGPR accumulator fails to compile -- illegal VGPR to")

@@ -44,16 +44,16 @@ struct MbState {
 constexpr uint32_t A0 = 0x9FCCF645u, A1 = 0x4385DF64u, A2 = 0x1FC65DA4u, A3 = 0x2360ED05u;
 #define SMEM_INS                                                                                         \
   [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c0] "s"(inc.w0), [c1] "s"(inc.w1),             \
-      [c23] "s"(inc.hi), [m] "s"(m)
+      [c23] "s"(inc.hi), [m] "s"(m), [mm] "s"((uint64_t)m << 32 | m)
 __device__ __forceinline__ void draw_pair_s(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
                                             uint32_t a1, uint32_t a2, uint32_t a3, const Inc& inc,
-                                            uint32_t m, uint32_t& zmin, uint64_t& u, uint64_t& v) {
+                                            uint32_t m, uint64_t& zs, uint64_t& u, uint64_t& v) {
   uint64_t k1, k2, k3;
   uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
   asm volatile(SA_PCG_DRAW_ASM
                "v_sub_co_u32_e64 %[vlo], %[k2], %[vlo], v6\n\t"
-               "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"
                "v_lshl_add_u64 %[u], v[6:7], 0, %[u]\n\t"
+               "s_nop 0\n\t"
                "v_subb_co_u32_e64 %[vhi], %[k2], %[vhi], v7, %[k2]"
                : SA_PCG_DRAW_OUTS, [vlo] "+v"(vlo), [vhi] "+v"(vhi)
                : SMEM_INS
@@ -62,10 +62,9 @@ __device__ __forceinline__ void draw_pair_s(uint32_t& s0, uint32_t& s1, uint32_t
 }
 __device__ __forceinline__ void draw_one_s(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3, uint32_t a0,
                                            uint32_t a1, uint32_t a2, uint32_t a3, const Inc& inc,
-                                           uint32_t m, uint32_t& zmin, uint64_t& u) {
+                                           uint32_t m, uint64_t& zs, uint64_t& u) {
   uint64_t k1, k2, k3;
   asm volatile(SA_PCG_DRAW_ASM
-               "v_cndmask_b32_e32 v7, v5, v4, vcc\n\t"
                "v_lshl_add_u64 %[u], v[6:7], 0, %[u]"
                : SA_PCG_DRAW_OUTS
                : SMEM_INS
@@ -100,6 +99,7 @@ __global__ void __launch_bounds__(256) k_smem(uint64_t* out, int iters, uint32_t
 #pragma unroll
     for (int c = 0; c < L; c++) acc2[k][c] = c + k;
   uint32_t zmin = 0xFFFFFFFFu;
+  uint64_t zs = 0;  // single draws: lane mask of raw == 0 draws
   cptr_t cp = (cptr_t)gconst;
   for (int it = 0; it < iters; it++) {
     cptr_t f = cp;
@@ -121,11 +121,11 @@ __global__ void __launch_bounds__(256) k_smem(uint64_t* out, int iters, uint32_t
         if constexpr (PAIRS) {
           constexpr int PI = Pairs<L>::count;
           const int cu = Pairs<L>::u(q % PI), cv = Pairs<L>::v(q % PI);
-          draw_pair_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, cinc, sm, zmin, acc2[k][cu],
+          draw_pair_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, cinc, sm, zs, acc2[k][cu],
                       acc2[k][cv]);
         } else {
           const int cu = q % L;
-          draw_one_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, cinc, sm, zmin, acc2[k][cu]);
+          draw_one_s(st[q][0], st[q][1], st[q][2], st[q][3], va0, va1, va2, va3, cinc, sm, zs, acc2[k][cu]);
         }
         if (PREF && k == 0 && q + 1 < P) {
           cptr_t g = cp + 8 * (q + 1);
@@ -136,7 +136,7 @@ __global__ void __launch_bounds__(256) k_smem(uint64_t* out, int iters, uint32_t
       }
     }
   }
-  uint64_t acc = zmin;
+  uint64_t acc = zmin ^ zs;
 #pragma unroll
   for (int k = 0; k < E; k++)
 #pragma unroll
@@ -168,6 +168,7 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
 #pragma unroll
     for (int c = 0; c < L; c++) acc2[k][c] = c + k;
   uint32_t zmin = 0xFFFFFFFFu;
+  uint64_t zs = 0;  // single draws: lane mask of raw == 0 draws
   cptr_t cp = (cptr_t)gconst;
   for (int it = 0; it < iters; it++) {
     ZeroAcc zh = zero_acc_init();  // the paired draws' zero test, per tile as in the kernel
@@ -197,11 +198,11 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
         if (G.qb < 0) {
           uint32_t s0 = (uint32_t)sa.p01, s1 = (uint32_t)(sa.p01 >> 32);
           if (G.va >= 0 && G.va_add)
-            pcg_draw_pair_a(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua], ak[G.va]);
+            pcg_draw_pair_a(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zs, ak[G.ua], ak[G.va]);
           else if (G.va >= 0)
-            pcg_draw_pair(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua], ak[G.va]);
+            pcg_draw_pair(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zs, ak[G.ua], ak[G.va]);
           else
-            pcg_draw_one(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua]);
+            pcg_draw_one(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zs, ak[G.ua]);
           sa.p01 = ((uint64_t)s1 << 32) | s0;
         } else {
           MbState& sb = st[G.qb];
@@ -229,7 +230,7 @@ __global__ void __launch_bounds__(256) k_dual(uint64_t* out, int iters, uint32_t
     }
     if (zero_acc_hit(zh)) zmin = 0;
   }
-  uint64_t acc = zmin;
+  uint64_t acc = zmin ^ zs;
 #pragma unroll
   for (int k = 0; k < 2; k++)
 #pragma unroll
@@ -262,6 +263,7 @@ __global__ void __launch_bounds__(256, W) k_dualE(uint64_t* out, int iters, uint
 #pragma unroll
     for (int c = 0; c < L; c++) acc2[k][c] = c + k;
   uint32_t zmin = 0xFFFFFFFFu;
+  uint64_t zs = 0;  // single draws: lane mask of raw == 0 draws
   cptr_t cp = (cptr_t)gconst;
   for (int it = 0; it < iters; it++) {
     ZeroAcc zh = zero_acc_init();  // the paired draws' zero test, per tile as in the kernel
@@ -291,11 +293,11 @@ __global__ void __launch_bounds__(256, W) k_dualE(uint64_t* out, int iters, uint
         if (G.qb < 0) {
           uint32_t s0 = (uint32_t)sa.p01, s1 = (uint32_t)(sa.p01 >> 32);
           if (G.va >= 0 && G.va_add)
-            pcg_draw_pair_a(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua], ak[G.va]);
+            pcg_draw_pair_a(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zs, ak[G.ua], ak[G.va]);
           else if (G.va >= 0)
-            pcg_draw_pair(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua], ak[G.va]);
+            pcg_draw_pair(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zs, ak[G.ua], ak[G.va]);
           else
-            pcg_draw_one(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zmin, ak[G.ua]);
+            pcg_draw_one(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, fma_, zs, ak[G.ua]);
           sa.p01 = ((uint64_t)s1 << 32) | s0;
         } else {
           MbState& sb = st[G.qb];
@@ -323,7 +325,7 @@ __global__ void __launch_bounds__(256, W) k_dualE(uint64_t* out, int iters, uint
     }
     if (zero_acc_hit(zh)) zmin = 0;
   }
-  uint64_t acc = zmin;
+  uint64_t acc = zmin ^ zs;
 #pragma unroll
   for (int k = 0; k < E; k++)
 #pragma unroll
@@ -429,6 +431,7 @@ __global__ void __launch_bounds__(256) k_draws(uint64_t* out, int iters, uint32_
 #pragma unroll
   for (int c = 0; c < L; c++) acc1[c] = c;
   uint32_t zmin = 0xFFFFFFFFu;
+  uint64_t zs = 0;  // single draws: lane mask of raw == 0 draws
   lds_ptr slp = (lds_ptr)(sl);
   for (int it = 0; it < iters; it++) {
 #pragma unroll
@@ -448,15 +451,15 @@ __global__ void __launch_bounds__(256) k_draws(uint64_t* out, int iters, uint32_
       if constexpr (PAIRS) {
         constexpr int PI = Pairs<L>::count;
         const int cu = Pairs<L>::u(q % PI), cv = Pairs<L>::v(q % PI);
-        pcg_draw_pair(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, cinc, sm, zmin, acc1[cu],
+        pcg_draw_pair(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, cinc, sm, zs, acc1[cu],
                       acc1[cv]);
       } else {
         const int cu = q % L;
-        pcg_draw_one(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, cinc, sm, zmin, acc1[cu]);
+        pcg_draw_one(st[q][0], st[q][1], st[q][2], st[q][3], A0, A1, A2, A3, cinc, sm, zs, acc1[cu]);
       }
     }
   }
-  uint64_t acc = zmin;
+  uint64_t acc = zmin ^ zs;
 #pragma unroll
   for (int c = 0; c < L; c++) acc += acc1[c];
 #pragma unroll

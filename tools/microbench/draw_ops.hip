@@ -48,6 +48,10 @@ enum {
   kSubK,      // v_sub_u32_e32 v, 64, v (its 64 - r)
   kLshr64,    // v_lshrrev_b64 v[..], v, v[..]
   kLshl64,    // v_lshlrev_b64 v[..], v, v[..]
+  kXorK,      // v_xor_b32_e32 v, 63, v (the shift-rotation form's 63 - r)
+  kLshlAdd1,  // v_lshl_add_u64 v[..], v[..], 1, v[..] (its join of the two shifted parts)
+  kCmpEq64,   // v_cmp_eq_u64_e32 vcc, s[..], v[..] (its raw == 0 test)
+  kCmpEq64Or, // the same compare + s_or_b64 of the lane mask into an SGPR accumulator
   kNumOps
 };
 static const char* kNames[kNumOps] = {
@@ -55,7 +59,8 @@ static const char* kNames[kNumOps] = {
     "v_addc_co_u32_e64", "v_bitop3_b32", "v_cmp_gt_i32_e64", "v_lshrrev_b32", "v_alignbit_b32",
     "v_cndmask_b32_e64", "v_min3_u32", "v_lshl_add_u64", "v_sub_co_u32_e64", "v_subb_co_u32_e64",
     "v_add_u32_e32", "v_cmp_gt_i32_e32", "v_cndmask_b32_e32", "v_or_b32_e32", "v_sub_u32_e32 (64 - v)",
-    "v_lshrrev_b64", "v_lshlrev_b64"};
+    "v_lshrrev_b64", "v_lshlrev_b64", "v_xor_b32_e32 (63 ^ v)", "v_lshl_add_u64 (shift 1)",
+    "v_cmp_eq_u64_e32", "v_cmp_eq_u64_e32 + s_or_b64"};
 
 template <int OP>
 __global__ void __launch_bounds__(256) k_op(uint64_t* out, unsigned long long* clk, int iters, uint64_t seed) {
@@ -153,6 +158,24 @@ __global__ void __launch_bounds__(256) k_op(uint64_t* out, unsigned long long* c
 #undef X
     } else if constexpr (OP == kLshl64) {
 #define X(i) asm volatile("v_lshlrev_b64 %0, %1, %0" : "+v"(a##i) : "v"(bl));
+      R8(X) R8(X)
+#undef X
+    } else if constexpr (OP == kXorK) {
+#define X(i) asm volatile("v_xor_b32_e32 %0, 63, %0" : "+v"(LO(i)));
+      R8(X) R8(X)
+#undef X
+    } else if constexpr (OP == kLshlAdd1) {
+#define X(i) asm volatile("v_lshl_add_u64 %0, %1, 1, %0" : "+v"(a##i) : "v"(b));
+      R8(X) R8(X)
+#undef X
+    } else if constexpr (OP == kCmpEq64) {
+#define X(i) asm volatile("v_cmp_eq_u64_e32 vcc, %1, %0" : : "v"(a##i), "s"(b) : "vcc");
+      R8(X) R8(X)
+#undef X
+    } else if constexpr (OP == kCmpEq64Or) {
+      // per compare one SALU OR, as in the draw (counted as one wave instruction)
+#define X(i) asm volatile("v_cmp_eq_u64_e32 vcc, %1, %0\n\ts_or_b64 s[40:41], s[40:41], vcc" : : "v"(a##i), "s"(b) : "vcc", "scc", "s40", "s41");
+      asm volatile("s_mov_b64 s[40:41], 0" ::: "s40", "s41");
       R8(X) R8(X)
 #undef X
     } else {
