@@ -352,3 +352,20 @@ def test_single_draw_equals_numpy_pcg64(name):
                 assert e["vlo"] | e["vhi"] << 32 == (v - t) & M64
             elif name == "pcg_draw_pair_a":
                 assert e["v"] == (v + t) & M64
+
+
+def test_draw_instruction_budget():
+    """The committed header's per-block VALU counts: 48-50 per
+    two pair draws, 46 per two one-sided draws, no s_nop padding, and the
+    header matches what the generator emits today."""
+    import subprocess
+    import sys
+
+    text = open(os.path.join(ROOT, "sfl_amd", "csrc", "sa_draw2.h")).read()
+    counts = dict(re.findall(r"// (pcg_draw2_\w+): (\d+) VALU \+ 0 s_nop", text))
+    assert {k: int(v) for k, v in counts.items()} == {
+        "pcg_draw2_pair_ss": 50, "pcg_draw2_pair_sa": 49, "pcg_draw2_pair_as": 49, "pcg_draw2_pair_aa": 48,
+        "pcg_draw2_one": 46, "pcg_draw2_one_same": 46}
+    gen = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_draw2.py")],
+                         capture_output=True, text=True, check=True).stdout
+    assert gen == text, "sa_draw2.h is stale: regenerate with tools/gen_draw2.py"

@@ -1,0 +1,7 @@
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gpu_zero_tile.py tests/test_gpu_rejection.py > gpurun_out/zero_tile.log 2>&1
+rc=$?
+grep -E "PASSED|FAILED|passed|failed|Error" gpurun_out/zero_tile.log | tail -20
+exit $rc
