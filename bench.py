@@ -615,6 +615,12 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     digests = torch.zeros(Lc, dtype=torch.int64, device=dev) if args.digests else None
     flags = torch.zeros(1, dtype=torch.int32, device=dev)
     kev, xev = [], []  # event pairs around every masking launch / exchange of the timed steps
+    # one launch per step and nothing else on the stream (N = 1, one chunk):
+    # the launches run back to back, so ONE event pair around the timed
+    # region gives their average duration; a timing-event pair around every
+    # launch would itself open a ~5-10 us gap between launches (rocprof
+    # trace: 0 us between warm-up launches, 10 us between timed ones)
+    region = not multi and len(pipe.bounds) == 1
 
     def step(i, timed):
         if by_elems:
@@ -635,7 +641,7 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
         # launches (each chunk's launch still waits for that chunk's previous
         # exchange); the timed region ends with a device synchronise
         pipe.run(xs, [1.0] * Lc, gens[i], plan.n_cross, sum_buf, None, fxp_bits=args.fxp_bits,
-                 digests=digests, flags=flags, kernel_events=kev if timed else None,
+                 digests=digests, flags=flags, kernel_events=kev if timed and not region else None,
                  exchange_events=xev if timed else None, join=False, dec=dec, gather=v.gather)
 
     for i in range(warmup):
@@ -645,8 +651,13 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if region:
+        kev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+        kev[0][0].record(torch.cuda.current_stream(dev))
     for i in range(steps):
         step(warmup + i, True)
+    if region:
+        kev[0][1].record(torch.cuda.current_stream(dev))
     torch.cuda.synchronize()
     if multi:
         dist.barrier()
@@ -672,7 +683,9 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     res = {"name": v.name, "ms_per_step": ms, "value": C * N / (ms / 1e3), "steps": steps, "warmup": warmup,
            "kernel_ms_per_step": kern_ms, "chunks": len(pipe.bounds), "kernel": kname, "fused": fused,
            "local_clients": Lc, "n_loc": n_loc, "pair_draws": len(plan.pairs) * n_loc,
-           "one_sided_draws": len(plan.cross) * n_loc, "zero_draw_flag": flagged}
+           "one_sided_draws": len(plan.cross) * n_loc, "zero_draw_flag": flagged,
+           "kernel_timing": ("one HIP event pair on the launch stream around the timed region's back-to-back "
+                             "launches" if region else "a HIP event pair around every launch")}
     if multi:
         # bytes each rank hands the exchange per step; algbw as nccl-tests
         # defines it (buffer bytes / time), busbw the per-rank wire bytes
@@ -873,6 +886,7 @@ def main():
                      "launches_per_step": launches,
                      "algorithmic_bytes_per_launch": bytes_alg / launches,
                      "kernel_ms_per_launch": kern_ms / launches,
+                     "kernel_timing": r["kernel_timing"],
                      "valu": {"pcg64_draws_per_step": draws, "pair_draws_per_step": r["pair_draws"],
                               "one_sided_draws_per_step": r["one_sided_draws"],
                               "draws_per_s": draws / (kern_ms / 1e3),

@@ -58,3 +58,25 @@ def test_bench_n_ranks_every_design(world):
             assert v["kernel"].startswith("k_clients<float, float, 8, 0, ")
         else:
             assert v["xchg_ms"] > 0 and v["bytes_per_rank_per_step"] > 0
+
+
+def test_bench_n1_line():
+    """The driver's N = 1 bench path at a small size: one JSON line with the
+    contract's fields; one launch per step timed by one event pair around
+    the timed region (kernel time <= wall time per step)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--elems", "1000003", "--steps", "5",
+                        "--warmup", "2", "--cpu-baseline-seconds", "0"],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "roofline", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 5 and d["warmup"] == 2
+    rf = d["roofline"]
+    assert rf["launches_per_step"] == 1 and rf["kernel_timing"].startswith("one HIP event pair")
+    assert 0 < rf["kernel_ms_per_step"] <= d["ms_per_step"] * 1.01
+    assert abs(d["value"] - 8 * 1000003 / (d["ms_per_step"] / 1e3)) < 1e-6 * d["value"]
