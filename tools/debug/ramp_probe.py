@@ -46,6 +46,17 @@ def main():
     xs, s = bufs()
     torch.cuda.synchronize()
     out["fresh_buffers"] = batch(xs, s)
+    # 1 s idle, then ~100 ms of other GPU load in this process right before
+    # the batch: does preceding load (not this kernel) remove the ramp?
+    time.sleep(1.0)
+    t = torch.empty(100_000_000, device=dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(60):
+        t.mul_(1.0000001)
+    e1.record()
+    out["after_1s_idle_then_load"] = batch(xs, s)
+    out["load_ms"] = round(e0.elapsed_time(e1), 3)
     print(json.dumps(out))
 
 
