@@ -15,18 +15,21 @@ GPU, config 3 at N=8); each rank runs the fused masking over its clients
 (internal pairs + cross streams), pipelined in chunks against the exchange
 of the uint64 partial sums over xGMI.  `value` is measured on the sharded
 server (every rank receives and decodes its shard of the
-masked sum), its exchange done by ncclReduceScatter in place or by direct
-shard transfers + a local sum, whichever a short probe of both finds
-faster on this node (`exchange_probe`); the same process group then times every other
-design (`exchange_variants`: the shards also gathered to rank 0, the
+masked sum), its exchange done by ncclReduceScatter in place -- measured
+FIRST, before any other design; the same process group then times every
+other design (`exchange_variants`: the shards also gathered to rank 0, the
 sharded server over direct shard transfers, ncclReduce of the partial sums
-to rank 0, element sharding with and without the gather), so one run
-reports them all.  Total work is fixed as N grows:
+to rank 0, element sharding with and without the gather), each contained:
+a design that raises is recorded with its error, one that hangs past
+--variant-timeout makes rank 0 print the line so far (the headline stands).
+Total work is fixed as N grows:
 "scaling": "strong".  `python bench.py --gpus N` starts its N rank
 processes itself (torch.distributed.run as a child process with a c10d
-rendezvous on 127.0.0.1 port 0, before this process touches the GPU); under
-an outer torchrun (WORLD_SIZE set) it runs as one rank.  A rank still
-running after --watchdog-seconds (480) dumps every thread's stack and exits.
+rendezvous on 127.0.0.1 port 0, before this process touches the GPU; a
+failing rank's traceback is printed at the end); under an outer torchrun
+(WORLD_SIZE set) it runs as one rank.  A rank still running after
+--watchdog-seconds (480) without a headline dumps every thread's stack and
+exits 1.
 
 Inputs: synthetic N(0, 0.01^2) fp32 gradients generated on the GPU
 (torch.Generator seeded 20260116+c); pair seeds (0x5ECA66<<32)|(u<<16)|v as
@@ -342,14 +345,64 @@ def launch_ranks(args) -> int:
         with os.fdopen(fd, "w") as f:
             json.dump(cpu, f)
         env["SFL_BENCH_CPU_BASELINE"] = tmp
+    # every rank's stderr also goes to <log_dir>/.../<rank>/stderr.log (and
+    # still to the console, prefixed by the rank), so a failing rank's
+    # traceback survives the interleaving of eight ranks' output; stdout is
+    # left alone (rank 0's JSON line stays a bare line)
+    log_dir = tempfile.mkdtemp(prefix="sfl_bench_ranks_")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
            "--rdzv-backend", "c10d", "--rdzv-endpoint", "127.0.0.1:0", "--rdzv-id", f"sfl-bench-{uuid.uuid4().hex}",
-           "--local-addr", "127.0.0.1", os.path.abspath(__file__), *sys.argv[1:]]
+           "--local-addr", "127.0.0.1", "--log-dir", log_dir, "--redirects", "2", "--tee", "2",
+           os.path.abspath(__file__), *sys.argv[1:]]
     try:
-        return subprocess.run(cmd, env=env).returncode
+        rc = subprocess.run(cmd, env=env).returncode
+        if rc != 0:
+            sys.stderr.write(failing_ranks_report(log_dir))
+            sys.stderr.flush()
+        return rc
     finally:
         if tmp:
             os.unlink(tmp)
+        import shutil
+
+        shutil.rmtree(log_dir, ignore_errors=True)
+
+
+def failing_ranks_report(log_dir: str, lines_per_rank: int = 40) -> str:
+    """After a failed torchrun child: for every rank whose error file or
+    stderr log holds a traceback, its last traceback (torchrun's error.json
+    from @record first, else the tail of stderr.log from the last
+    'Traceback')."""
+    import glob
+
+    out = []
+    for path in sorted(glob.glob(os.path.join(log_dir, "**", "stderr.log"), recursive=True)):
+        rank_dir = os.path.dirname(path)
+        rank = os.path.basename(rank_dir)
+        text = ""
+        err_json = os.path.join(rank_dir, "error.json")
+        if os.path.exists(err_json):
+            try:
+                with open(err_json) as f:
+                    msg = json.load(f).get("message", {})
+                text = msg.get("extraInfo", {}).get("py_callstack", "") if isinstance(msg, dict) else str(msg)
+            except (OSError, ValueError):
+                text = ""
+        if not text:
+            with open(path, errors="replace") as f:
+                log = f.read()
+            # a Python exception, or a fatal signal's stacks (faulthandler is
+            # enabled in every rank)
+            i = max(log.rfind("Traceback (most recent call last)"), log.rfind("Fatal Python error"))
+            if i < 0:
+                continue
+            text = log[i:]
+        tail = text.rstrip().splitlines()[-lines_per_rank:]
+        out.append(f"---- bench.py: rank {rank} failed; its last traceback ({os.path.relpath(path, log_dir)}) ----\n"
+                   + "\n".join(tail) + "\n")
+    if not out:
+        return f"---- bench.py: the rank processes failed, no rank left a traceback under {log_dir} ----\n"
+    return "".join(out)
 
 
 def _draw_issue(case: str, waves: int, local_rank: int | None) -> dict | None:
@@ -405,10 +458,12 @@ def rank_cpu_baseline(args, world: int, rank: int):
     return cpu_baseline(args.clients, args.fxp_bits, rank_cpu_seconds(args, world), parallel=world == 1)
 
 
-def dry_run(args, world: int, rank: int, cpu) -> None:
+def dry_run(args, world: int, rank: int, cpu, wd: Watchdog) -> None:
     """Launcher rehearsal without a GPU (tests/test_bench_launcher.py): every
-    rank joins a gloo group and reports its pid; rank 0 prints one line
-    naming the headline design and every variant the GPU run would time."""
+    rank joins a gloo group and reports its pid, then the N > 1 design
+    sequence runs as on the GPU -- the headline first, every other design
+    contained by run_variants and the watchdog -- with dry_design's gloo
+    steps in place of the masking and the exchange; rank 0 prints one line."""
     import torch.distributed as dist
 
     multi = world > 1 or args.dist
@@ -419,16 +474,31 @@ def dry_run(args, world: int, rank: int, cpu) -> None:
         allr = [None] * world
         dist.all_gather_object(allr, ranks[0])
         ranks = allr
-        dist.destroy_process_group()
+    ctx = {"args": args, "world": world, "rank": rank}
     head = headline_variant(args, multi)
+    wd.enter("headline")
+    r = dry_design(ctx, head, args.steps, args.warmup)
+    line = {"metric": METRIC, "value": r["value"], "dry_run": True,
+            "data": "dry run: no GPU; every step one gloo all_reduce of 4 KiB (the control flow, not a rate)",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"],
+            "ranks": ranks, "config": {"workload": workload(args, world, head), "design": head.name},
+            "cpu_baseline": cpu, "watchdog_seconds": args.watchdog_seconds,
+            "variant_timeout_seconds": args.variant_timeout}
+    if multi:
+        line["exchange_variants"] = [dict(variant_summary(r), workload=workload(args, world, head))]
+        with wd.lock:
+            wd.line = line if rank == 0 else {}
+        others = other_variants(args, head)
+
+        def summarise(x):
+            return dict(variant_summary(x), workload=workload(args, world, Variant(x["name"])))
+
+        run_variants(ctx, dry_design, others, summarise, line, wd)
+    wd.enter("done")
     if rank == 0:
-        line = {"metric": METRIC, "value": None, "dry_run": True, "n_gpus": world, "ranks": ranks,
-                "config": {"workload": workload(args, world, head)}, "cpu_baseline": cpu,
-                "watchdog_seconds": args.watchdog_seconds}
-        if multi:
-            line["exchange_variants"] = [{"name": v.name, "workload": workload(args, world, v)}
-                                         for v in [head, *other_variants(args, head)]]
-        print(json.dumps(line), flush=True)
+        wd.emit(line)
+    if multi:
+        dist.destroy_process_group()
 
 
 METRIC = "grad elems/s device-resident: 100M-float quantize+mask+sum, 8 clients"
@@ -549,21 +619,268 @@ class GlooStandinComm:
         pass
 
 
-def probe_exchange(ctx, args):
-    """The sharded server has two implementations of its one exchange step
-    (the same shards, bytes and result): RCCL's reduce-scatter, or direct
-    shard transfers + a local sum.  Which is faster depends on RCCL's
-    schedule on this node's xGMI mesh, so without an explicit --exchange the
-    headline takes the faster of a short probe of both (--probe-steps each,
-    max over ranks, so every rank picks the same) and the line says so."""
-    args_gather = "+gather" if args.gather else ""
-    cands = [Variant(ex + args_gather) for ex in ("sharded", "direct")]
-    timed = [run_design(ctx, v, args.probe_steps, 3)["ms_per_step"] for v in cands]
-    best = 0 if timed[0] <= timed[1] else 1
-    return cands[best], {"steps": args.probe_steps, "warmup": 3, "chosen": cands[best].name,
-                         "ms_per_step": {v.name: t for v, t in zip(cands, timed)},
-                         "note": "two implementations of the sharded server's exchange (same shards, bytes and "
-                                 "result); the headline is measured with --steps on the faster one"}
+# ------------------------------------------------ failure containment (N > 1)
+#
+# The driver's N > 1 run is the only place the exchange designs meet xGMI, so
+# one bad design must not cost the line: the headline (the reduce-scatter
+# sharded server, the design with the most evidence) runs FIRST, every other
+# design runs inside `run_variants` (an exception is recorded in its
+# exchange_variants entry; the ranks agree over a gloo control group before
+# the next one), and the watchdog thread prints the line built so far when a
+# design hangs.  SFL_BENCH_INJECT rehearses each failure (tests only):
+#   fail:<design>[@<rank>]   run_design of <design> raises (on one rank or all)
+#   hang:<design>[@<rank>]   run_design of <design> never returns
+#   raise:rank<r>            rank r raises at start-up, before any collective
+
+def injected(kind: str, design: str | None, rank: int) -> bool:
+    """Whether SFL_BENCH_INJECT asks for failure ``kind`` here (see above)."""
+    spec = os.environ.get("SFL_BENCH_INJECT", "")
+    for item in filter(None, spec.split(",")):
+        k, _, rest = item.partition(":")
+        if k != kind:
+            continue
+        if kind == "raise":
+            if rest == f"rank{rank}":
+                return True
+            continue
+        name, _, r = rest.partition("@")
+        if name == design and (not r or int(r) == rank):
+            return True
+    return False
+
+
+def inject_in_design(v_name: str, rank: int) -> None:
+    if injected("fail", v_name, rank):
+        raise RuntimeError(f"SFL_BENCH_INJECT: injected failure in design {v_name!r} on rank {rank}")
+    if injected("hang", v_name, rank):
+        print(f"bench.py rank {rank}: SFL_BENCH_INJECT: design {v_name!r} hangs", file=sys.stderr, flush=True)
+        while True:
+            time.sleep(3600)
+
+
+class Watchdog:
+    """Bounds a rank's run and keeps its measurement.
+
+    * A design other than the headline that runs longer than
+      ``variant_timeout`` seconds (or the run nearing ``total`` seconds after
+      the headline finished) is declared hung: rank 0 prints the line built
+      so far with that design marked and ``variants_incomplete``, every rank
+      dumps its threads' stacks to stderr and exits 0 -- the headline stands.
+    * Before the headline has finished there is nothing to keep: at
+      ``total`` seconds ``faulthandler`` (a C thread, which fires even while
+      the main thread holds the GIL) dumps every stack and exits 1.
+
+    A Python thread, polled every 0.25 s: it runs while the main thread waits
+    in a GIL-releasing call (a ctypes RCCL call, a device synchronise, a
+    c10d wait), which is where a hung collective leaves it."""
+
+    def __init__(self, total: float, variant_timeout: float, rank: int):
+        import threading
+
+        self.total, self.variant_timeout, self.rank = total, variant_timeout, rank
+        self.t0 = time.monotonic()
+        self.phase, self.t_phase = "setup", self.t0
+        self.line = None        # rank 0's line so far, once the headline has finished
+        self.pending = []       # designs not yet run
+        self.lock = threading.Lock()
+        self.printed = False
+        if total > 0:
+            import faulthandler
+
+            faulthandler.dump_traceback_later(total, exit=True)
+            threading.Thread(target=self._loop, name="bench-watchdog", daemon=True).start()
+
+    def enter(self, phase: str) -> None:
+        with self.lock:
+            self.phase, self.t_phase = phase, time.monotonic()
+            if phase in self.pending:
+                self.pending.remove(phase)
+
+    def emit(self, line: dict) -> bool:
+        """Print ``line`` (rank 0), once per process."""
+        with self.lock:
+            if self.printed:
+                return False
+            self.printed = True
+        print(json.dumps(line), flush=True)
+        return True
+
+    def _loop(self):
+        warned = False
+        while True:
+            time.sleep(0.25)
+            now = time.monotonic()
+            with self.lock:
+                phase, t_phase, line = self.phase, self.t_phase, self.line
+            left = self.total - (now - self.t0)
+            if line is not None and phase not in ("headline", "done") and (
+                    now - t_phase > self.variant_timeout or left < 10):
+                self._give_up(phase, now - t_phase)
+            if line is None and left < 3 and not warned:
+                warned = True
+                print(f"bench.py rank {self.rank}: headline not finished after {self.total - 3:.0f} s; "
+                      f"dumping every thread's stack and exiting", file=sys.stderr, flush=True)
+
+    def _give_up(self, phase: str, waited: float):
+        import copy
+        import faulthandler
+
+        with self.lock:
+            line = copy.deepcopy(self.line)
+            pending = list(self.pending)
+        msg = (f"design {phase!r} did not finish within {waited:.0f} s on rank {self.rank} (hung); every rank's "
+               f"stacks are on stderr; the headline and the designs before it stand")
+        errs = published_errors(phase) if self.rank == 0 else []
+        if errs:  # a rank that raised left its peers waiting in the design's collectives
+            msg += "; errors raised by ranks: " + "; ".join(errs)
+        print(f"bench.py rank {self.rank}: {msg}", file=sys.stderr, flush=True)
+        if self.rank == 0:
+            line.setdefault("exchange_variants", []).append({"name": phase, "error": "hung", "detail": msg})
+            line["exchange_variants"] += [{"name": p, "error": "skipped", "detail": f"not run: {phase!r} hung"}
+                                          for p in pending]
+            line["variants_incomplete"] = True
+            self.emit(line)
+        faulthandler.dump_traceback(all_threads=True)
+        sys.stderr.flush()
+        os._exit(0)
+
+
+def _store():
+    """The process group's c10d store (torchrun's TCPStore): independent of
+    the collectives, so a rank can leave a message there that rank 0 can read
+    while a design's collectives hang."""
+    try:
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            return dist.distributed_c10d._get_default_store()
+    except Exception:  # noqa: BLE001 -- best effort, the line does not depend on it
+        pass
+    return None
+
+
+def publish_error(design: str, rank: int, text: str) -> None:
+    s = _store()
+    if s is not None:
+        try:
+            s.set(f"sfl_bench_err/{design}/{rank}", text)
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def published_errors(design: str, world: int | None = None) -> list[str]:
+    s = _store()
+    if s is None:
+        return []
+    world = world or int(os.environ.get("WORLD_SIZE", "1"))
+    out = []
+    for r in range(world):
+        key = f"sfl_bench_err/{design}/{r}"
+        try:
+            if s.check([key]):
+                out.append(s.get(key).decode(errors="replace"))
+        except Exception:  # noqa: BLE001
+            pass
+    return out
+
+
+def control_group(ctx):
+    """A gloo group for agreement between designs: CPU tensors, so it still
+    works when a design left the GPU streams or the RCCL communicator
+    unusable."""
+    import torch.distributed as dist
+
+    if ctx.get("ctrl") is None:
+        ctx["ctrl"] = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
+    return ctx["ctrl"]
+
+
+def run_variants(ctx, runner, variants, summarise, out: dict, wd: Watchdog) -> None:
+    """Every design after the headline, each contained: an exception on any
+    rank is printed there (traceback on stderr) and recorded in its entry of
+    out["exchange_variants"]; the ranks agree (gloo all_gather of the error
+    texts) before the next design.  A design that failed on EVERY rank left
+    no collective half-issued, so the next one runs; one that failed on some
+    ranks only may have left the others' exchange pending, so the remaining
+    designs are skipped and the line printed as it stands."""
+    import traceback
+
+    import torch.distributed as dist
+
+    args, rank = ctx["args"], ctx["rank"]
+    group = control_group(ctx)
+    with wd.lock:
+        wd.pending = [v.name for v in variants]
+    for i, v in enumerate(variants):
+        wd.enter(v.name)
+        err = None
+        try:
+            res = runner(ctx, v, args.variant_steps, min(5, args.warmup))
+        except Exception as e:  # noqa: BLE001 -- contained, reported in the line
+            err = f"rank {rank}: {e!r}"
+            print(f"bench.py rank {rank}: design {v.name!r} failed:", file=sys.stderr)
+            traceback.print_exc()
+            sys.stderr.flush()
+            publish_error(v.name, rank, err)
+        errs = [None] * ctx["world"]
+        dist.all_gather_object(errs, err, group=group)
+        failed = [e for e in errs if e is not None]
+        with wd.lock:
+            if not failed:
+                out["exchange_variants"].append(summarise(res))
+                continue
+            out["exchange_variants"].append({"name": v.name, "error": "failed", "detail": "; ".join(failed)})
+            if len(failed) < ctx["world"]:
+                rest = [x.name for x in variants[i + 1:]]
+                out["exchange_variants"] += [{"name": p, "error": "skipped",
+                                              "detail": f"not run: {v.name!r} failed on some ranks only"}
+                                             for p in rest]
+                out["variants_incomplete"] = True
+                wd.pending = []
+                return
+    with wd.lock:
+        wd.pending = []
+
+
+def variant_summary(x: dict) -> dict:
+    return {"name": x["name"], "value": x["value"], "ms_per_step": x["ms_per_step"], "steps": x["steps"],
+            "kernel_ms_per_step": x["kernel_ms_per_step"], "kernel": x["kernel"], "chunks": x["chunks"],
+            "xchg_ms": x["exchange"]["ms_per_step"], "bytes_per_rank_per_step": x["exchange"]["bytes_per_rank_per_step"],
+            "algbw_GBps": x["exchange"]["algbw_GBps"], "busbw_GBps": x["exchange"]["busbw_GBps"],
+            "collective": x["exchange"]["collective"]}
+
+
+def dry_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
+    """--dry-run's stand-in for run_design (no GPU): every step is one gloo
+    all_reduce of a small CPU tensor among the ranks, timed like a design
+    (barrier on both sides, max over ranks), with run_design's result keys
+    and the fault injection; its numbers are the control flow's, not a rate."""
+    import torch
+    import torch.distributed as dist
+
+    args, world, rank = ctx["args"], ctx["world"], ctx["rank"]
+    inject_in_design(v.name, rank)
+    multi = world > 1
+    t = torch.ones(1024)
+    for _ in range(warmup):
+        if multi:
+            dist.all_reduce(t)
+    if multi:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if multi:
+            dist.all_reduce(t)
+    if multi:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if multi:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    ms = float(el[0]) * 1e3 / max(1, steps)
+    return {"name": v.name, "ms_per_step": ms, "value": args.clients * args.elems / max(ms / 1e3, 1e-9),
+            "steps": steps, "warmup": warmup, "kernel_ms_per_step": 0.0, "chunks": 1, "kernel": "none (dry run)",
+            "exchange": {"ms_per_step": ms, "bytes_per_rank_per_step": 4096, "algbw_GBps": None, "busbw_GBps": None,
+                         "collective": "dry run: one gloo all_reduce of 4 KiB per step"}}
 
 
 def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
@@ -578,6 +895,7 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     from sfl_amd.parallel_sum import PipelinedMaskedSum, element_shard, plan_generators, plan_rank
 
     args, world, rank, dev, comm = ctx["args"], ctx["world"], ctx["rank"], ctx["dev"], ctx["comm"]
+    inject_in_design(v.name, rank)
     multi = comm is not None
     C, N = args.clients, args.elems
     by_elems = v.shard == "elements"
@@ -754,10 +1072,9 @@ def main():
                          f"('all' = {','.join(VARIANTS)}; a comma list; 'none')")
     ap.add_argument("--variant-steps", type=int, default=None,
                     help="timed steps per extra design (default: min(200, --steps))")
-    ap.add_argument("--probe-steps", type=int, default=20,
-                    help="N>1 sharded server without --exchange: time this many steps of each exchange "
-                         "implementation (reduce-scatter, direct transfers) first and take the faster for the "
-                         "headline (0: always the reduce-scatter)")
+    ap.add_argument("--variant-timeout", type=float, default=120.0,
+                    help="N>1: a design after the headline still running after this many seconds is declared "
+                         "hung; rank 0 prints the line so far with that design marked, every rank exits 0")
     ap.add_argument("--digests", action="store_true",
                     help="also fold every client's masked values into an XOR digest (test checksum)")
     ap.add_argument("--dry-run", action="store_true",
@@ -767,9 +1084,10 @@ def main():
                          "collectives through gloo host round trips (RCCL refuses two ranks on one GPU); runs "
                          "every design's code path, its timings are not the product's")
     ap.add_argument("--watchdog-seconds", type=float, default=480.0,
-                    help="a rank still running after this long dumps every thread's stack (faulthandler) and "
-                         "exits (a hung collective cannot be interrupted from Python; torchrun then stops the "
-                         "other ranks); below the driver's 600 s lease; 0 disables")
+                    help="a rank still running after this long exits: with the headline done, rank 0 first "
+                         "prints the line so far (Watchdog); before it, faulthandler dumps every thread's stack "
+                         "and exits 1 (torchrun then stops the other ranks); below the driver's 600 s lease; "
+                         "0 disables")
     args = ap.parse_args()
     if args.variant_steps is None:
         args.variant_steps = max(1, min(200, args.steps))
@@ -779,30 +1097,30 @@ def main():
 
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dist):
         sys.exit(launch_ranks(args))
+    # a rank: an uncaught exception is written to torchrun's error file, so
+    # the launcher's failure summary names this rank and shows its traceback
+    from torch.distributed.elastic.multiprocessing.errors import record
+
+    record(rank_main)(args)
+
+
+def rank_main(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.watchdog_seconds > 0:
-        import faulthandler
-        import threading
+    import faulthandler
 
-        def _note():
-            print(f"bench.py rank {rank}: still running after {args.watchdog_seconds - 2:.0f} s; dumping every "
-                  f"thread's stack and exiting", file=sys.stderr, flush=True)
-
-        t = threading.Timer(max(0.0, args.watchdog_seconds - 2), _note)
-        t.daemon = True
-        t.start()
-        # a C thread: dumps and exits even while the main thread sits in a
-        # collective holding the GIL
-        faulthandler.dump_traceback_later(args.watchdog_seconds, exit=True)
+    faulthandler.enable(all_threads=True)  # a fatal signal in a rank leaves its stacks in its stderr log
+    wd = Watchdog(args.watchdog_seconds, args.variant_timeout, rank)
+    if injected("raise", None, rank):
+        raise RuntimeError(f"SFL_BENCH_INJECT: rank {rank} fails at start-up")
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # CPU baseline first: its per-client worker processes are forked, which
     # must happen before this process initialises the GPU
     cpu = rank_cpu_baseline(args, world, rank)
     if args.dry_run:
-        dry_run(args, world, rank, cpu)
+        dry_run(args, world, rank, cpu, wd)
         return
     multi = world > 1 or args.dist
     # same-box draw-loop ceilings, also before this process initialises the GPU
@@ -831,9 +1149,7 @@ def main():
     ctx = {"args": args, "world": world, "rank": rank, "dev": dev, "comm": comm, "rehearse": rehearse,
            "names": [f"client{c}" for c in range(C)]}
     head = headline_variant(args, multi)
-    probe = None
-    if multi and args.exchange is None and head.shard == "clients" and args.probe_steps > 0:
-        head, probe = probe_exchange(ctx, args)
+    wd.enter("headline")
     r = run_design(ctx, head, args.steps, args.warmup, keep=args.extra and world == 1)
     if r["zero_draw_flag"]:
         print("warning: PRG zero-draw flag raised", file=sys.stderr)
@@ -901,30 +1217,33 @@ def main():
                               "frac": ideal_s / (kern_ms / 1e3),
                               "issue": int_ops}},
     }
-    if multi:
-        out["exchange"] = r["exchange"]
-        if probe is not None:
-            out["exchange_probe"] = probe
-        variants = [r]
-        for v in other_variants(args, head):
-            variants.append(run_design(ctx, v, args.variant_steps, min(5, args.warmup)))
-        out["exchange_variants"] = [
-            {"name": x["name"], "value": x["value"], "ms_per_step": x["ms_per_step"], "steps": x["steps"],
-             "kernel_ms_per_step": x["kernel_ms_per_step"], "kernel": x["kernel"], "chunks": x["chunks"],
-             "xchg_ms": x["exchange"]["ms_per_step"], "bytes_per_rank_per_step": x["exchange"]["bytes_per_rank_per_step"],
-             "algbw_GBps": x["exchange"]["algbw_GBps"], "busbw_GBps": x["exchange"]["busbw_GBps"],
-             "collective": x["exchange"]["collective"]} for x in variants]
     if rehearse:
         out["rehearsal"] = ("--rehearse-one-gpu: every rank on cuda:0, collectives through gloo host round "
                             "trips; the N > 1 control flow, not the product's rate")
+    out["cpu_baseline"] = cpu
+    if multi:
+        # the headline is in hand: from here on a failed or hung design is
+        # recorded in its exchange_variants entry and cannot cost the line
+        out["exchange"] = r["exchange"]
+        out["exchange_variants"] = [variant_summary(r)]
+        out["variant_timeout_seconds"] = args.variant_timeout
+        with wd.lock:
+            wd.line = out if rank == 0 else {}
+        run_variants(ctx, run_design, other_variants(args, head), variant_summary, out, wd)
     if args.extra and world == 1:
         from sfl_amd import kernels as K
 
         kept = ctx["kept"]
         out["extra"] = extra_measurements(args, kept["xs"], kept["plan"], kept["gens"], K, torch, dev)
+    wd.enter("done")
     if rank == 0:
-        out["cpu_baseline"] = cpu
-        print(json.dumps(out), flush=True)
+        wd.emit(out)
+    if out.get("variants_incomplete"):
+        # a design failed on some ranks only: their peers' exchange may still
+        # be pending on the GPU, which a communicator teardown would wait for
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
     if comm is not None:
         comm.close()
         dist.destroy_process_group()

@@ -120,7 +120,7 @@ def test_bench_kernel_variant_table_matches_the_registry():
 def test_n_gt_1_line_names_every_exchange_design_and_a_safe_launch():
     """One `bench.py --gpus N` run times every N>1 design in the same process
     group (exchange_variants, the headline first); the ranks rendezvous on a
-    port the store bound itself (no probe); the watchdog fires before the
+    port the store bound itself (no port probe); the watchdog fires before the
     driver's 600 s lease."""
     import bench
 
@@ -198,3 +198,73 @@ def test_pmc_valu_reads_the_census_of_the_timed_kernel():
     half = bench.pmc_valu("void sa::k_clients<float, float, 8, 0, 4>", n // 2)
     assert abs(half["valu_wave_instr"] * 2 - v["valu_wave_instr"]) < 1
     assert bench.pmc_valu("void sa::k_clients<float, float, 3, 5, 4>", n) is None
+
+
+def _dry(n, inject, *extra):
+    env = _env()
+    env["SFL_BENCH_INJECT"] = inject
+    return subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--dry-run", "--cpu-baseline-seconds", "0",
+                           "--steps", "3", "--warmup", "1", *extra],
+                          capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+
+
+def test_failed_design_is_recorded_and_the_run_goes_on():
+    """A design after the headline that raises on every rank is recorded in
+    its exchange_variants entry (with the error) and the next design runs;
+    the headline value stands, exactly one line, exit 0."""
+    r = _dry(2, "fail:direct")
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    assert line["value"] > 0 and line["config"]["design"] == "sharded" and not line.get("variants_incomplete")
+    got = {v["name"]: v for v in line["exchange_variants"]}
+    assert got["direct"]["error"] == "failed" and "injected failure in design 'direct'" in got["direct"]["detail"]
+    assert got["reduce"]["value"] > 0 and got["elements+gather"]["value"] > 0
+
+
+def test_hung_design_prints_the_line_so_far():
+    """A design that hangs past --variant-timeout: rank 0's watchdog prints
+    the line built so far (the headline and the designs before the hang),
+    the hung design marked, the rest skipped; every rank exits 0."""
+    r = _dry(2, "hang:elements", "--variant-timeout", "4")
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    assert line["value"] > 0 and line["variants_incomplete"]
+    got = {v["name"]: v for v in line["exchange_variants"]}
+    assert got["sharded"]["value"] > 0 and got["reduce"]["value"] > 0
+    assert got["elements"]["error"] == "hung" and got["elements+gather"]["error"] == "skipped"
+
+
+def test_design_failing_on_one_rank_names_the_rank():
+    """A design raising on ONE rank leaves its peers in the design's
+    collectives: the watchdog declares it hung and the line carries the
+    failing rank's error (published through the c10d store)."""
+    r = _dry(2, "fail:reduce@1", "--variant-timeout", "4")
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    got = {v["name"]: v for v in line["exchange_variants"]}
+    assert got["reduce"]["error"] == "hung" and "rank 1: RuntimeError" in got["reduce"]["detail"]
+    assert got["elements"]["error"] == "skipped" and got["direct"]["value"] > 0
+
+
+def test_failing_rank_prints_its_traceback_last():
+    """A rank that fails at start-up: the launcher's stderr ends with that
+    rank's traceback (per-rank logs / torchrun's error file), rc != 0."""
+    r = _dry(4, "raise:rank3")
+    assert r.returncode != 0
+    tail = r.stderr[-2500:]
+    assert "rank 3 failed" in tail and "SFL_BENCH_INJECT: rank 3 fails at start-up" in tail, tail
+    assert not _json_lines(r.stdout)
+
+
+def test_injection_parser():
+    import bench
+
+    os.environ["SFL_BENCH_INJECT"] = "fail:direct@2,hang:elements,raise:rank3"
+    try:
+        assert bench.injected("fail", "direct", 2) and not bench.injected("fail", "direct", 1)
+        assert bench.injected("hang", "elements", 0) and bench.injected("hang", "elements", 7)
+        assert not bench.injected("hang", "elements+gather", 0)
+        assert bench.injected("raise", None, 3) and not bench.injected("raise", None, 0)
+    finally:
+        del os.environ["SFL_BENCH_INJECT"]
+    assert not bench.injected("fail", "direct", 0)
