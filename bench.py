@@ -478,13 +478,14 @@ def dry_run(args, world: int, rank: int, cpu, wd: Watchdog) -> None:
     head = headline_variant(args, multi)
     wd.enter("headline")
     r = dry_design(ctx, head, args.steps, args.warmup)
-    line = {"metric": METRIC, "value": r["value"], "dry_run": True,
+    line = {"metric": METRIC, "value": r["value"], "dry_run": True, "check": {"round": 0, "decoded_xor": r["check_xor"]},
             "data": "dry run: no GPU; every step one gloo all_reduce of 4 KiB (the control flow, not a rate)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"],
             "ranks": ranks, "config": {"workload": workload(args, world, head), "design": head.name},
             "cpu_baseline": cpu, "watchdog_seconds": args.watchdog_seconds,
             "variant_timeout_seconds": args.variant_timeout}
     if multi:
+        line["designs_agree"] = True
         line["exchange_variants"] = [dict(variant_summary(r), workload=workload(args, world, head))]
         with wd.lock:
             wd.line = line if rank == 0 else {}
@@ -631,6 +632,7 @@ class GlooStandinComm:
 #   fail:<design>[@<rank>]   run_design of <design> raises (on one rank or all)
 #   hang:<design>[@<rank>]   run_design of <design> never returns
 #   raise:rank<r>            rank r raises at start-up, before any collective
+#   corrupt:<design>[@<rank>] the design's round-0 result check is off by one bit
 
 def injected(kind: str, design: str | None, rank: int) -> bool:
     """Whether SFL_BENCH_INJECT asks for failure ``kind`` here (see above)."""
@@ -827,7 +829,12 @@ def run_variants(ctx, runner, variants, summarise, out: dict, wd: Watchdog) -> N
         failed = [e for e in errs if e is not None]
         with wd.lock:
             if not failed:
-                out["exchange_variants"].append(summarise(res))
+                entry = summarise(res)
+                want = out.get("check", {}).get("decoded_xor")
+                if want is not None and entry.get("check_xor") != want:
+                    entry["mismatch"] = f"round-0 result check {entry.get('check_xor')} != the headline's {want}"
+                    out["designs_agree"] = False
+                out["exchange_variants"].append(entry)
                 continue
             out["exchange_variants"].append({"name": v.name, "error": "failed", "detail": "; ".join(failed)})
             if len(failed) < ctx["world"]:
@@ -847,7 +854,7 @@ def variant_summary(x: dict) -> dict:
             "kernel_ms_per_step": x["kernel_ms_per_step"], "kernel": x["kernel"], "chunks": x["chunks"],
             "xchg_ms": x["exchange"]["ms_per_step"], "bytes_per_rank_per_step": x["exchange"]["bytes_per_rank_per_step"],
             "algbw_GBps": x["exchange"]["algbw_GBps"], "busbw_GBps": x["exchange"]["busbw_GBps"],
-            "collective": x["exchange"]["collective"]}
+            "collective": x["exchange"]["collective"], "check_xor": x.get("check_xor")}
 
 
 def dry_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
@@ -877,10 +884,65 @@ def dry_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     if multi:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     ms = float(el[0]) * 1e3 / max(1, steps)
+    check = int(injected("corrupt", v.name, rank))
+    if multi:  # combined over the ranks like result_check
+        parts = [None] * world
+        dist.all_gather_object(parts, check)
+        check = 0
+        for p in parts:
+            check ^= p
     return {"name": v.name, "ms_per_step": ms, "value": args.clients * args.elems / max(ms / 1e3, 1e-9),
             "steps": steps, "warmup": warmup, "kernel_ms_per_step": 0.0, "chunks": 1, "kernel": "none (dry run)",
             "exchange": {"ms_per_step": ms, "bytes_per_rank_per_step": 4096, "algbw_GBps": None, "busbw_GBps": None,
-                         "collective": "dry run: one gloo all_reduce of 4 KiB per step"}}
+                         "collective": "dry run: one gloo all_reduce of 4 KiB per step"},
+            "check_xor": f"{check:016x}"}
+
+
+CHECK_NOTE = ("XOR of the bits of the decoded float64 aggregate (all C clients, every element) of round 0, "
+              "recomputed after the timed region by one more untimed step of the same design: every design and "
+              "every N must print the same value (the same inputs, seeds and stream positions)")
+
+
+def result_check(ctx, v: Variant, step, sum_buf, dec, dec_all, sharded: bool, by_elems: bool) -> str:
+    """The design's result for round 0, reduced to one 64-bit XOR of the
+    decoded vector's float64 bits (CHECK_NOTE), combined over the ranks: a
+    mis-indexed shard transfer or a wrong slot shows as a differing value
+    between designs (run_variants flags it) or between N = 1 and N > 1."""
+    import torch
+    import torch.distributed as dist
+
+    from sfl_amd import kernels as K
+
+    args, world, rank, dev, comm = ctx["args"], ctx["world"], ctx["rank"], ctx["dev"], ctx["comm"]
+    step(0, False)
+    torch.cuda.synchronize()
+    dig = torch.zeros(1, dtype=torch.int64, device=dev)
+    src = None
+    if by_elems:  # every rank its decoded slice; with the gather rank 0 holds them all
+        src = dec_all if v.gather else dec
+        if v.gather and rank != 0:
+            src = None
+        if comm is None:  # world 1 without --dist: the slice is the whole vector, not decoded by the step
+            src = torch.empty(args.elems, dtype=torch.float64, device=dev)
+            K.decode(sum_buf[:args.elems], src, fxp_bits=args.fxp_bits)
+    elif sharded:  # every rank decoded its shards in place (zeros elsewhere); with the gather rank 0 all
+        src = dec if (not v.gather or rank == 0) else None
+    elif rank == 0:  # reduce (and N = 1): rank 0 holds the masked sum
+        src = torch.empty(args.elems, dtype=torch.float64, device=dev)
+        K.decode(sum_buf[:args.elems], src, fxp_bits=args.fxp_bits)
+    if src is not None:
+        K.xor_digest(src.view(torch.int64), dig)
+    torch.cuda.synchronize()
+    x = int(dig.item()) & (2 ** 64 - 1)
+    if injected("corrupt", v.name, rank):  # SFL_BENCH_INJECT: a wrong result on this rank
+        x ^= 1
+    if comm is not None and world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, x, group=control_group(ctx))
+        x = 0
+        for p in parts:
+            x ^= p
+    return f"{x:016x}"
 
 
 def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
@@ -988,6 +1050,7 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
                          device="cpu" if ctx.get("rehearse") else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms, xchg_ms = float(t[0]), float(t[1]), float(t[2])
+    check = result_check(ctx, v, step, sum_buf, dec, dec_all, sharded, by_elems)
     flagged = bool(int(flags.item()))
     ms = elapsed * 1e3 / steps
     n_streams = len(plan.pairs) + len(plan.cross)
@@ -1001,7 +1064,7 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     res = {"name": v.name, "ms_per_step": ms, "value": C * N / (ms / 1e3), "steps": steps, "warmup": warmup,
            "kernel_ms_per_step": kern_ms, "chunks": len(pipe.bounds), "kernel": kname, "fused": fused,
            "local_clients": Lc, "n_loc": n_loc, "pair_draws": len(plan.pairs) * n_loc,
-           "one_sided_draws": len(plan.cross) * n_loc, "zero_draw_flag": flagged,
+           "one_sided_draws": len(plan.cross) * n_loc, "zero_draw_flag": flagged, "check_xor": check,
            "kernel_timing": ("one HIP event pair on the launch stream around the timed region's back-to-back "
                              "launches" if region else "a HIP event pair around every launch")}
     if multi:
@@ -1221,7 +1284,9 @@ def rank_main(args):
         out["rehearsal"] = ("--rehearse-one-gpu: every rank on cuda:0, collectives through gloo host round "
                             "trips; the N > 1 control flow, not the product's rate")
     out["cpu_baseline"] = cpu
+    out["check"] = {"round": 0, "decoded_xor": r["check_xor"], "note": CHECK_NOTE}
     if multi:
+        out["designs_agree"] = True
         # the headline is in hand: from here on a failed or hung design is
         # recorded in its exchange_variants entry and cannot cost the line
         out["exchange"] = r["exchange"]

@@ -239,6 +239,9 @@ class LoopbackServer:
         if self._bufs is None or self._bufs[0] != n:
             dev = torch.device("cuda", self.gpu)
             ce = min(n, chunk_elems())
+            if self._bufs is not None:  # the old result pages (8n bytes, HIP-registered) go now, not at GC
+                self._bufs[4][2].close()
+                self._bufs = None
             ring = [[torch.empty(ce, dtype=torch.int64).pin_memory() for _ in range(2)] for _ in self.conns]
             devb = [torch.empty(n, dtype=torch.int64, device=dev) for _ in self.conns]
             streams = [torch.cuda.Stream(dev) for _ in self.conns]
@@ -248,8 +251,17 @@ class LoopbackServer:
             self._bufs = (n, ring, devb, streams, agg)
         return self._bufs[1:]
 
-    def round(self, n: int, rnd: int, *, average: bool = False, verify_digest: bool = False,
-              keep_masked: bool = False, timeout: float = 600.0, copy_out: bool = True):
+    def round(self, n: int, rnd: int, **kw):
+        """One aggregation round on the server's GPU (``_round``): HIP calls
+        made here without a tensor argument (host registration, events) go
+        to that device too, whatever device the calling process is on."""
+        import torch
+
+        with torch.cuda.device(self.gpu):
+            return self._round(n, rnd, **kw)
+
+    def _round(self, n: int, rnd: int, *, average: bool = False, verify_digest: bool = False,
+               keep_masked: bool = False, timeout: float = 600.0, copy_out: bool = True):
         """One aggregation round over n-element vectors -> (float64 result, timings).
 
         ``copy_out=False`` returns the server's own result buffer (the pages the
@@ -511,11 +523,6 @@ class LoopbackClient:
         GPU box's kernel that stalls sendfile()d transfers, tools/socket_floor.py
         --client-sequential).  ``result()`` then joins it; ``last_result_xor``
         holds the XOR of the result's 64-bit words."""
-        import torch
-
-        from . import _lib as L
-        from . import kernels as K
-
         n = x.size
         if self._rx is not None:
             raise RuntimeError("the previous round's result was not collected (result())")
@@ -536,6 +543,28 @@ class LoopbackClient:
             t = threading.Thread(target=self._receive_result, args=(n, target, box), daemon=True)
             t.start()
             self._rx = (t, box, keep, n)
+        try:
+            return self._mask_and_send(x, n, rnd, weight, dp)
+        except BaseException:
+            # the result receiver started above would stay blocked in recv and
+            # the next submit() would report an uncollected round: end the
+            # connection (the server sees the failure) and the thread with it
+            if self._rx is not None:
+                t = self._rx[0]
+                self._rx = None
+                try:
+                    self.sock.shutdown(socket.SHUT_RDWR)
+                except OSError:
+                    pass
+                t.join(timeout=30)
+            raise
+
+    def _mask_and_send(self, x: np.ndarray, n: int, rnd: int, weight, dp) -> dict:
+        import torch
+
+        from . import _lib as L
+        from . import kernels as K
+
         hx, hmb, dx, dm, cs = self._buffers(n)
         hm = hmb.tensor()
         dev = dx.device
@@ -671,16 +700,35 @@ def synthetic_gradient(c: int, n: int, rnd: int = 0) -> np.ndarray:
     return (g.standard_normal(n, dtype=np.float32) * np.float32(1e-2)).astype(np.float32)
 
 
+def placement(n_procs: int, gpus: list[int], server_gpu: int | None = None) -> tuple[int, list[int]]:
+    """Where the parties run: (the server's GPU, the GPU of each client
+    process g = gpus[g % len(gpus)]).  One client process per GPU on the
+    8-GPU node (config 3), or four parties per process and one process per
+    GPU (config 5), so every GPU's PCIe link carries only its own parties'
+    H2D / D2H -- as the reference runs one party per process on its own
+    device (tests/conftest.py:386-394, sfl/distributed/op_strategy.py:131-141).
+    The server takes ``server_gpu`` (default ``gpus[0]``)."""
+    if not gpus:
+        raise ValueError("placement: no GPUs")
+    if n_procs < 0:
+        raise ValueError("placement: negative process count")
+    return (gpus[0] if server_gpu is None else server_gpu), [gpus[g % len(gpus)] for g in range(n_procs)]
+
+
 def client_process(parties: list, port: int, n: int, rounds: int, gpu: int, fxp_bits: int, out_q,
                    keep_results: bool = True) -> None:
     """Entry point of one spawned process hosting one or more client parties
     (``parties``: (name, index, pair seeds or None, weight) tuples), each on
-    its own socket and thread.  Every party records the XOR of each round's
-    result; ``keep_results=False`` receives the results through a ring of two
-    chunk buffers instead of a whole-vector array (config 5's 32 parties x
-    256M elements would otherwise hold 64 GB of results)."""
+    its own socket and thread, all on GPU ``gpu``.  Every party records the
+    XOR of each round's result; ``keep_results=False`` receives the results
+    through a ring of two chunk buffers instead of a whole-vector array
+    (config 5's 32 parties x 256M elements would otherwise hold 64 GB of
+    results)."""
     import threading
 
+    import torch
+
+    torch.cuda.set_device(gpu)  # this process's HIP calls (host registration, copies) on its own GPU
     dump_after = float(os.environ.get("SFL_LOOPBACK_DUMP_AFTER", "0"))
     if dump_after > 0:  # diagnostics: every thread's stack if the process is still here then
         import faulthandler
@@ -726,30 +774,36 @@ def client_process(parties: list, port: int, n: int, rounds: int, gpu: int, fxp_
 def run_loopback(names: list[str], n: int, rounds: int = 1, *, seeds: dict | None = None, weights=None,
                  average: bool = False, gpu: int = 0, fxp_bits: int = 18, keep_masked: bool = False,
                  verify_digest: bool = False, timeout: float = 600.0, parties_per_process: int = 1,
-                 keep_results: bool = True):
+                 keep_results: bool = True, gpus: list[int] | None = None, server_gpu: int | None = None):
     """Spawn the client parties (``parties_per_process`` per OS process), run
     ``rounds`` rounds with this process as the server.  Returns (results per
     round, server timings, client stats, received masked vectors).
-    ``keep_results=False``: neither the server nor the clients keep each
-    round's result (results holds None per round); every client checksums
-    what it received either way (``stats[i][r]["result_xor"]``)."""
+    ``gpus``: client process g runs on ``gpus[g % len(gpus)]``, the server on
+    ``server_gpu`` (default ``gpus[0]``; ``placement``); without it every
+    party is on ``gpu``.  ``keep_results=False``: neither the server nor the
+    clients keep each round's result (results holds None per round); every
+    client checksums what it received either way
+    (``stats[i][r]["result_xor"]``)."""
     import multiprocessing as mp
 
     ctx = mp.get_context("spawn")
-    srv = LoopbackServer(len(names), gpu=gpu, fxp_bits=fxp_bits)
+    k = max(1, int(parties_per_process))
+    n_procs = -(-len(names) // k)
+    srv_gpu, proc_gpus = placement(n_procs, list(gpus) if gpus else [gpu], server_gpu)
+    srv = LoopbackServer(len(names), gpu=srv_gpu, fxp_bits=fxp_bits)
     q = ctx.Queue()
     procs = []
     specs = []
     for i, p in enumerate(names):
         ps = None if seeds is None else {v: seeds[p][v] for v in names if v != p}
         specs.append((p, i, ps, None if weights is None else weights[i]))
-    k = max(1, int(parties_per_process))
-    for g in range(0, len(specs), k):
-        pr = ctx.Process(target=client_process, args=(specs[g:g + k], srv.port, n, rounds, gpu, fxp_bits, q,
-                                                      keep_results))
+    for g in range(n_procs):
+        pr = ctx.Process(target=client_process, args=(specs[g * k:(g + 1) * k], srv.port, n, rounds, proc_gpus[g],
+                                                      fxp_bits, q, keep_results))
         pr.start()
         procs.append(pr)
     results, timings, masked = [], [], []
+    placed = {"server_gpu": srv_gpu, "client_process_gpus": proc_gpus, "parties_per_process": k}
     try:
         srv.accept(timeout=timeout)
         for r in range(rounds):
@@ -757,6 +811,7 @@ def run_loopback(names: list[str], n: int, rounds: int = 1, *, seeds: dict | Non
             out, t = srv.round(n, r, average=average, keep_masked=keep_masked, verify_digest=verify_digest,
                                copy_out=keep_results)
             t["t_start"] = t_start  # successive starts give the steady-state period (copy-out included)
+            t["placement"] = placed
             results.append(out if keep_results else None)
             timings.append(t)
             if keep_masked:

@@ -268,3 +268,17 @@ def test_injection_parser():
     finally:
         del os.environ["SFL_BENCH_INJECT"]
     assert not bench.injected("fail", "direct", 0)
+
+
+def test_design_with_a_different_result_is_flagged():
+    """Every design's round-0 result check must equal the headline's; one
+    that differs is marked (mismatch) and the line says designs_agree false."""
+    r = _dry(2, "corrupt:direct@1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    got = {v["name"]: v for v in line["exchange_variants"]}
+    assert "mismatch" in got["direct"] and "mismatch" not in got["reduce"]
+    assert line["designs_agree"] is False
+    r = _dry(2, "")
+    (line,) = _json_lines(r.stdout)
+    assert line["designs_agree"] is True and all("mismatch" not in v for v in line["exchange_variants"])

@@ -22,8 +22,34 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def oracle_check(C: int, n: int, fxp_bits: int = 18) -> str:
+    """bench.py's round-0 result check from the oracle: the bench's synthetic
+    inputs regenerated the same way (torch.Generator on the GPU), the masked
+    sum = sum of the quantized vectors (the pair masks cancel), decoded, and
+    the float64 bits XOR-ed."""
+    import numpy as np
+
+    from oracle import secagg as o
+
+    dev = torch.device("cuda", 0)
+    qs = []
+    for c in range(C):
+        g = torch.Generator(device=dev).manual_seed(20260116 + c)
+        x = (torch.randn(n, generator=g, device=dev, dtype=torch.float32) * 1e-2).cpu().numpy()
+        qs.append(o.quantize(x, None, fxp_bits))
+    dec = o.decode(o.server_sum(qs), fxp_bits)
+    return f"{int(np.bitwise_xor.reduce(dec.view(np.uint64))):016x}"
+
+
+@pytest.fixture(scope="module")
+def check_1m():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return oracle_check(8, 1000003)
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_bench_n_ranks_every_design(world):
+def test_bench_n_ranks_every_design(world, check_1m):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     env = dict(os.environ)
@@ -46,6 +72,9 @@ def test_bench_n_ranks_every_design(world):
     # the headline is the reduce-scatter sharded server, measured first
     assert line["n_gpus"] == world and "rehearsal" in line and line["config"]["design"] == "sharded"
     assert "exchange_probe" not in line and line["exchange_variants"][0]["name"] == "sharded"
+    # every design's round-0 result equals the oracle's (and so N = 1's)
+    assert line["check"]["decoded_xor"] == check_1m and line["designs_agree"] is True
+    assert all(v["check_xor"] == check_1m for v in line["exchange_variants"]), line["exchange_variants"]
     per = 8 // world
     assert line["config"]["clients_per_gpu"] == per
     assert line["roofline"]["kernel"].startswith(f"k_clients<float, float, {per}, {8 - per}, ")
@@ -60,7 +89,7 @@ def test_bench_n_ranks_every_design(world):
             assert v["xchg_ms"] > 0 and v["bytes_per_rank_per_step"] > 0
 
 
-def test_bench_n1_line():
+def test_bench_n1_line(check_1m):
     """The driver's N = 1 bench path at a small size: one JSON line with the
     contract's fields; one launch per step timed by one event pair around
     the timed region (kernel time <= wall time per step)."""
@@ -80,6 +109,7 @@ def test_bench_n1_line():
     assert rf["launches_per_step"] == 1 and rf["kernel_timing"].startswith("one HIP event pair")
     assert 0 < rf["kernel_ms_per_step"] <= d["ms_per_step"] * 1.01
     assert abs(d["value"] - 8 * 1000003 / (d["ms_per_step"] / 1e3)) < 1e-6 * d["value"]
+    assert d["check"]["decoded_xor"] == check_1m
 
 
 def _rehearse(world, inject, *extra, timeout=115):

@@ -122,3 +122,27 @@ def test_loopback_chunks_without_result_copies(monkeypatch, send):
         exp = o.secure_sum(xs, names, seeds=seeds, offset=r * n)[0]
         want = int(np.bitwise_xor.reduce(exp.view(np.uint64)))
         assert [stats[c][r]["result_xor"] for c in range(len(names))] == [want] * len(names), r
+
+
+def test_loopback_multi_gpu_placement_bit_exact():
+    """run_loopback(gpus=[0, 0]): the placement path of the 8-GPU node
+    (client process g on gpus[g % len(gpus)], the server on its own device
+    context) on the one GPU of this box; wire images and results bit-exact
+    vs the oracle, the placement recorded in the timings."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.loopback import run_loopback, synthetic_gradient
+
+    names = [f"g{i}" for i in range(4)]
+    n, rounds = 30_011, 2
+    seeds = o.seeds_for(names)
+    res, timings, stats, masked = run_loopback(names, n, rounds, seeds=seeds, keep_masked=True, verify_digest=True,
+                                               gpus=[0, 0], parties_per_process=1, timeout=300)
+    assert timings[0]["placement"] == {"server_gpu": 0, "client_process_gpus": [0, 0, 0, 0],
+                                       "parties_per_process": 1}
+    for r in range(rounds):
+        xs = [synthetic_gradient(c, n, r) for c in range(len(names))]
+        exp, _, m = o.secure_sum(xs, names, seeds=seeds, offset=r * n)
+        assert np.array_equal(res[r], exp), r
+        for c in range(len(names)):
+            assert np.array_equal(masked[r][c], m[c]), (r, c)

@@ -247,3 +247,9 @@ def test_bench_self_launched_dist_world1(opts):
     assert names[0] == want and len(names) == len(bench_variants())
     assert all(v["value"] > 0 and v["kernel_ms_per_step"] > 0 for v in line["exchange_variants"])
     assert line["roofline"]["kernel"].startswith("k_clients<float, float, 8, 0, 4>")
+    # every design (through RCCL at world 1) gives the oracle's round-0 result
+    from test_gpu_bench_rehearsal import oracle_check
+
+    want_check = oracle_check(8, 1000003)
+    assert line["designs_agree"] is True and line["check"]["decoded_xor"] == want_check
+    assert all(v["check_xor"] == want_check for v in line["exchange_variants"])

@@ -59,3 +59,42 @@ def test_send_ranges_through_a_full_socket_buffer(monkeypatch, send):
     assert bytes(got) == bytes(buf.array)
     buf.close()
     assert buf.fd == -1
+
+
+def test_placement_one_process_per_gpu():
+    """run_loopback(gpus=...): client process g on gpus[g % len(gpus)], the
+    server on server_gpu (default gpus[0]) -- config 3 (8 processes on 8
+    GPUs), config 5 (8 processes of 4 parties on 8 GPUs), the one-GPU boxes
+    (gpus=[0, 0]) and more processes than GPUs."""
+    assert lb.placement(8, list(range(8))) == (0, list(range(8)))
+    assert lb.placement(8, list(range(8)), server_gpu=7) == (7, list(range(8)))
+    assert lb.placement(3, [0, 0]) == (0, [0, 0, 0])
+    assert lb.placement(5, [2, 3]) == (2, [2, 3, 2, 3, 2])
+    assert lb.placement(0, [1]) == (1, [])
+    with pytest.raises(ValueError):
+        lb.placement(2, [])
+
+
+def test_submit_failure_releases_the_result_receiver(monkeypatch):
+    """a submit() that fails after its result-receiver thread
+    started ends that thread (the connection is shut down) and clears the
+    round in flight, so the failure is what the caller sees -- not a later
+    'previous round's result was not collected'."""
+    srv = socket.create_server(("127.0.0.1", 0))
+    cl = lb.LoopbackClient("alice", 0, srv.getsockname()[1])
+    peer, _ = srv.accept()
+
+    def boom(*a, **k):
+        raise RuntimeError("H2D failed")
+
+    monkeypatch.setattr(cl, "_mask_and_send", boom)
+    x = np.zeros(16, dtype=np.float32)
+    with pytest.raises(RuntimeError, match="H2D failed"):
+        cl.submit(x, 0, result_into=np.empty(16))
+    assert cl._rx is None
+    assert not [t for t in threading.enumerate() if getattr(t, "_target", None) == cl._receive_result]
+    with pytest.raises(RuntimeError, match="H2D failed"):  # the same error again, not 'not collected'
+        cl.submit(x, 1)
+    cl.close()
+    peer.close()
+    srv.close()

@@ -6,7 +6,13 @@ round moves each client's fp32 gradient H2D, masks it, moves the masked u64
 vector D2H, sends it over 127.0.0.1, and the server receives, H2D, sums,
 decodes and broadcasts the float64 result.
 
-usage: python tools/loopback_bench.py [--clients 8] [--elems 100000000] [--rounds 3]
+usage: python tools/loopback_bench.py [--clients 8] [--elems 100000000] [--rounds 3] [--gpus N]
+
+--gpus N places client process g on GPU g % N and the server on GPU 0
+(sfl_amd.loopback.placement): on the 8-GPU node config 3 is
+`--clients 8 --elems 100000000 --gpus 8` and config 5
+`--clients 32 --elems 256000000 --parties-per-process 4 --gpus 8`, so every
+GPU's PCIe link carries only its own parties' copies.
 """
 import argparse
 import json
@@ -32,6 +38,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--parties-per-process", type=int, default=1,
                     help="client parties hosted per OS process (config 5: 32 clients as 8 x 4)")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="client process g on GPU g %% N, the server on GPU 0 (one GPU: every party on GPU 0)")
     ap.add_argument("--ab", type=int, default=0,
                     help="A/B passes over the host-path knobs (SFL_LOOPBACK_SEND x SFL_LOOPBACK_WAIT), one line "
                          "per run")
@@ -55,7 +63,8 @@ def main():
 
     def one_run():
         res, timings, stats, _ = run_loopback(names, args.elems, args.rounds, seeds=seeds, timeout=900,
-                                              parties_per_process=args.parties_per_process, keep_results=False)
+                                              parties_per_process=args.parties_per_process, keep_results=False,
+                                              gpus=list(range(args.gpus)))
         # no server-side copy of the results: every client must have received the same bytes
         xors = [{s[r]["result_xor"] for s in stats.values()} for r in range(args.rounds)]
         if any(len(x) != 1 for x in xors):
@@ -77,7 +86,8 @@ def main():
             "period_s": period, "grad_elems_per_s": args.clients * args.elems / period,
             "round_s_median": rs,
             "server": {k: float(np.median([t[k] for t in steady])) for k in steady[0]
-                       if k not in ("t_start", "stages")},
+                       if k not in ("t_start", "stages", "placement")},
+            "placement": timings[0]["placement"], "gpus": args.gpus,
             # host-side profile (sfl_amd.loopback.StageClock): wall and thread-CPU
             # seconds per named copy / wait, summed over the threads that ran it,
             # median over the steady rounds (server) or over clients x rounds
