@@ -269,6 +269,40 @@ K_LEAN1, K_SUM_ONLY = 2, 4
 SUM_ONLY_SHAPES = {(2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (4, 4), (2, 6), (2, 2), (1, 1), (1, 3), (1, 7)}
 
 
+CROSS_COUNTS = (32, 24, 16, 8, 4, 2, 1)  # kCrossCounts (sfl_amd/csrc/sa_internal.h)
+K_CROSS_ONLY = 8
+
+
+def multi_launch_plan(L: int, X: int) -> tuple[int, list[int]] | None:
+    """sa_fused_clients' multi-launch schedule for a per-rank shape beyond one
+    launch (L <= 8 local clients, sum only): (X1, masks-only launch sizes) --
+    the first fused sum-only launch takes the internal pairs and the first X1
+    cross streams of every client (the largest X1 < X with a sum-only
+    instantiation and at most 32 streams), the rest go in launches of the
+    largest kCrossCounts that fits.  None when one launch holds the shape
+    (or none can: L > 8)."""
+    pi = L * (L - 1) // 2
+    if L > 8 or pi + L * X <= 32:
+        return None
+    x1 = next((x for x in range(X - 1, -1, -1) if pi + L * x <= 32 and (L, x) in SUM_ONLY_SHAPES), None)
+    if x1 is None:
+        return None
+    rest, sizes = L * (X - x1), []
+    while rest:
+        c = next(c for c in CROSS_COUNTS if c <= rest)
+        sizes.append(c)
+        rest -= c
+    return x1, sizes
+
+
+def multi_launch_text(L: int, X: int) -> str:
+    x1, sizes = multi_launch_plan(L, X)
+    return (f"pair-shared multi-launch schedule: k_clients<float,float,{L},{x1}> (the "
+            f"{L * (L - 1) // 2} internal pairs once + {L * x1} cross streams) then {len(sizes)} masks-only "
+            f"k_clients<float,float,1,X,{K_LEAN1 | K_SUM_ONLY | K_CROSS_ONLY}> launches (X = "
+            f"{'+'.join(str(c) for c in sizes)} cross streams) adding into the sum")
+
+
 def kernel_variant(L: int, X: int, digests: bool) -> int:
     lean = K_LEAN1 if L == 1 else 0
     if not digests and (L, X) in SUM_ONLY_SHAPES:
@@ -527,15 +561,19 @@ def workload(args, world: int, v: Variant) -> str:
                     f"k_clients<float,float,<=8,0> launches (the groups' clients and internal pairs) + "
                     f"{len(blocks)} k_clients<float,float,8,0,1> launches (two quads' cross pairs, "
                     f"sa_fused_bipartite), all adding into the sum")
+        if L <= 8 and not args.digests and multi_launch_plan(L, X):
+            return (f"{C} clients x {N} fp32 grad elems on 1 GPU, fxp {args.fxp_bits}, ring 2^64: "
+                    + multi_launch_text(L, X))
         if L > 8 or pairs + L * X > 32:  # beyond sa_fused_clients' shapes: client by client
             return (f"{C} clients x {N} fp32 grad elems on 1 GPU, fxp {args.fxp_bits}, ring 2^64: per-client "
                     f"sa_mask passes of <= 16 streams accumulating into the sum ({C - 1} streams per client, "
                     f"no pair sharing)")
         return (f"{C} clients x {N} fp32 grad elems on 1 GPU, fxp {args.fxp_bits}, ring 2^64: one fused launch "
                 f"k_clients<float,float,{L},{X}> ({pairs} pair streams)")
+    ml = multi_launch_plan(L, X) if not args.digests else None
     return (f"{C} clients x {N} fp32 grad elems over {world} GPUs, fxp {args.fxp_bits}, ring 2^64; per rank: "
             f"{L} local client(s), {pairs} internal pair + {L * X} cross streams "
-            f"(k_clients<float,float,{L},{X}>), pipelined " +
+            f"({multi_launch_text(L, X) if ml else f'k_clients<float,float,{L},{X}>'}), pipelined " +
             {"sharded": "ncclReduceScatter(uint64) of the partial sum, each rank decoding its shard (sharded server)",
              "direct": "direct shard transfers (ncclSend/Recv, uint64) of the partial sum, each rank summing "
                        "and decoding its shard (sharded server)",
@@ -1059,6 +1097,8 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     if not fused and Lc > 8 and plan.n_cross == 0 and not args.digests:  # kernels.fused_many
         kname = (f"pair-shared schedule for {Lc} local clients: k_clients<float, float, 8, 0, 1> "
                  f"(sa_fused_bipartite) + k_clients<float, float, <=8, 0> launches")
+    elif not fused and not args.digests and multi_launch_plan(Lc, plan.n_cross):
+        kname = multi_launch_text(Lc, plan.n_cross)
     elif not fused:  # sa_fused_clients masks client by client (sa_mask passes of <= 16 streams)
         kname = f"k_clients<float, float, 1, X<=16> per client and pass (fallback for {Lc} local clients)"
     res = {"name": v.name, "ms_per_step": ms, "value": C * N / (ms / 1e3), "steps": steps, "warmup": warmup,

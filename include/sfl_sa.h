@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SA_ABI_VERSION 1
+#define SA_ABI_VERSION 2
 
 /* status codes */
 #define SA_OK 0
@@ -142,11 +142,16 @@ int sa_mask(const void* x, int x_type, int compute_type, uint64_t n, double weig
  *   cross           n_clients * n_cross streams, client-major
  *   sum_out         n u64; accumulate != 0 means sum_out[i] += local sum
  *   digests         n_clients u64 (XOR-accumulated; zero them first)
- * Shapes without a fused kernel (more than 8 clients, more than 32 streams,
- * or an uninstantiated (C, n_cross)) return SA_ERR_UNSUPPORTED: the caller
- * then masks client by client with sa_mask(..., sum_accum), same result, or
- * -- more than 8 clients, only the sum wanted -- runs the pair-shared
- * schedule with sa_fused_bipartite below.
+ * More than 32 streams with only the sum wanted (no digests, no masked_out;
+ * float32; e.g. 32 clients, 4 per GPU: 6 pairs + 4 x 28 cross streams): a
+ * multi-launch schedule on the same stream -- one fused launch with the
+ * internal pairs (each still expanded once) and the first cross streams,
+ * then masks-only launches of the remaining cross streams into sum_out.
+ * Other shapes without a fused kernel (more than 8 clients, more than 32
+ * streams with digests or wire images, or an uninstantiated (C, n_cross))
+ * return SA_ERR_UNSUPPORTED: the caller then masks client by client with
+ * sa_mask(..., sum_accum), same result, or -- more than 8 clients, only
+ * the sum wanted -- runs the pair-shared schedule with sa_fused_bipartite.
  * Replaces: the client-side `mask` calls plus server `_sum`'s
  * np.sum(..., axis=0) for co-located parties. */
 int sa_fused_clients(const sa_local_client* clients, int n_clients, int x_type, uint64_t n,
@@ -224,8 +229,9 @@ int sa_xor_u64(const uint64_t* v, uint64_t n, uint64_t* digest, void* stream);
 /* sumsq_layer, min(1, clip / sqrt(||layer|| * ||all||)) per layer,     */
 /* is_clip_each_layer).  The noise is Philox4x32-10 + Box-Muller keyed   */
 /* by (key, element index), not numpy's unseeded global MT19937 stream:  */
-/* parity for the noise is distributional, for the clip exact up to the  */
-/* float32 rounding of the norm.                                         */
+/* parity for the noise is distributional; the clip follows the         */
+/* reference's float32 norm arithmetic (sa_sumsq_f32), up to its BLAS    */
+/* dot's float32 accumulation order.                                     */
 /* ------------------------------------------------------------------ */
 
 #define SA_DP_PARTIALS 1024 /* doubles of scratch for sa_sumsq_f32 */
@@ -241,8 +247,14 @@ typedef struct sa_dp {
   uint64_t counter0; /* noise index of element 0 (multiple of 4) */
 } sa_dp;
 
-/* *sumsq (+)= sum x[i]^2 in float64, deterministic fixed-order reduction;
- * `partials` is caller scratch of SA_DP_PARTIALS doubles. */
+/* *sumsq (+)= this layer's squared L2 norm as the reference forms it
+ * (mechanism_fl.py:132-135 on float32 arrays): sum x[i]^2 by a
+ * deterministic fixed-order float64 reduction, rounded to float32, then
+ * np.linalg.norm's float32 sqrt and ** 2 in float32; accumulating layers add
+ * in float32 (the reference's python sum), the float32 value held in the
+ * double.  (The reference's float32 BLAS dot accumulates in float32; here
+ * the dot is exact to float64 before its one rounding -- DESIGN.md §4.)
+ * `partials` is caller scratch of SA_DP_PARTIALS doubles.  ABI version 2. */
 int sa_sumsq_f32(const float* x, uint64_t n, double* partials, double* sumsq, int accumulate, void* stream);
 
 /* out = clip-and-noise(x) (out may alias x). */

@@ -3,9 +3,13 @@ checker for tests/ and bench.py's baseline; the product path never imports
 it).
 
 * GaussianModelDP clip formula: sfl/security/privacy/mechanism/mechanism_fl.py
-  :71 (global norm), :81-84 (per-layer scale), :107-110 (global scale),
-  :112-127 (noise / num_updates, np.add), float32 throughout as numpy
-  evaluates it for float32 inputs.
+  :71 (global norm), :81-84 (per-layer scale), :104-108 (global scale),
+  :112-127 (noise / num_updates, np.add), :132-135 (global_norm: float32
+  np.linalg.norm per layer, ** 2, python sum, np.sqrt), with numpy 1.23.5's
+  scalar promotion (the reference's pin, uv.lock:1189-1190).  One deviation:
+  the layer's dot is the exact float64 sum rounded once to float32, where
+  the reference's BLAS sdot accumulates in float32 in its own order
+  (|difference| <= n * 2^-24 of the dot in the worst case).
 * Philox4x32-10: Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as
   easy as 1, 2, 3" (SC'11), Random123 constants; pinned by the published
   known-answer vectors in tests/test_dp_oracle.py.
@@ -56,15 +60,40 @@ def gauss(key: int, counter0: int, n: int) -> np.ndarray:
     return z.reshape(-1)[off:off + n]
 
 
-def clip_scale(sumsq: float, clip: float, sumsq_layer=None) -> np.float32:
-    """min(1, clip / norm) in float32 (norm from the float64 sum of squares)."""
-    norm_all = np.float32(np.sqrt(sumsq))
+def layer_sq_norm(a) -> np.float32:
+    """One layer's ``np.linalg.norm(a) ** 2`` as the reference evaluates it on
+    a float32 array (mechanism_fl.py:133, numpy 1.23.5): the float32 dot --
+    here the exact float64 sum rounded once (the reference's BLAS sdot adds
+    in float32 in its own order) -- np.sqrt in float32, then
+    ``** 2`` in float32."""
+    dot = np.float32(np.sum(np.asarray(a, dtype=np.float64).reshape(-1) ** 2))
+    norm = np.sqrt(dot, dtype=np.float32)
+    return np.float32(norm * norm)
+
+
+def global_sq(inputs) -> np.float32:
+    """``sum([np.linalg.norm(i) ** 2 for i in inputs])``: python's sum from 0
+    over float32 scalars stays float32 (mechanism_fl.py:133)."""
+    t = np.float32(0)
+    for a in inputs:
+        t = np.float32(t + layer_sq_norm(a))
+    return t
+
+
+def clip_scale(sumsq, clip: float, sumsq_layer=None) -> np.float32:
+    """min(1, clip / norm) as mechanism_fl.py:71-84,104-108 computes it under
+    numpy 1.23.5: ``sumsq`` / ``sumsq_layer`` the float32 squared norms
+    (global_sq, layer_sq_norm); norm = np.sqrt in float32; the per-layer
+    denominator np.sqrt(layer_norm * norm) in float32; a python-float clip
+    divided by a float32 scalar is a float64 division (value-based casting
+    of two scalars); multiplying the float32 array rounds it to float32."""
+    norm_all = np.sqrt(np.float32(sumsq), dtype=np.float32)
     denom = norm_all
     if sumsq_layer is not None:
-        denom = np.sqrt(np.float32(np.sqrt(sumsq_layer)) * norm_all)
+        denom = np.sqrt(np.float32(np.sqrt(np.float32(sumsq_layer), dtype=np.float32) * norm_all), dtype=np.float32)
     with np.errstate(divide="ignore", invalid="ignore"):
-        r = np.float32(clip) / denom
-    return r if r < np.float32(1) else np.float32(1)
+        r = np.float64(np.float32(clip)) / np.float64(denom)
+    return np.float32(r) if r < 1.0 else np.float32(1)
 
 
 def perturb(x: np.ndarray, scale, z: np.ndarray, sigma: float, num_updates: float) -> np.ndarray:
@@ -78,11 +107,11 @@ def gaussian_model_dp(inputs, noise_multiplier, num_updates, l2_norm_clip=1.0, k
                       is_clip_each_layer=False):
     """Restated GaussianModelDP.__call__ with this build's noise stream."""
     sigma = noise_multiplier * l2_norm_clip * l2_norm_clip
-    total = sum(float(np.sum(np.asarray(a, dtype=np.float64) ** 2)) for a in inputs)
+    total = global_sq(inputs)
     out, ctr = [], counter0
     for a in inputs:
         a = np.asarray(a, dtype=np.float32)
-        lay = float(np.sum(a.astype(np.float64) ** 2)) if is_clip_each_layer else None
+        lay = layer_sq_norm(a) if is_clip_each_layer else None
         s = clip_scale(total, l2_norm_clip, lay)
         z = gauss(key, ctr, a.size)
         out.append(perturb(a.reshape(-1), s, z, sigma, num_updates).reshape(a.shape))

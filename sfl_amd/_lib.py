@@ -24,6 +24,7 @@ SA_F32, SA_F64, SA_I64 = 0, 1, 2
 SA_FLAG_PRG_REJECT = 1
 SA_UNIQUE_ID_BYTES = 128
 SA_DP_PARTIALS = 1024
+ABI_VERSION = 2  # include/sfl_sa.h SA_ABI_VERSION (2: sa_sumsq_f32 forms the reference's float32 norm)
 TUNING_ABI_OFFSET = 1000  # sa_abi_version() of an SA_ABLATE / SA_TIMING build
 
 # every symbol include/sfl_sa.h declares (checked by tests/test_boundary.py)
@@ -140,9 +141,9 @@ def lib():
                 raise SALibraryError(_load_error) from e
             _declare(handle)
             ver = handle.sa_abi_version()
-            if ver == 1 + TUNING_ABI_OFFSET and os.environ.get("SFL_SA_ALLOW_TUNING_BUILD") == "1":
+            if ver == ABI_VERSION + TUNING_ABI_OFFSET and os.environ.get("SFL_SA_ALLOW_TUNING_BUILD") == "1":
                 pass  # tools/ timing a tuning variant on purpose (never the product)
-            elif ver != 1:
+            elif ver != ABI_VERSION:
                 raise SALibraryError(
                     f"{LIB_PATH}: ABI version {ver}" + (" (a tuning build: SA_ABLATE / SA_TIMING; results of "
                                                         "ablation builds are wrong)" if ver > TUNING_ABI_OFFSET

@@ -313,6 +313,52 @@ int sa_mask_impl(const void* x, int x_type, int compute_type, uint64_t n, double
   return SA_OK;
 }
 
+// One masks-only launch: sum_out += sum over the cnt streams of +-(raw + K)
+// mod 2^64 (the kCrossOnly kernel: no input vector, nothing quantized).
+static int launch_cross_group(const sa_mask_stream* ms, int cnt, uint64_t n, uint64_t* sum_out, uint32_t* flags,
+                              void* stream) {
+  KArgs a;
+  memset(&a, 0, sizeof(a));
+  a.n = n;
+  a.scale_d = 1.0;
+  a.scale_f = 1.0f;
+  uint64_t bias = 0;
+  for (int j = 0; j < cnt; j++) {
+    fill_stream(a.s[j], ms[j].gen, ms[j].sign);
+    bias += ms[j].sign > 0 ? fold_plus() : fold_minus();
+  }
+  a.c[0].x = nullptr;  // never read: the kCrossOnly kernel loads no input
+  a.c[0].bias = bias;
+  a.sum_out = sum_out;
+  a.sum_mode = 2;
+  a.flags = flags;
+  const LaunchFn fn = find_clients_kernel(SA_F32, SA_F32, 1, cnt, kLean1 | kSumOnly | kCrossOnly);
+  if (!fn) {
+    sa_set_error("masks-only launch: no kernel for %d streams", cnt);
+    return SA_ERR_UNSUPPORTED;
+  }
+  return fn(a, stream);
+}
+
+// sum_out += the masks of `count` one-sided streams, in launches of the
+// largest instantiated count (kCrossCounts) that fits the remaining streams.
+static int launch_cross(const sa_mask_stream* ms, int count, uint64_t n, uint64_t* sum_out, uint32_t* flags,
+                        void* stream) {
+  for (int j = 0; j < count;) {
+    const int r = count - j;
+    int cnt = 1;
+    for (int c : kCrossCounts)
+      if (c <= r) {
+        cnt = c;
+        break;
+      }
+    const int rc = launch_cross_group(ms + j, cnt, n, sum_out, flags, stream);
+    if (rc) return rc;
+    j += cnt;
+  }
+  return SA_OK;
+}
+
 extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, int x_type,
                                 uint64_t n, int fxp_bits, const sa_pcg64* pair_gens,
                                 const int8_t* pair_sign, const sa_mask_stream* cross,
@@ -332,9 +378,45 @@ extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, i
     return SA_ERR_UNSUPPORTED;
   }
   if (PI + L * n_cross > kMaxStreams) {
-    sa_set_error("sa_fused_clients: %d streams exceed the %d per launch", PI + L * n_cross,
-                 kMaxStreams);
-    return SA_ERR_UNSUPPORTED;
+    // More streams than one launch holds (config 5 at 8 GPUs: 4 local clients,
+    // 6 internal pairs + 4 x 28 cross streams).  With only the sum wanted, a
+    // multi-launch schedule that still draws every internal pair ONCE: a
+    // fused sum-only launch with the pairs and the first X1 cross streams of
+    // every client, then masks-only launches of the remaining cross streams
+    // adding into the sum (their per-client split does not matter there).
+    bool any_out = digests != nullptr;
+    for (int c = 0; c < L; c++) any_out = any_out || clients[c].masked_out != nullptr;
+    int X1 = -1;
+    if (!any_out && x_type == SA_F32)
+      for (int x = n_cross - 1; x >= 0 && X1 < 0; x--)
+        if (PI + L * x <= kMaxStreams && find_clients_kernel(x_type, x_type, L, x, (L == 1 ? kLean1 : 0) | kSumOnly))
+          X1 = x;
+    if (X1 < 0) {  // digests / wire images wanted, or no first launch: the caller masks client by client
+      sa_set_error("sa_fused_clients: %d streams exceed the %d per launch", PI + L * n_cross, kMaxStreams);
+      return SA_ERR_UNSUPPORTED;
+    }
+    for (int j = 0; j < L * n_cross; j++)
+      if (cross[j].sign != 1 && cross[j].sign != -1) {
+        sa_set_error("sa_fused_clients: cross stream %d sign %d", j, cross[j].sign);
+        return SA_ERR_ARG;
+      }
+    sa_mask_stream first[kMaxStreams], rest[kMaxLocal * (kMaxStreams + 1)];
+    if (L * (n_cross - X1) > (int)(sizeof(rest) / sizeof(rest[0]))) {
+      sa_set_error("sa_fused_clients: %d cross streams per client exceed the multi-launch schedule", n_cross);
+      return SA_ERR_UNSUPPORTED;
+    }
+    int nr = 0;
+    for (int c = 0; c < L; c++)
+      for (int j = 0; j < n_cross; j++) {
+        if (j < X1)
+          first[c * X1 + j] = cross[c * n_cross + j];
+        else
+          rest[nr++] = cross[c * n_cross + j];
+      }
+    const int rc = sa_fused_clients(clients, L, x_type, n, fxp_bits, pair_gens, pair_sign, first, X1, sum_out,
+                                    accumulate, nullptr, flags, stream);
+    if (rc) return rc;
+    return n == 0 ? SA_OK : launch_cross(rest, nr, n, sum_out, flags, stream);
   }
   if (!aligned16(sum_out)) {
     sa_set_error("sa_fused_clients: sum_out must be 16-byte aligned");

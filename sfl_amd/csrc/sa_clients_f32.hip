@@ -12,6 +12,7 @@ LaunchFn find_other_kernel(int xt, int ct, int L, int X);
 #define F32(L, X) SA_ENTRY(float, float, SA_F32, SA_F32, L, X)
 #define L1(X) SA_ENTRY_K(float, float, SA_F32, SA_F32, 1, X, kLean1)
 #define SO(L, X) SA_ENTRY_K(float, float, SA_F32, SA_F32, L, X, kSumOnly)
+#define XO(X) SA_ENTRY_K(float, float, SA_F32, SA_F32, 1, X, kLean1 | kSumOnly | kCrossOnly)
 LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K) {
   static const KernelEntry kEntriesF32[] = {
     F32(1, 0),  F32(1, 1),  F32(1, 2),  F32(1, 3),  F32(1, 4),  F32(1, 5),  F32(1, 6),
@@ -30,6 +31,10 @@ LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K) {
     SA_ENTRY_K(float, float, SA_F32, SA_F32, 1, 1, kLean1 | kSumOnly),
     SA_ENTRY_K(float, float, SA_F32, SA_F32, 1, 3, kLean1 | kSumOnly),
     SA_ENTRY_K(float, float, SA_F32, SA_F32, 1, 7, kLean1 | kSumOnly),
+    // masks only, one accumulator of one-sided streams added into the sum:
+    // the later launches of sa_fused_clients' multi-launch schedule
+    // (kCrossCounts)
+    XO(1), XO(2), XO(4), XO(8), XO(16), XO(24), XO(32),
     // one client without the general paths (continue, weight vectors, DP)
     L1(0), L1(1), L1(2), L1(3), L1(4), L1(5), L1(6), L1(7), L1(8), L1(9), L1(10), L1(11), L1(12),
     L1(13), L1(14), L1(15), L1(16),
@@ -41,6 +46,7 @@ LaunchFn find_clients_kernel(int xt, int ct, int L, int X, int K) {
 #undef F32
 #undef L1
 #undef SO
+#undef XO
 
 }  // namespace sa
 

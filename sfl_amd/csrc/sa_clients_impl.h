@@ -591,7 +591,10 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
   constexpr bool kGeneral = (L == 1) && !(K & kLean1);
   // only the masked sum leaves the launch (no digests, no wire images): the
   // finish and epilogue carry no digest / store code at all
-  constexpr bool kSum = (K & (kSumOnly | kBipartite)) != 0;
+  constexpr bool kSum = (K & (kSumOnly | kBipartite | kCrossOnly)) != 0;
+  // cross streams only, masks only: one accumulator, nothing loaded
+  constexpr bool kCross = (K & kCrossOnly) != 0;
+  static_assert(!kCross || (L == 1 && !kGeneral), "kCrossOnly: one lean accumulator");
   static_assert(L >= 1 && L <= kMaxLocal, "L");
   static_assert(P <= kMaxStreams, "P");
 
@@ -710,7 +713,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
         if (SA_ABLATE & 8) {
 #pragma unroll
           for (int k = 0; k < kE; k++) xv[c].v[k] = (XT)(int)(i + k + c);
-        } else if constexpr ((K & kBipartite) != 0) {  // masks only: the clients' values enter elsewhere
+        } else if constexpr ((K & (kBipartite | kCrossOnly)) != 0) {  // masks only: the values enter elsewhere
           xv[c].v[0] = xv[c].v[1] = (XT)0;
         } else {
           xv[c] = bload2<XT>(make_rsrc(ka->c[c].x, cont ? 0 : n * sizeof(XT)), i);
@@ -854,7 +857,11 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
     };
     static_assert(kE == 2, "finish() takes the lane's two elements");
     float p[L][kE];
-    if constexpr ((K & kBipartite) != 0) {
+    if constexpr (kCross) {
+      // masks only (sa_fused_clients' later launches): the one accumulator
+#pragma unroll
+      for (int k = 0; k < kE; k++) sum[k] = acc[k][0];
+    } else if constexpr ((K & kBipartite) != 0) {
       // masks only (sa_fused_bipartite): the sum of the 8 accumulators, the
       // upper quad's stored negated
 #pragma unroll

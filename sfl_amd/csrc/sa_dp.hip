@@ -35,13 +35,21 @@ __global__ void __launch_bounds__(256) k_sumsq_partial(const float* __restrict__
   if (threadIdx.x == 0) partials[blockIdx.x] = (w[0] + w[1]) + (w[2] + w[3]);
 }
 
-// fixed-order sum of the partials (deterministic) -> *out (or += *out)
+// fixed-order sum of the partials (deterministic), then the layer's squared
+// norm as the reference forms it in float32 (mechanism_fl.py:132-135,
+// numpy 1.23.5 on float32 arrays): np.linalg.norm -> sqrt(float32 x.x), ** 2
+// in float32, and the layers' values summed in float32 (python sum from 0)
+// -> *out (or += *out in float32), a float32 value held in a double
 __global__ void __launch_bounds__(64) k_sumsq_final(const double* __restrict__ partials, int k, double* out,
                                                     int accumulate) {
   double acc = 0.0;
   for (int j = threadIdx.x; j < k; j += 64) acc += partials[j];
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  if (threadIdx.x == 0) *out = accumulate ? *out + acc : acc;
+  if (threadIdx.x == 0) {
+    const float norm = __fsqrt_rn((float)acc);  // np.linalg.norm: float32 dot, float32 sqrt
+    const float sq = __fmul_rn(norm, norm);      // ** 2
+    *out = accumulate ? (double)__fadd_rn((float)*out, sq) : (double)sq;
+  }
 }
 
 struct DpArgs {

@@ -44,6 +44,16 @@ constexpr int kLean1 = 2;
 // launch -1.25 % in A/B (profiles/r02/ab_sum_only_kernel_kb.jsonl).  Flags
 // combine (kLean1 | kSumOnly); kBipartite launches are masks-only sums.
 constexpr int kSumOnly = 4;
+// kCrossOnly: one accumulator (L = 1) of one-sided streams, masks only (no
+// input loads, no quantize), added into the sum: the later launches of a
+// per-rank shape with more streams than one launch holds (sa_fused_clients'
+// multi-launch schedule, e.g. 4 local clients + 28 cross streams each at 32
+// clients over 8 GPUs).  Used as kLean1 | kSumOnly | kCrossOnly.
+constexpr int kCrossOnly = 8;
+// the stream counts instantiated for kCrossOnly (sa_clients_f32.hip), largest
+// first: a schedule takes the largest that fits its remaining streams, so any
+// count is covered (the per-rank shapes of the benches by the first three)
+constexpr int kCrossCounts[] = {32, 24, 16, 8, 4, 2, 1};
 
 
 // Kernel-argument image (lives in the kernarg segment; read with scalar loads).

@@ -111,12 +111,18 @@ __device__ __forceinline__ float dp_apply(float x, float scale, float z, float s
 
 // scale = min(1, clip / norm) in float32 (mechanism_fl.py:107); with a layer
 // sum of squares, min(1, clip / sqrt(norm_layer * norm_all)) (:81-84).
+// The clip scale as GaussianModelDP computes it under the reference's numpy
+// 1.23.5 (mechanism_fl.py:71-84,104-108,132-135), from sa_sumsq_f32's float32
+// squared norms: norm = np.sqrt(float32 sum) in float32; the per-layer
+// denominator np.sqrt(layer_norm * norm) in float32; clip / denom with a
+// python-float clip is a float64 division (value-based casting of two
+// scalars); the float32 array times that float64 scalar rounds it to float32.
 __device__ __forceinline__ float dp_scale(const double* sumsq, const double* sumsq_layer, float clip) {
-  const float norm_all = (float)sqrt(*sumsq);
+  const float norm_all = __fsqrt_rn((float)*sumsq);
   float denom = norm_all;
-  if (sumsq_layer) denom = sqrtf(__fmul_rn((float)sqrt(*sumsq_layer), norm_all));
-  const float r = __fdiv_rn(clip, denom);
-  return r < 1.0f ? r : 1.0f;
+  if (sumsq_layer) denom = __fsqrt_rn(__fmul_rn(__fsqrt_rn((float)*sumsq_layer), norm_all));
+  const double r = __ddiv_rn((double)clip, (double)denom);
+  return r < 1.0 ? (float)r : 1.0f;
 }
 #endif
 

@@ -282,3 +282,44 @@ def test_design_with_a_different_result_is_flagged():
     r = _dry(2, "")
     (line,) = _json_lines(r.stdout)
     assert line["designs_agree"] is True and all("mismatch" not in v for v in line["exchange_variants"])
+
+
+def test_multi_launch_plan_names_config5_schedule():
+    """Per-rank shapes beyond one launch (sum only): the first launch takes
+    the internal pairs + X1 cross streams per client, masks-only launches of
+    kCrossCounts the rest -- every cross stream exactly once; config 5 at 8
+    GPUs is <4,4> + 3 x 32, and --clients 32 --gpus 8 names it."""
+    import bench
+
+    assert bench.multi_launch_plan(4, 28) == (4, [32, 32, 32])
+    assert bench.multi_launch_plan(8, 24) == (0, [32] * 6)
+    assert bench.multi_launch_plan(4, 4) is None and bench.multi_launch_plan(16, 16) is None
+    for L in range(1, 9):
+        for X in range(0, 60):
+            p = bench.multi_launch_plan(L, X)
+            if p is None:
+                continue
+            x1, sizes = p
+            pi = L * (L - 1) // 2
+            assert pi + L * x1 <= 32 and (L, x1) in bench.SUM_ONLY_SHAPES
+            assert sum(sizes) == L * (X - x1) and all(c in bench.CROSS_COUNTS for c in sizes)
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--dry-run", "--cpu-baseline-seconds", "0",
+                        "--clients", "32", "--elems", "1000", "--steps", "1", "--warmup", "0", "--variants", "none"],
+                       capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    assert "pair-shared multi-launch schedule: k_clients<float,float,4,4>" in line["config"]["workload"]
+    assert "X = 32+32+32" in line["config"]["workload"]
+
+
+def test_cross_only_counts_match_the_registry():
+    """bench.CROSS_COUNTS mirrors kCrossCounts, and every count is instantiated."""
+    import re
+
+    import bench
+
+    hdr = open(os.path.join(ROOT, "sfl_amd", "csrc", "sa_internal.h")).read()
+    counts = tuple(int(v) for v in re.search(r"kCrossCounts\[\] = \{([^}]*)\}", hdr).group(1).split(","))
+    assert counts == bench.CROSS_COUNTS
+    src = open(os.path.join(ROOT, "sfl_amd", "csrc", "sa_clients_f32.hip")).read()
+    assert {int(v) for v in re.findall(r"\bXO\((\d+)\)", src)} == set(counts)

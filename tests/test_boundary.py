@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(declared) == set(L.EXPORTED)
-    assert lib.sa_abi_version() == 1
+    assert lib.sa_abi_version() == 2
 
 
 def test_library_is_built_for_gfx950():
@@ -168,7 +168,8 @@ def test_tuning_builds_report_a_refused_abi_version(tmp_path):
     from sfl_amd import _lib as L
 
     src = os.path.join(ROOT, "sfl_amd", "csrc", "sa_host.cpp")
-    for define, want in (("", 1), ("-DSA_ABLATE=8", 1 + L.TUNING_ABI_OFFSET), ("-DSA_TIMING", 1 + L.TUNING_ABI_OFFSET)):
+    for define, want in (("", L.ABI_VERSION), ("-DSA_ABLATE=8", L.ABI_VERSION + L.TUNING_ABI_OFFSET),
+                         ("-DSA_TIMING", L.ABI_VERSION + L.TUNING_ABI_OFFSET)):
         so = tmp_path / f"host{abs(hash(define))}.so"
         cmd = ["g++", "-std=c++17", "-shared", "-fPIC", "-O1", src, "-o", str(so)] + ([define] if define else [])
         subprocess.run(cmd, check=True, capture_output=True)

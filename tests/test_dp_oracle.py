@@ -45,3 +45,34 @@ def test_clip_formula_matches_reference_expression():
         nl = np.float32(np.linalg.norm(a.astype(np.float64)))
         s = np.float32(min(1.0, np.float32(0.5) / np.sqrt(nl * np.float32(norm))))
         assert np.allclose(b, a * s, rtol=2e-7, atol=0)
+
+
+@pytest.mark.parametrize("each_layer", [False, True])
+def test_clip_restatement_vs_numpy_reference_arithmetic(each_layer):
+    """oracle.dp's clip (the device's arithmetic) against mechanism_fl.py:
+    71-108,132-135 evaluated by numpy itself (noise 0): equal up to the
+    reference's float32 BLAS dot error, measured here, plus 4 ulps; the
+    float32 structure of the norm (per-layer float32 norm, ** 2, float32
+    sum) is what the oracle restates."""
+    rng = np.random.default_rng(4)
+    layers = [(rng.standard_normal(s) * 0.05).astype(np.float32) for s in ((64, 50), (50,), (50, 3), (3,))]
+
+    def gnorm(arrs):
+        return np.sqrt(sum([np.linalg.norm(a) ** 2 for a in arrs]))
+
+    norm_all = gnorm(layers)
+    if each_layer:
+        ref = [a * min(1, 0.5 / np.sqrt(gnorm([a]) * norm_all)) for a in layers]
+    else:
+        ref = [a * min(1, 0.5 / norm_all) for a in layers]
+    got = D.gaussian_model_dp(layers, 0.0, 8, 0.5, is_clip_each_layer=each_layer)
+    exact = [np.sqrt(np.sum(a.astype(np.float64) ** 2)) for a in layers]
+    rel = max(abs(float(np.linalg.norm(a)) - e) / e for a, e in zip(layers, exact))
+    for g, r in zip(got, ref):
+        np.testing.assert_allclose(g, r, rtol=2 * rel + 4 * 2.0**-24, atol=0)
+    # the float32 structure: the squared global norm is a float32 sum of float32 squares
+    t = np.float32(0)
+    for a in layers:
+        t = t + D.layer_sq_norm(a)
+        assert t.dtype == np.float32
+    assert D.global_sq(layers) == t

@@ -34,12 +34,22 @@ def _sumsq(x):
 
 @pytest.mark.parametrize("n", [1, 3, 4, 1027, 1_000_003])
 def test_sumsq_deterministic_and_accurate(n):
+    """sa_sumsq_f32 = the layer's np.linalg.norm(x) ** 2 in float32 as the
+    reference forms it (oracle layer_sq_norm), deterministic; accumulating
+    two layers adds in float32 (the reference's python sum)."""
     x = torch.randn(n, device=DEV)
     a, b = _sumsq(x), _sumsq(x)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
-    ref = float(np.sum(x.cpu().numpy().astype(np.float64) ** 2))
-    assert abs(a.item() - ref) <= 1e-12 * ref
+    xh = x.cpu().numpy()
+    assert a.item() == float(D.layer_sq_norm(xh))
+    assert np.float32(a.item()) == a.item()  # a float32 value
+    from sfl_amd import _lib as L
+
+    part = torch.empty(L.SA_DP_PARTIALS, dtype=torch.float64, device=DEV)
+    y = torch.randn(n + 5, device=DEV)
+    _K().sumsq_f32(y, a, part, accumulate=True)
+    assert a.item() == float(D.global_sq([xh, y.cpu().numpy()]))
 
 
 @pytest.mark.parametrize("clip", [0.5, 1e6])
@@ -120,6 +130,55 @@ def test_gaussian_model_dp_class_vs_oracle(each_layer):
     exp0 = D.gaussian_model_dp(layers, 0.0, 8, 2.0)
     for g, e in zip(got0, exp0):
         assert np.array_equal(g, e)
+
+
+def _reference_clip_numpy(inputs, clip, each_layer):
+    """mechanism_fl.py:71-108 with noise_multiplier = 0, restated on numpy's
+    own float32 arithmetic (np.linalg.norm per layer, ** 2, python sum,
+    np.sqrt, min(1, clip / norm), the float32 array times the scale).  Runs
+    under this image's numpy 2 (NEP 50: clip / float32 divides in float32,
+    where the reference's numpy 1.23.5 divides in float64 -- within one ulp
+    of the scale)."""
+    def gnorm(arrs):
+        return np.sqrt(sum([np.linalg.norm(a) ** 2 for a in arrs]))
+
+    norm_all = gnorm(inputs)
+    if each_layer:
+        return [a * min(1, clip / np.sqrt(gnorm([a]) * norm_all)) for a in inputs]
+    scale = min(1, clip / norm_all)
+    return [a * scale for a in inputs]
+
+
+@pytest.mark.parametrize("each_layer", [False, True])
+@pytest.mark.parametrize("clip", [0.5, 1e6])
+def test_gaussian_model_dp_vs_reference_numpy_clip(each_layer, clip):
+    """GaussianModelDP with noise_multiplier = 0 against
+    the reference's clip evaluated by numpy itself.  The device forms the
+    norm with the reference's float32 structure (sa_sumsq_f32); what is left
+    is the reference's BLAS float32 dot, whose accumulation error the test
+    measures (|np.linalg.norm - exact| / exact) and allows, plus 4 ulps of
+    float32 for the scale's division and the product.  With no clipping
+    (clip 1e6: scale 1) the output is the input bit for bit."""
+    from sfl_amd.security.privacy import GaussianModelDP
+
+    rng = np.random.default_rng(17)
+    layers = [(rng.standard_normal(s) * 0.05).astype(np.float32) for s in ((300, 200), (200,), (200, 10), (10,))]
+    layers.append((rng.standard_normal(1_000_003) * 0.01).astype(np.float32))
+    dp = GaussianModelDP(noise_multiplier=0.0, num_clients=8, l2_norm_clip=clip, is_clip_each_layer=each_layer,
+                         seed=3)
+    got = dp(layers)
+    ref = _reference_clip_numpy(layers, clip, each_layer)
+    exact = [np.sqrt(np.sum(a.astype(np.float64) ** 2)) for a in layers]
+    blas_rel = max(abs(float(np.linalg.norm(a)) - e) / e for a, e in zip(layers, exact))
+    tot_exact = np.sqrt(sum(e * e for e in exact))
+    blas_rel = max(blas_rel, abs(float(np.sqrt(sum([np.linalg.norm(a) ** 2 for a in layers]))) - tot_exact) / tot_exact)
+    tol = 2 * blas_rel + 4 * 2.0**-24
+    for g, r, a in zip(got, ref, layers):
+        assert g.dtype == np.float32 and r.dtype == np.float32
+        if clip == 1e6:
+            assert np.array_equal(g, a) and np.array_equal(r, a)
+        else:
+            np.testing.assert_allclose(g, r, rtol=tol, atol=0)
 
 
 def test_loopback_client_dp_round_vs_oracle():

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--bipartite", action="store_true",
                     help="also time one sa_fused_bipartite launch (16 cross pairs of two quads, masks only, "
                          "accumulating into the sum: 16 B of HBM traffic per element)")
+    ap.add_argument("--fallback", action="store_true",
+                    help="also time the per-client path (two sa_mask passes per client, accumulating into the "
+                         "sum) for every shape beyond one fused launch, interleaved with its multi-launch schedule")
     ap.add_argument("--calib", type=int, default=0,
                     help="also launch sa_sum_u64 over this many u64 inputs (known bytes, for PMC calibration)")
     args = ap.parse_args()
@@ -49,12 +52,18 @@ def main():
         pg, ps, cross = plan_generators(plan, pair_seed)
         s = torch.empty(N, dtype=torch.int64, device=dev)
         cases.append(dict(C=C, W=W, L=len(plan.clients), plan=plan, xs=xs, pg=pg, ps=ps, cross=cross, s=s,
-                          times=[]))
+                          times=[], path="fused"))
+        if args.fallback and len(plan.pairs) + len(plan.cross) > 32:
+            cases.append(dict(cases[-1], times=[], path="per-client fallback"))
     for _ in range(args.rounds):
         for cs in cases:
             def run():
-                K.fused_clients(cs["xs"], [1.0] * cs["L"], cs["pg"], cs["ps"], cs["cross"], cs["plan"].n_cross,
-                                cs["s"])
+                fn = K.fused_clients if cs["path"] == "fused" else K._fused_fallback
+                if fn is K.fused_clients:
+                    fn(cs["xs"], [1.0] * cs["L"], cs["pg"], cs["ps"], cs["cross"], cs["plan"].n_cross, cs["s"])
+                else:
+                    fn(cs["xs"], [1.0] * cs["L"], cs["pg"], cs["ps"], cs["cross"], cs["plan"].n_cross, cs["s"], 18,
+                       False, None, None, None)
             run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -104,7 +113,7 @@ def main():
         t = sorted(cs["times"])
         ms = t[len(t) // 2]
         draws = (len(cs["plan"].pairs) + len(cs["plan"].cross)) * N
-        out.append({"C": cs["C"], "W": cs["W"], "L": cs["L"], "ms_median": ms, "ms_min": t[0],
+        out.append({"C": cs["C"], "W": cs["W"], "L": cs["L"], "path": cs["path"], "ms_median": ms, "ms_min": t[0],
                     "draws_per_s": draws / (ms / 1e3), "local_grad_elems_per_s": cs["L"] * N / (ms / 1e3),
                     "hbm_GBps": (4 * cs["L"] * N + 8 * N) / (ms / 1e3) / 1e9})
     res = {"lib": os.environ.get("SFL_SA_LIB", "default"), "elems": N, "cases": out}
