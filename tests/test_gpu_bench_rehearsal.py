@@ -5,7 +5,7 @@ self-launcher, W torchrun ranks, every design's code path in run_design
 to rank 0, element sharding with and without the gather) and the max-over-
 ranks timing, with the collectives through gloo host round trips because
 RCCL refuses two ranks on one GPU ("Duplicate GPU detected",
-tools/debug/rccl_two_ranks_one_gpu.py).  RCCL itself runs at world 1 in
+tools/rccl_two_ranks_one_gpu.py).  RCCL itself runs at world 1 in
 tests/test_gpu_rccl.py; the data path of every rank is checked against the
 oracle in tests/test_gpu_dist_pipeline.py and test_gpu_world_emulation.py."""
 import json
