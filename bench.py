@@ -512,7 +512,8 @@ def dry_run(args, world: int, rank: int, cpu, wd: Watchdog) -> None:
     head = headline_variant(args, multi)
     wd.enter("headline")
     r = dry_design(ctx, head, args.steps, args.warmup)
-    line = {"metric": METRIC, "value": r["value"], "dry_run": True, "check": {"round": 0, "decoded_xor": r["check_xor"]},
+    check_local = r.pop("check_local")
+    line = {"metric": METRIC, "value": r["value"], "dry_run": True, "check": {"round": 0, "decoded_xor": None},
             "data": "dry run: no GPU; every step one gloo all_reduce of 4 KiB (the control flow, not a rate)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"],
             "ranks": ranks, "config": {"workload": workload(args, world, head), "design": head.name},
@@ -523,12 +524,15 @@ def dry_run(args, world: int, rank: int, cpu, wd: Watchdog) -> None:
         line["exchange_variants"] = [dict(variant_summary(r), workload=workload(args, world, head))]
         with wd.lock:
             wd.line = line if rank == 0 else {}
+        settle_check(ctx, r, check_local, line, wd)
         others = other_variants(args, head)
 
         def summarise(x):
             return dict(variant_summary(x), workload=workload(args, world, Variant(x["name"])))
 
         run_variants(ctx, dry_design, others, summarise, line, wd)
+    else:
+        line["check"]["decoded_xor"] = f"{check_local:016x}"
     wd.enter("done")
     if rank == 0:
         wd.emit(line)
@@ -774,7 +778,12 @@ class Watchdog:
         if errs:  # a rank that raised left its peers waiting in the design's collectives
             msg += "; errors raised by ranks: " + "; ".join(errs)
         print(f"bench.py rank {self.rank}: {msg}", file=sys.stderr, flush=True)
-        if self.rank == 0:
+        if self.rank == 0 and phase == "check":  # the headline's result check hung: the designs after it never ran
+            line["check"]["error"] = "hung"
+            line["check"]["detail"] = msg
+            line["variants_incomplete"] = True
+            self.emit(line)
+        elif self.rank == 0:
             line.setdefault("exchange_variants", []).append({"name": phase, "error": "hung", "detail": msg})
             line["exchange_variants"] += [{"name": p, "error": "skipped", "detail": f"not run: {phase!r} hung"}
                                           for p in pending]
@@ -856,6 +865,7 @@ def run_variants(ctx, runner, variants, summarise, out: dict, wd: Watchdog) -> N
         err = None
         try:
             res = runner(ctx, v, args.variant_steps, min(5, args.warmup))
+            combine_check(ctx, res)
         except Exception as e:  # noqa: BLE001 -- contained, reported in the line
             err = f"rank {rank}: {e!r}"
             print(f"bench.py rank {rank}: design {v.name!r} failed:", file=sys.stderr)
@@ -869,7 +879,7 @@ def run_variants(ctx, runner, variants, summarise, out: dict, wd: Watchdog) -> N
             if not failed:
                 entry = summarise(res)
                 want = out.get("check", {}).get("decoded_xor")
-                if want is not None and entry.get("check_xor") != want:
+                if want is not None and entry.get("check_xor") is not None and entry["check_xor"] != want:
                     entry["mismatch"] = f"round-0 result check {entry.get('check_xor')} != the headline's {want}"
                     out["designs_agree"] = False
                 out["exchange_variants"].append(entry)
@@ -922,18 +932,12 @@ def dry_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     if multi:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     ms = float(el[0]) * 1e3 / max(1, steps)
-    check = int(injected("corrupt", v.name, rank))
-    if multi:  # combined over the ranks like result_check
-        parts = [None] * world
-        dist.all_gather_object(parts, check)
-        check = 0
-        for p in parts:
-            check ^= p
+    check = int(injected("corrupt", v.name, rank))  # this rank's part (combine_check XORs them)
     return {"name": v.name, "ms_per_step": ms, "value": args.clients * args.elems / max(ms / 1e3, 1e-9),
             "steps": steps, "warmup": warmup, "kernel_ms_per_step": 0.0, "chunks": 1, "kernel": "none (dry run)",
             "exchange": {"ms_per_step": ms, "bytes_per_rank_per_step": 4096, "algbw_GBps": None, "busbw_GBps": None,
                          "collective": "dry run: one gloo all_reduce of 4 KiB per step"},
-            "check_xor": f"{check:016x}"}
+            "check_local": check}
 
 
 CHECK_NOTE = ("XOR of the bits of the decoded float64 aggregate (all C clients, every element) of round 0, "
@@ -941,13 +945,12 @@ CHECK_NOTE = ("XOR of the bits of the decoded float64 aggregate (all C clients, 
               "every N must print the same value (the same inputs, seeds and stream positions)")
 
 
-def result_check(ctx, v: Variant, step, sum_buf, dec, dec_all, sharded: bool, by_elems: bool) -> str:
-    """The design's result for round 0, reduced to one 64-bit XOR of the
-    decoded vector's float64 bits (CHECK_NOTE), combined over the ranks: a
-    mis-indexed shard transfer or a wrong slot shows as a differing value
-    between designs (run_variants flags it) or between N = 1 and N > 1."""
+def result_check(ctx, v: Variant, step, sum_buf, dec, dec_all, sharded: bool, by_elems: bool) -> int:
+    """This rank's part of the design's round-0 result check: the XOR of the
+    float64 bits of the decoded elements this rank holds (CHECK_NOTE).  No
+    collective here: combine_check XORs the ranks' parts, once the line it
+    belongs to is safe (the headline's line registered with the watchdog)."""
     import torch
-    import torch.distributed as dist
 
     from sfl_amd import kernels as K
 
@@ -974,13 +977,44 @@ def result_check(ctx, v: Variant, step, sum_buf, dec, dec_all, sharded: bool, by
     x = int(dig.item()) & (2 ** 64 - 1)
     if injected("corrupt", v.name, rank):  # SFL_BENCH_INJECT: a wrong result on this rank
         x ^= 1
-    if comm is not None and world > 1:
-        parts = [None] * world
+    return x
+
+
+def combine_check(ctx, res: dict) -> str:
+    """XOR the ranks' parts of a design's round-0 result check (gloo control
+    group): a mis-indexed shard transfer or a wrong slot shows as a value
+    differing between designs (run_variants flags it) or between N = 1 and
+    N > 1."""
+    import torch.distributed as dist
+
+    x = res.pop("check_local")
+    if ctx["world"] > 1 and dist.is_initialized():
+        parts = [None] * ctx["world"]
         dist.all_gather_object(parts, x, group=control_group(ctx))
         x = 0
         for p in parts:
-            x ^= p
-    return f"{x:016x}"
+            x = None if p is None or x is None else x ^ p
+    res["check_xor"] = None if x is None else f"{x:016x}"
+    return res["check_xor"]
+
+
+def settle_check(ctx, r: dict, check_local: int, out: dict, wd: Watchdog) -> None:
+    """The headline's round-0 check, combined over the ranks AFTER its line
+    is registered with the watchdog (phase "check": a hang here prints the
+    line without the check, an exception leaves the error in its place)."""
+    import traceback
+
+    wd.enter("check")
+    try:
+        r["check_local"] = check_local
+        x = combine_check(ctx, r)
+    except Exception as e:  # noqa: BLE001 -- the line stands without the check
+        traceback.print_exc()
+        x = None
+        out["check"]["error"] = repr(e)
+    with wd.lock:
+        out["check"]["decoded_xor"] = x
+        out["exchange_variants"][0]["check_xor"] = x
 
 
 def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
@@ -1088,7 +1122,13 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
                          device="cpu" if ctx.get("rehearse") else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms, xchg_ms = float(t[0]), float(t[1]), float(t[2])
-    check = result_check(ctx, v, step, sum_buf, dec, dec_all, sharded, by_elems)
+    try:  # the check is extra: a failure here must not cost the design's timing
+        check = result_check(ctx, v, step, sum_buf, dec, dec_all, sharded, by_elems)
+    except Exception:  # noqa: BLE001
+        import traceback
+
+        traceback.print_exc()
+        check = None
     flagged = bool(int(flags.item()))
     ms = elapsed * 1e3 / steps
     n_streams = len(plan.pairs) + len(plan.cross)
@@ -1104,7 +1144,7 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     res = {"name": v.name, "ms_per_step": ms, "value": C * N / (ms / 1e3), "steps": steps, "warmup": warmup,
            "kernel_ms_per_step": kern_ms, "chunks": len(pipe.bounds), "kernel": kname, "fused": fused,
            "local_clients": Lc, "n_loc": n_loc, "pair_draws": len(plan.pairs) * n_loc,
-           "one_sided_draws": len(plan.cross) * n_loc, "zero_draw_flag": flagged, "check_xor": check,
+           "one_sided_draws": len(plan.cross) * n_loc, "zero_draw_flag": flagged, "check_local": check,
            "kernel_timing": ("one HIP event pair on the launch stream around the timed region's back-to-back "
                              "launches" if region else "a HIP event pair around every launch")}
     if multi:
@@ -1324,17 +1364,21 @@ def rank_main(args):
         out["rehearsal"] = ("--rehearse-one-gpu: every rank on cuda:0, collectives through gloo host round "
                             "trips; the N > 1 control flow, not the product's rate")
     out["cpu_baseline"] = cpu
-    out["check"] = {"round": 0, "decoded_xor": r["check_xor"], "note": CHECK_NOTE}
+    check_local = r.pop("check_local")
+    out["check"] = {"round": 0, "decoded_xor": None, "note": CHECK_NOTE}
     if multi:
         out["designs_agree"] = True
-        # the headline is in hand: from here on a failed or hung design is
-        # recorded in its exchange_variants entry and cannot cost the line
+        # the headline is in hand: from here on a failed or hung design (or
+        # check) is recorded in the line and cannot cost it
         out["exchange"] = r["exchange"]
         out["exchange_variants"] = [variant_summary(r)]
         out["variant_timeout_seconds"] = args.variant_timeout
         with wd.lock:
             wd.line = out if rank == 0 else {}
+        settle_check(ctx, r, check_local, out, wd)
         run_variants(ctx, run_design, other_variants(args, head), variant_summary, out, wd)
+    else:
+        out["check"]["decoded_xor"] = None if check_local is None else f"{check_local:016x}"
     if args.extra and world == 1:
         from sfl_amd import kernels as K
 
