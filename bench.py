@@ -1218,6 +1218,9 @@ def main():
     ap.add_argument("--variant-timeout", type=float, default=120.0,
                     help="N>1: a design after the headline still running after this many seconds is declared "
                          "hung; rank 0 prints the line so far with that design marked, every rank exits 0")
+    ap.add_argument("--masking-reserve", type=int, default=0,
+                    help="CUs of the masking grid left free for the overlapped exchange kernels "
+                         "(sa_set_masking_reserve; tools/overlap_probe.py measured <= 3 %% either way)")
     ap.add_argument("--digests", action="store_true",
                     help="also fold every client's masked values into an XOR digest (test checksum)")
     ap.add_argument("--dry-run", action="store_true",
@@ -1279,7 +1282,7 @@ def rank_main(args):
     gpu = 0 if rehearse else local_rank
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    _lib.lib()
+    _lib.check(_lib.lib().sa_set_masking_reserve(args.masking_reserve), "sa_set_masking_reserve")
     comm = None
     if multi and rehearse:
         dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -177,6 +177,15 @@ int sa_fused_bipartite(const sa_local_client* clients, int x_type, uint64_t n, i
                        const sa_pcg64* pair_gens, const int8_t* pair_sign, uint64_t* sum_out,
                        int accumulate, uint32_t* flags, void* stream);
 
+/* Host setting for this process's masking launches (sa_mask, sa_fused_*):
+ * leave `cus` CUs' worth of the kernel's occupancy free for kernels that run
+ * concurrently on other streams -- the RCCL exchange of the previous chunk
+ * in the pipelined multi-GPU path, whose kernels otherwise wait for the
+ * masking grid (occupancy-sized, it fills every CU) to drain.  0 (default):
+ * the whole GPU.  At most half of the occupancy is ever reserved.  Results
+ * are unchanged (the grid only decides which tiles a block takes). */
+int sa_set_masking_reserve(int cus);
+
 /* Server `_sum`: out[i] = sum_k in[k][i] mod 2^64 (np.sum over uint64,
  * pattern of sfl/security/aggregation/sparse_plain_aggregator.py:88-94).
  * `in` is a HOST array of k device pointers; out may alias in[0]. */

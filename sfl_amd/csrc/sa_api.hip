@@ -4,6 +4,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <unordered_map>
 
@@ -13,6 +14,26 @@
 #include "sa_philox.h"
 
 namespace sa {
+
+// CUs' worth of the masking kernel's blocks left free for kernels on other
+// streams (sa_set_masking_reserve); 0: the masking grid fills the GPU
+static std::atomic<int> g_masking_reserve{0};
+
+int occupancy_blocks(const void* kernel);
+
+int masking_grid_cap(const void* kernel) {
+  const int maxb = occupancy_blocks(kernel);
+  const int reserve = g_masking_reserve.load(std::memory_order_relaxed);
+  if (maxb <= 0 || reserve <= 0) return maxb;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+    sa_set_error("occupancy query failed");
+    return -1;
+  }
+  const int keep = maxb - (maxb / cus) * reserve;
+  return keep > maxb / 2 ? keep : maxb / 2;
+}
 
 int occupancy_blocks(const void* kernel) {
   static std::mutex mu;
@@ -545,6 +566,15 @@ extern "C" int sa_fused_bipartite(const sa_local_client* clients, int x_type, ui
     return SA_ERR_UNSUPPORTED;
   }
   return fn(a, stream);
+}
+
+extern "C" int sa_set_masking_reserve(int cus) {
+  if (cus < 0 || cus > 128) {
+    sa_set_error("sa_set_masking_reserve: %d CUs (0..128)", cus);
+    return SA_ERR_ARG;
+  }
+  g_masking_reserve.store(cus, std::memory_order_relaxed);
+  return SA_OK;
 }
 
 extern "C" int sa_sum_u64(const uint64_t* const* in, int k, uint64_t n, uint64_t* out,

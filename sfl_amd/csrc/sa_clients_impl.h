@@ -973,6 +973,7 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
 // launcher
 // ----------------------------------------------------------------------------
 int occupancy_blocks(const void* kernel);  // sa_api.hip
+int masking_grid_cap(const void* kernel);  // sa_api.hip: occupancy less sa_set_masking_reserve's CUs
 
 // Buffer offsets are 32-bit byte offsets, so one launch covers at most
 // kChunkElems elements (4 GiB of u64); longer vectors are cut into chunks
@@ -984,7 +985,7 @@ template <typename XT, typename CT, int L, int X, int K = kAllPairs>
 int launch_clients(const KArgs& in, void* stream) {
   constexpr int P = Pairs<L, K>::count + L * X;
   const void* kfn = reinterpret_cast<const void*>(&k_clients<XT, CT, L, X, K>);
-  const int maxb = occupancy_blocks(kfn);
+  const int maxb = masking_grid_cap(kfn);
   if (maxb <= 0) return SA_ERR_HIP;
   for (uint64_t off = 0; off < in.n; off += kChunkElems) {
     KArgs a = in;

@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(64) k_sumsq_final(const double* __restrict__ p
   for (int j = threadIdx.x; j < k; j += 64) acc += partials[j];
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
   if (threadIdx.x == 0) {
-    const float norm = __fsqrt_rn((float)acc);  // np.linalg.norm: float32 dot, float32 sqrt
+    const float norm = sqrt_f32_rn((float)acc);  // np.linalg.norm: float32 dot, float32 sqrt
     const float sq = __fmul_rn(norm, norm);      // ** 2
     *out = accumulate ? (double)__fadd_rn((float)*out, sq) : (double)sq;
   }

@@ -117,10 +117,16 @@ __device__ __forceinline__ float dp_apply(float x, float scale, float z, float s
 // denominator np.sqrt(layer_norm * norm) in float32; clip / denom with a
 // python-float clip is a float64 division (value-based casting of two
 // scalars); the float32 array times that float64 scalar rounds it to float32.
+// float32 sqrt correctly rounded, as numpy's np.sqrt on float32: the float64
+// square root rounded to float32 (innocuous double rounding for sqrt: 53 >=
+// 2*24 + 2); gfx950's v_sqrt_f32 is 1 ulp, which the reference would see as
+// a different clip scale.
+__device__ __forceinline__ float sqrt_f32_rn(float x) { return (float)sqrt((double)x); }
+
 __device__ __forceinline__ float dp_scale(const double* sumsq, const double* sumsq_layer, float clip) {
-  const float norm_all = __fsqrt_rn((float)*sumsq);
+  const float norm_all = sqrt_f32_rn((float)*sumsq);
   float denom = norm_all;
-  if (sumsq_layer) denom = __fsqrt_rn(__fmul_rn(__fsqrt_rn((float)*sumsq_layer), norm_all));
+  if (sumsq_layer) denom = sqrt_f32_rn(__fmul_rn(sqrt_f32_rn((float)*sumsq_layer), norm_all));
   const double r = __ddiv_rn((double)clip, (double)denom);
   return r < 1.0 ? (float)r : 1.0f;
 }

@@ -147,3 +147,40 @@ def test_config5_per_rank_schedule_full_size():
                                          seed=r) >= 8 * 4096
     torch.cuda.synchronize()
     assert torch.equal(total, q_sum)
+
+
+def test_masking_reserve_leaves_results_unchanged():
+    """sa_set_masking_reserve (CUs of the masking grid left free for the
+    overlapped exchange) changes only which tiles a block takes: the sum of a
+    fused launch, of the multi-launch schedule and of a single-client pass is
+    bit-identical at every reserve; out-of-range values are refused."""
+    from oracle import secagg as o
+    from sfl_amd import _lib as L
+    from sfl_amd import kernels as K
+    from sfl_amd.parallel_sum import plan_generators, plan_rank
+
+    n = 3_000_017
+    names = [f"client{c}" for c in range(32)]
+    seeds = o.seeds_for(names)
+    seed_of = lambda u, v: seeds[names[u]][names[v]]  # noqa: E731
+    outs = []
+    try:
+        for r in (0, 8, 64, 128):
+            L.check(L.lib().sa_set_masking_reserve(r), "reserve")
+            res = []
+            for W in (8, 4, 32):  # 4 + 28 (multi-launch), 8 + 24 (multi-launch), 1 + 31 (passes)
+                plan = plan_rank(names, W, 1)
+                torch.manual_seed(W)
+                xs = [torch.randn(n, device=DEV) * 1e-2 for _ in plan.clients]
+                pg, ps, cross = plan_generators(plan, seed_of, offset=5)
+                s = torch.empty(n, dtype=torch.int64, device=DEV)
+                K.fused_clients(xs, [1.0] * len(xs), pg, ps, cross, plan.n_cross, s)
+                res.append(s)
+            torch.cuda.synchronize()
+            outs.append(res)
+    finally:
+        L.lib().sa_set_masking_reserve(0)
+    for res in outs[1:]:
+        for a, b in zip(outs[0], res):
+            assert torch.equal(a, b)
+    assert L.lib().sa_set_masking_reserve(-1) != L.SA_OK and L.lib().sa_set_masking_reserve(129) != L.SA_OK
