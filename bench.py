@@ -170,7 +170,7 @@ def cpu_baseline_parallel(C: int, fxp_bits: int, n: int) -> dict:
             "seconds": round(t, 3)}
 
 
-PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r03", "r02", "r01")]  # newest first
+PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r04", "r03", "r02", "r01")]  # newest first
 PMC_ELEMS = 100_000_000  # element positions per launch of the committed PMC passes
 
 

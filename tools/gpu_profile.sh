@@ -25,14 +25,14 @@ tail -1 gpurun_out/bench_prof.jsonl | cut -c1-300
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_server -o run -- \
   python3 tools/server_bench.py > gpurun_out/server_bench_prof.jsonl 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
-  python3 tools/kernel_bench.py --shapes 8:1,8:2,8:4,8:8 --rounds 1 --reps 2 --calib 8 --bipartite > gpurun_out/pmc_fetch.log 2>&1
+  python3 tools/kernel_bench.py --shapes 8:1,8:2,8:4,8:8,32:8 --rounds 1 --reps 2 --calib 8 --bipartite > gpurun_out/pmc_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- \
-  python3 tools/kernel_bench.py --shapes 8:1,8:2,8:4,8:8 --rounds 1 --reps 2 --calib 8 --bipartite > gpurun_out/pmc_write.log 2>&1
+  python3 tools/kernel_bench.py --shapes 8:1,8:2,8:4,8:8,32:8 --rounds 1 --reps 2 --calib 8 --bipartite > gpurun_out/pmc_write.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_server_fetch -o run -- \
   python3 tools/server_bench.py --reps 3 > gpurun_out/pmc_server_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_server_write -o run -- \
   python3 tools/server_bench.py --reps 3 > gpurun_out/pmc_server_write.log 2>&1
-tools/pmc_sq.sh 8:1,8:2,8:4,8:8 > /dev/null
+tools/pmc_sq.sh 8:1,8:2,8:4,8:8,32:8 > /dev/null
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_dp -o run -- \
   python3 tools/dp_bench.py --reps 10 --passes 1 > gpurun_out/dp_bench_prof.jsonl 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_dp_fetch -o run -- \
