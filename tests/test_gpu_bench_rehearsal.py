@@ -149,3 +149,30 @@ def test_bench_8_ranks_failing_rank_names_itself():
     assert r.returncode != 0
     tail = r.stderr[-3000:]
     assert "rank 3 failed" in tail and "SFL_BENCH_INJECT: rank 3 fails at start-up" in tail, tail
+
+
+def test_full_size_check_n1_n8_and_oracle():
+    """The driver's configurations at the headline size (8 x 100M): the N = 1
+    line's round-0 check equals the oracle's (the bench's synthetic inputs,
+    quantized and summed by numpy: the masks cancel) and the N = 8 rehearsal's
+    (8 rank processes on this GPU, <1,7> lean launches, the 8-chunk pipelined
+    sharded server with gloo stand-ins of the reduce-scatter) -- the value
+    the driver's SCALE lines must all print."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    common = ["--steps", "1", "--warmup", "0", "--cpu-baseline-seconds", "0", "--variants", "none"]
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *common],
+                        capture_output=True, text=True, timeout=150, env=env, cwd=ROOT)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    (l1,) = [json.loads(x) for x in r1.stdout.splitlines() if x.startswith("{")]
+    r8 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--rehearse-one-gpu",
+                         "--watchdog-seconds", "200", *common],
+                        capture_output=True, text=True, timeout=230, env=env, cwd=ROOT)
+    assert r8.returncode == 0, r8.stderr[-3000:]
+    (l8,) = [json.loads(x) for x in r8.stdout.splitlines() if x.startswith("{")]
+    want = oracle_check(8, 100_000_000)
+    assert l1["check"]["decoded_xor"] == want
+    assert l8["check"]["decoded_xor"] == want and l8["config"]["clients_per_gpu"] == 1
