@@ -513,7 +513,7 @@ def dry_run(args, world: int, rank: int, cpu, wd: Watchdog) -> None:
     wd.enter("headline")
     r = dry_design(ctx, head, args.steps, args.warmup)
     check_local = r.pop("check_local")
-    line = {"metric": METRIC, "value": r["value"], "dry_run": True, "check": {"round": 0, "decoded_xor": None},
+    line = {"metric": METRIC, "value": r["value"], "dry_run": True, "check": {"round": 0, "decoded_digest": None},
             "data": "dry run: no GPU; every step one gloo all_reduce of 4 KiB (the control flow, not a rate)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"],
             "ranks": ranks, "config": {"workload": workload(args, world, head), "design": head.name},
@@ -532,7 +532,7 @@ def dry_run(args, world: int, rank: int, cpu, wd: Watchdog) -> None:
 
         run_variants(ctx, dry_design, others, summarise, line, wd)
     else:
-        line["check"]["decoded_xor"] = f"{check_local:016x}"
+        line["check"]["decoded_digest"] = f"{check_local:016x}"
     wd.enter("done")
     if rank == 0:
         wd.emit(line)
@@ -878,9 +878,9 @@ def run_variants(ctx, runner, variants, summarise, out: dict, wd: Watchdog) -> N
         with wd.lock:
             if not failed:
                 entry = summarise(res)
-                want = out.get("check", {}).get("decoded_xor")
-                if want is not None and entry.get("check_xor") is not None and entry["check_xor"] != want:
-                    entry["mismatch"] = f"round-0 result check {entry.get('check_xor')} != the headline's {want}"
+                want = out.get("check", {}).get("decoded_digest")
+                if want is not None and entry.get("check_digest") is not None and entry["check_digest"] != want:
+                    entry["mismatch"] = f"round-0 result check {entry.get('check_digest')} != the headline's {want}"
                     out["designs_agree"] = False
                 out["exchange_variants"].append(entry)
                 continue
@@ -902,7 +902,7 @@ def variant_summary(x: dict) -> dict:
             "kernel_ms_per_step": x["kernel_ms_per_step"], "kernel": x["kernel"], "chunks": x["chunks"],
             "xchg_ms": x["exchange"]["ms_per_step"], "bytes_per_rank_per_step": x["exchange"]["bytes_per_rank_per_step"],
             "algbw_GBps": x["exchange"]["algbw_GBps"], "busbw_GBps": x["exchange"]["busbw_GBps"],
-            "collective": x["exchange"]["collective"], "check_xor": x.get("check_xor")}
+            "collective": x["exchange"]["collective"], "check_digest": x.get("check_digest")}
 
 
 def dry_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
@@ -932,7 +932,7 @@ def dry_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     if multi:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     ms = float(el[0]) * 1e3 / max(1, steps)
-    check = int(injected("corrupt", v.name, rank))  # this rank's part (combine_check XORs them)
+    check = int(injected("corrupt", v.name, rank))  # this rank's part (combine_check adds them)
     return {"name": v.name, "ms_per_step": ms, "value": args.clients * args.elems / max(ms / 1e3, 1e-9),
             "steps": steps, "warmup": warmup, "kernel_ms_per_step": 0.0, "chunks": 1, "kernel": "none (dry run)",
             "exchange": {"ms_per_step": ms, "bytes_per_rank_per_step": 4096, "algbw_GBps": None, "busbw_GBps": None,
@@ -940,27 +940,50 @@ def dry_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
             "check_local": check}
 
 
-CHECK_NOTE = ("XOR of the bits of the decoded float64 aggregate (all C clients, every element) of round 0, "
-              "recomputed after the timed region by one more untimed step of the same design: every design and "
-              "every N must print the same value (the same inputs, seeds and stream positions)")
+CHECK_NOTE = ("sum over i of bits(decoded[i]) * (2i + 1) * 0x9E3779B97F4A7C15 mod 2^64 over the decoded float64 "
+              "aggregate of round 0 (all C clients, every element), recomputed after the timed region by one more "
+              "untimed step of the same design: every design and every N must print the same value (the same "
+              "inputs, seeds and stream positions)")
 
 
-def result_check(ctx, v: Variant, step, sum_buf, dec, dec_all, sharded: bool, by_elems: bool) -> int:
-    """This rank's part of the design's round-0 result check: the XOR of the
-    float64 bits of the decoded elements this rank holds (CHECK_NOTE).  No
-    collective here: combine_check XORs the ranks' parts, once the line it
-    belongs to is safe (the headline's line registered with the watchdog)."""
+CHECK_MULT = 0x9E3779B97F4A7C15  # odd: the position weight of element i is (2i + 1) * CHECK_MULT mod 2^64
+
+
+def position_digest(t, base: int) -> int:
+    """sum_i bits(t[i]) * (2 (base + i) + 1) * CHECK_MULT mod 2^64 over a
+    float64 device vector whose element i is element base + i of the
+    aggregate: position-weighted, so a shard decoded into the wrong place
+    changes it (an XOR or plain sum would not see a permutation).  In slices
+    of 2^26 elements to bound the temporaries; int64 products and sums wrap
+    like uint64."""
+    import torch
+
+    mult = CHECK_MULT - (1 << 64)  # the same 64 bits as a signed int64
+    out, n, step = 0, t.numel(), 1 << 26
+    bits = t.view(torch.int64)
+    for lo in range(0, n, step):
+        hi = min(n, lo + step)
+        h = (torch.arange(base + lo, base + hi, device=t.device, dtype=torch.int64) * 2 + 1) * mult
+        out = (out + int((bits[lo:hi] * h).sum().item())) & ((1 << 64) - 1)
+    return out
+
+
+def result_check(ctx, v: Variant, step, sum_buf, dec, dec_all, sharded: bool, by_elems: bool, e0: int) -> int:
+    """This rank's part of the design's round-0 result check (CHECK_NOTE):
+    the position digest of the decoded elements this rank holds (zeros
+    elsewhere contribute nothing).  No collective here: combine_check adds
+    the ranks' parts mod 2^64 once the line it belongs to is safe (the
+    headline's line registered with the watchdog)."""
     import torch
 
     from sfl_amd import kernels as K
 
-    args, world, rank, dev, comm = ctx["args"], ctx["world"], ctx["rank"], ctx["dev"], ctx["comm"]
+    args, rank, dev, comm = ctx["args"], ctx["rank"], ctx["dev"], ctx["comm"]
     step(0, False)
     torch.cuda.synchronize()
-    dig = torch.zeros(1, dtype=torch.int64, device=dev)
-    src = None
-    if by_elems:  # every rank its decoded slice; with the gather rank 0 holds them all
-        src = dec_all if v.gather else dec
+    src, base = None, 0
+    if by_elems:  # every rank its decoded slice (global start e0); with the gather rank 0 holds them all
+        src, base = (dec_all, 0) if v.gather else (dec, e0)
         if v.gather and rank != 0:
             src = None
         if comm is None:  # world 1 without --dist: the slice is the whole vector, not decoded by the step
@@ -971,20 +994,17 @@ def result_check(ctx, v: Variant, step, sum_buf, dec, dec_all, sharded: bool, by
     elif rank == 0:  # reduce (and N = 1): rank 0 holds the masked sum
         src = torch.empty(args.elems, dtype=torch.float64, device=dev)
         K.decode(sum_buf[:args.elems], src, fxp_bits=args.fxp_bits)
-    if src is not None:
-        K.xor_digest(src.view(torch.int64), dig)
-    torch.cuda.synchronize()
-    x = int(dig.item()) & (2 ** 64 - 1)
+    x = position_digest(src, base) if src is not None else 0
     if injected("corrupt", v.name, rank):  # SFL_BENCH_INJECT: a wrong result on this rank
-        x ^= 1
+        x = (x + 1) & ((1 << 64) - 1)
     return x
 
 
 def combine_check(ctx, res: dict) -> str:
-    """XOR the ranks' parts of a design's round-0 result check (gloo control
-    group): a mis-indexed shard transfer or a wrong slot shows as a value
-    differing between designs (run_variants flags it) or between N = 1 and
-    N > 1."""
+    """Add the ranks' parts of a design's round-0 result check mod 2^64 (gloo
+    control group): a mis-indexed shard transfer or a wrong slot shows as a
+    value differing between designs (run_variants flags it) or between N = 1
+    and N > 1."""
     import torch.distributed as dist
 
     x = res.pop("check_local")
@@ -993,9 +1013,9 @@ def combine_check(ctx, res: dict) -> str:
         dist.all_gather_object(parts, x, group=control_group(ctx))
         x = 0
         for p in parts:
-            x = None if p is None or x is None else x ^ p
-    res["check_xor"] = None if x is None else f"{x:016x}"
-    return res["check_xor"]
+            x = None if p is None or x is None else (x + p) & ((1 << 64) - 1)
+    res["check_digest"] = None if x is None else f"{x:016x}"
+    return res["check_digest"]
 
 
 def settle_check(ctx, r: dict, check_local: int, out: dict, wd: Watchdog) -> None:
@@ -1013,8 +1033,8 @@ def settle_check(ctx, r: dict, check_local: int, out: dict, wd: Watchdog) -> Non
         x = None
         out["check"]["error"] = repr(e)
     with wd.lock:
-        out["check"]["decoded_xor"] = x
-        out["exchange_variants"][0]["check_xor"] = x
+        out["check"]["decoded_digest"] = x
+        out["exchange_variants"][0]["check_digest"] = x
 
 
 def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
@@ -1123,7 +1143,7 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms, xchg_ms = float(t[0]), float(t[1]), float(t[2])
     try:  # the check is extra: a failure here must not cost the design's timing
-        check = result_check(ctx, v, step, sum_buf, dec, dec_all, sharded, by_elems)
+        check = result_check(ctx, v, step, sum_buf, dec, dec_all, sharded, by_elems, e0)
     except Exception:  # noqa: BLE001
         import traceback
 
@@ -1368,7 +1388,7 @@ def rank_main(args):
                             "trips; the N > 1 control flow, not the product's rate")
     out["cpu_baseline"] = cpu
     check_local = r.pop("check_local")
-    out["check"] = {"round": 0, "decoded_xor": None, "note": CHECK_NOTE}
+    out["check"] = {"round": 0, "decoded_digest": None, "note": CHECK_NOTE}
     if multi:
         out["designs_agree"] = True
         # the headline is in hand: from here on a failed or hung design (or
@@ -1381,7 +1401,7 @@ def rank_main(args):
         settle_check(ctx, r, check_local, out, wd)
         run_variants(ctx, run_design, other_variants(args, head), variant_summary, out, wd)
     else:
-        out["check"]["decoded_xor"] = None if check_local is None else f"{check_local:016x}"
+        out["check"]["decoded_digest"] = None if check_local is None else f"{check_local:016x}"
     if args.extra and world == 1:
         from sfl_amd import kernels as K
 

@@ -323,3 +323,26 @@ def test_cross_only_counts_match_the_registry():
     assert counts == bench.CROSS_COUNTS
     src = open(os.path.join(ROOT, "sfl_amd", "csrc", "sa_clients_f32.hip")).read()
     assert {int(v) for v in re.findall(r"\bXO\((\d+)\)", src)} == set(counts)
+
+
+def test_position_digest_matches_numpy_and_sees_permutations():
+    """bench.position_digest (the round-0 result check): sum of bits(x[i]) *
+    (2(base+i)+1) * CHECK_MULT mod 2^64, additive over slices at their global
+    offsets (how the ranks' parts combine), and changed by swapping two
+    shards (an XOR or a plain sum would not be)."""
+    import numpy as np
+    import torch
+
+    import bench
+
+    rng = np.random.default_rng(3)
+    x = (rng.integers(-2**15, 2**15, 1_000_003) / 2.0**18).astype(np.float64)
+    idx = np.arange(x.size, dtype=np.uint64)
+    want = int(np.sum(x.view(np.uint64) * ((idx * np.uint64(2) + np.uint64(1)) * np.uint64(bench.CHECK_MULT)),
+                      dtype=np.uint64))
+    t = torch.from_numpy(x)
+    assert bench.position_digest(t, 0) == want
+    k = 400_001
+    assert (bench.position_digest(t[:k], 0) + bench.position_digest(t[k:], k)) % 2**64 == want
+    y = np.concatenate([x[k:2 * k], x[:k], x[2 * k:]])  # two shards swapped
+    assert bench.position_digest(torch.from_numpy(y), 0) != want

@@ -26,7 +26,7 @@ def oracle_check(C: int, n: int, fxp_bits: int = 18) -> str:
     """bench.py's round-0 result check from the oracle: the bench's synthetic
     inputs regenerated the same way (torch.Generator on the GPU), the masked
     sum = sum of the quantized vectors (the pair masks cancel), decoded, and
-    the float64 bits XOR-ed."""
+    the float64 bits digested by position (bench.position_digest)."""
     import numpy as np
 
     from oracle import secagg as o
@@ -38,7 +38,9 @@ def oracle_check(C: int, n: int, fxp_bits: int = 18) -> str:
         x = (torch.randn(n, generator=g, device=dev, dtype=torch.float32) * 1e-2).cpu().numpy()
         qs.append(o.quantize(x, None, fxp_bits))
     dec = o.decode(o.server_sum(qs), fxp_bits)
-    return f"{int(np.bitwise_xor.reduce(dec.view(np.uint64))):016x}"
+    idx = np.arange(n, dtype=np.uint64)
+    h = (idx * np.uint64(2) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)  # bench.CHECK_MULT
+    return f"{int(np.sum(dec.view(np.uint64) * h, dtype=np.uint64)):016x}"
 
 
 @pytest.fixture(scope="module")
@@ -73,8 +75,8 @@ def test_bench_n_ranks_every_design(world, check_1m):
     assert line["n_gpus"] == world and "rehearsal" in line and line["config"]["design"] == "sharded"
     assert "exchange_probe" not in line and line["exchange_variants"][0]["name"] == "sharded"
     # every design's round-0 result equals the oracle's (and so N = 1's)
-    assert line["check"]["decoded_xor"] == check_1m and line["designs_agree"] is True
-    assert all(v["check_xor"] == check_1m for v in line["exchange_variants"]), line["exchange_variants"]
+    assert line["check"]["decoded_digest"] == check_1m and line["designs_agree"] is True
+    assert all(v["check_digest"] == check_1m for v in line["exchange_variants"]), line["exchange_variants"]
     per = 8 // world
     assert line["config"]["clients_per_gpu"] == per
     assert line["roofline"]["kernel"].startswith(f"k_clients<float, float, {per}, {8 - per}, ")
@@ -109,7 +111,7 @@ def test_bench_n1_line(check_1m):
     assert rf["launches_per_step"] == 1 and rf["kernel_timing"].startswith("one HIP event pair")
     assert 0 < rf["kernel_ms_per_step"] <= d["ms_per_step"] * 1.01
     assert abs(d["value"] - 8 * 1000003 / (d["ms_per_step"] / 1e3)) < 1e-6 * d["value"]
-    assert d["check"]["decoded_xor"] == check_1m
+    assert d["check"]["decoded_digest"] == check_1m
 
 
 def _rehearse(world, inject, *extra, timeout=115):
@@ -174,5 +176,5 @@ def test_full_size_check_n1_n8_and_oracle():
     assert r8.returncode == 0, r8.stderr[-3000:]
     (l8,) = [json.loads(x) for x in r8.stdout.splitlines() if x.startswith("{")]
     want = oracle_check(8, 100_000_000)
-    assert l1["check"]["decoded_xor"] == want
-    assert l8["check"]["decoded_xor"] == want and l8["config"]["clients_per_gpu"] == 1
+    assert l1["check"]["decoded_digest"] == want
+    assert l8["check"]["decoded_digest"] == want and l8["config"]["clients_per_gpu"] == 1

@@ -251,5 +251,5 @@ def test_bench_self_launched_dist_world1(opts):
     from test_gpu_bench_rehearsal import oracle_check
 
     want_check = oracle_check(8, 1000003)
-    assert line["designs_agree"] is True and line["check"]["decoded_xor"] == want_check
-    assert all(v["check_xor"] == want_check for v in line["exchange_variants"])
+    assert line["designs_agree"] is True and line["check"]["decoded_digest"] == want_check
+    assert all(v["check_digest"] == want_check for v in line["exchange_variants"])
