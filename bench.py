@@ -783,6 +783,9 @@ class Watchdog:
             line["check"]["detail"] = msg
             line["variants_incomplete"] = True
             self.emit(line)
+        elif self.rank == 0 and phase == "host_resident":  # after every design: only this field is lost
+            line["host_resident"] = {"error": "hung", "detail": msg}
+            self.emit(line)
         elif self.rank == 0:
             line.setdefault("exchange_variants", []).append({"name": phase, "error": "hung", "detail": msg})
             line["exchange_variants"] += [{"name": p, "error": "skipped", "detail": f"not run: {phase!r} hung"}
@@ -895,6 +898,29 @@ def run_variants(ctx, runner, variants, summarise, out: dict, wd: Watchdog) -> N
                 return
     with wd.lock:
         wd.pending = []
+
+
+def run_contained(ctx, phase: str, fn, out: dict, wd: Watchdog) -> None:
+    """One more measurement after the designs, contained like them: its
+    result (or the ranks' errors) goes to out[phase]; a hang is the
+    watchdog's (phase named)."""
+    import traceback
+
+    import torch.distributed as dist
+
+    wd.enter(phase)
+    err, res = None, None
+    try:
+        res = fn()
+    except Exception as e:  # noqa: BLE001 -- contained, reported in the line
+        err = f"rank {ctx['rank']}: {e!r}"
+        traceback.print_exc()
+        publish_error(phase, ctx["rank"], err)
+    errs = [None] * ctx["world"]
+    dist.all_gather_object(errs, err, group=control_group(ctx))
+    failed = [e for e in errs if e is not None]
+    with wd.lock:
+        out[phase] = {"error": "failed", "detail": "; ".join(failed)} if failed else res
 
 
 def variant_summary(x: dict) -> dict:
@@ -1241,6 +1267,9 @@ def main():
     ap.add_argument("--masking-reserve", type=int, default=0,
                     help="CUs of the masking grid left free for the overlapped exchange kernels "
                          "(sa_set_masking_reserve; tools/overlap_probe.py measured <= 3 %% either way)")
+    ap.add_argument("--host-resident-steps", type=int, default=20,
+                    help="N>1 with the sharded headline: also time this many steps with inputs and results in "
+                         "pinned host memory (H2D / D2H inclusive, line field host_resident; 0: skip)")
     ap.add_argument("--digests", action="store_true",
                     help="also fold every client's masked values into an XOR digest (test checksum)")
     ap.add_argument("--dry-run", action="store_true",
@@ -1400,6 +1429,9 @@ def rank_main(args):
             wd.line = out if rank == 0 else {}
         settle_check(ctx, r, check_local, out, wd)
         run_variants(ctx, run_design, other_variants(args, head), variant_summary, out, wd)
+        if args.host_resident_steps > 0 and head.name == "sharded" and not out.get("variants_incomplete"):
+            run_contained(ctx, "host_resident", lambda: run_host_resident(
+                ctx, args.host_resident_steps, min(3, args.warmup)), out, wd)
     else:
         out["check"]["decoded_digest"] = None if check_local is None else f"{check_local:016x}"
     if args.extra and world == 1:
@@ -1419,6 +1451,87 @@ def rank_main(args):
     if comm is not None:
         comm.close()
         dist.destroy_process_group()
+
+
+def run_host_resident(ctx, steps: int, warmup: int) -> dict:
+    """N > 1: the headline design with its inputs and results in pinned host
+    memory (the north star's "starts and ends in host memory", in process):
+    per step every local client's fp32 vector is copied H2D chunk by chunk on
+    an H2D stream, chunk j is masked as soon as its copy lands, exchanged and
+    decoded on the comm stream (the reduce-scatter sharded server), and this
+    rank's decoded shard of chunk j goes D2H on a third stream; the next
+    step's H2D of chunk j waits for that D2H (the decode buffer is reused)
+    and for the previous launch of chunk j.  Timed like a design (barrier +
+    synchronise on both sides, max over ranks).  Not `value`."""
+    import torch
+    import torch.distributed as dist
+
+    from sfl_amd.parallel_sum import PipelinedMaskedSum, plan_generators, plan_rank, rank_shards
+
+    args, world, rank, dev, comm = ctx["args"], ctx["world"], ctx["rank"], ctx["dev"], ctx["comm"]
+    C, N = args.clients, args.elems
+    plan = plan_rank(ctx["names"], world, rank)
+    Lc = len(plan.clients)
+    host_x = torch.empty((Lc, N), dtype=torch.float32).pin_memory()
+    for i, c in enumerate(plan.clients):  # the headline's synthetic data
+        g = torch.Generator(device=dev).manual_seed(20260116 + c)
+        host_x[i].copy_(torch.randn(N, generator=g, device=dev, dtype=torch.float32) * 1e-2)
+    dev_x = torch.empty((Lc, N), dtype=torch.float32, device=dev)
+    pipe = PipelinedMaskedSum(comm, dev, N, args.chunks if args.chunks is not None else 8, exchange="sharded")
+    sum_buf = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
+    dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev)
+    host_dec = torch.empty(pipe.buffer_len, dtype=torch.float64).pin_memory()
+    shards = [(a, b) for a, b in rank_shards(pipe.bounds, world, rank, N)]
+    total = warmup + steps
+    gens = [[plan_generators(plan, pair_seed, offset=i * N + lo) for lo, _ in pipe.bounds] for i in range(total)]
+    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    J = len(pipe.bounds)
+    ev_in = [torch.cuda.Event() for _ in range(J)]
+    ev_dec = [torch.cuda.Event() for _ in range(J)]
+    ev_free = [torch.cuda.Event() for _ in range(J)]
+
+    def after(j):  # comm stream current: chunk j exchanged and decoded
+        a, b = shards[j]
+        ev_dec[j].record(pipe.comm_stream)
+        d2h.wait_event(ev_dec[j])
+        with torch.cuda.stream(d2h):
+            if b > a:
+                host_dec[a:b].copy_(dec[a:b], non_blocking=True)
+            ev_free[j].record(d2h)
+
+    def step(i):
+        with torch.cuda.stream(h2d):
+            for j, (lo, hi) in enumerate(pipe.bounds):
+                h2d.wait_event(ev_free[j])      # the previous step's D2H of this chunk's shard
+                h2d.wait_event(pipe.events[j])  # the previous step's launch over this chunk
+                for c in range(Lc):  # contiguous rows: one DMA each
+                    dev_x[c, lo:hi].copy_(host_x[c, lo:hi], non_blocking=True)
+                ev_in[j].record(h2d)
+        pipe.run([dev_x[c] for c in range(Lc)], [1.0] * Lc, gens[i], plan.n_cross, sum_buf, None,
+                 fxp_bits=args.fxp_bits, join=False, dec=dec, chunk_ready=ev_in, after_chunk=after)
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX, group=control_group(ctx))
+    ms = float(el[0]) * 1e3 / steps
+    shard_elems = sum(b - a for a, b in shards)
+    del host_x, dev_x, sum_buf, dec, host_dec, pipe, gens
+    torch.cuda.empty_cache()
+    return {"ms_per_step": ms, "grad_elems_per_s": C * N / (ms / 1e3), "steps": steps, "warmup": warmup,
+            "pcie_bytes_per_rank_per_step": {"h2d": 4 * Lc * N, "d2h": 8 * shard_elems},
+            "what": ("fp32 inputs in pinned host memory -> H2D per chunk (own stream) -> the headline's masking + "
+                     "reduce-scatter + shard decode -> D2H of this rank's decoded shard (own stream); max over "
+                     "ranks")}
 
 
 def extra_measurements(args, xs, plan, gens, K, torch, dev) -> dict:

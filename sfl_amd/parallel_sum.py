@@ -262,7 +262,7 @@ class PipelinedMaskedSum:
     def run(self, xs, weights, chunk_gens, n_cross: int, sum_buf, recv=None, *, root: int = 0,
             fxp_bits: int = 18, digests=None, flags=None, kernel_events: list | None = None,
             exchange_events: list | None = None, join: bool = True, dec=None, divisor: float = 1.0,
-            gather: bool = False):
+            gather: bool = False, chunk_ready: list | None = None, after_chunk=None):
         """``kernel_events``: if given, a timing-event pair recorded around
         each chunk's masking launch is appended (kernel time without the
         exchange); ``exchange_events`` likewise around each chunk's reduce on
@@ -271,7 +271,13 @@ class PipelinedMaskedSum:
         comm stream (the caller synchronises the device before reading the
         result); a following run() still orders each chunk's launch after
         that chunk's previous reduce, so back-to-back rounds overlap one
-        round's exchange tail with the next round's first launches."""
+        round's exchange tail with the next round's first launches.
+
+        Host-resident pipelines (bench.py's host_resident): ``chunk_ready[j]``
+        is an event the compute stream waits for before chunk j's launch
+        (its H2D), and ``after_chunk(j)`` is called with the comm stream
+        current right after chunk j's exchange and decode (to enqueue its
+        D2H)."""
         import torch
 
         from . import kernels as K
@@ -290,6 +296,8 @@ class PipelinedMaskedSum:
             if self._pending[j]:  # the previous round's reduce of this chunk still reads sum_buf
                 compute.wait_event(self.reduced[j])
                 self._pending[j] = False
+            if chunk_ready is not None:
+                compute.wait_event(chunk_ready[j])
             if kernel_events is not None:
                 kernel_events.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
                 kernel_events[-1][0].record(compute)
@@ -323,6 +331,8 @@ class PipelinedMaskedSum:
                     else:
                         self.comm.reduce_u64(sum_buf[lo:hi], recv[lo:hi] if recv is not None else None,
                                              root=root)
+                    if after_chunk is not None:
+                        after_chunk(j)
                     if exchange_events is not None:
                         exchange_events[-1][1].record(self.comm_stream)
                     self.reduced[j].record(self.comm_stream)

@@ -74,6 +74,9 @@ def test_bench_n_ranks_every_design(world, check_1m):
     # the headline is the reduce-scatter sharded server, measured first
     assert line["n_gpus"] == world and "rehearsal" in line and line["config"]["design"] == "sharded"
     assert "exchange_probe" not in line and line["exchange_variants"][0]["name"] == "sharded"
+    # the headline with inputs and results in pinned host memory (H2D / D2H inclusive)
+    hr = line["host_resident"]
+    assert hr["grad_elems_per_s"] > 0 and hr["pcie_bytes_per_rank_per_step"]["h2d"] == 4 * (8 // world) * 1000003, hr
     # every design's round-0 result equals the oracle's (and so N = 1's)
     assert line["check"]["decoded_digest"] == check_1m and line["designs_agree"] is True
     assert all(v["check_digest"] == check_1m for v in line["exchange_variants"]), line["exchange_variants"]
