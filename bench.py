@@ -1472,11 +1472,12 @@ def run_host_resident(ctx, steps: int, warmup: int) -> dict:
     C, N = args.clients, args.elems
     plan = plan_rank(ctx["names"], world, rank)
     Lc = len(plan.clients)
-    host_x = torch.empty((Lc, N), dtype=torch.float32).pin_memory()
-    for i, c in enumerate(plan.clients):  # the headline's synthetic data
+    # one allocation per client (16-B aligned whatever N is), the headline's synthetic data
+    host_x = [torch.empty(N, dtype=torch.float32).pin_memory() for _ in plan.clients]
+    for i, c in enumerate(plan.clients):
         g = torch.Generator(device=dev).manual_seed(20260116 + c)
         host_x[i].copy_(torch.randn(N, generator=g, device=dev, dtype=torch.float32) * 1e-2)
-    dev_x = torch.empty((Lc, N), dtype=torch.float32, device=dev)
+    dev_x = [torch.empty(N, dtype=torch.float32, device=dev) for _ in plan.clients]
     pipe = PipelinedMaskedSum(comm, dev, N, args.chunks if args.chunks is not None else 8, exchange="sharded")
     sum_buf = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
     dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev)
@@ -1504,10 +1505,10 @@ def run_host_resident(ctx, steps: int, warmup: int) -> dict:
             for j, (lo, hi) in enumerate(pipe.bounds):
                 h2d.wait_event(ev_free[j])      # the previous step's D2H of this chunk's shard
                 h2d.wait_event(pipe.events[j])  # the previous step's launch over this chunk
-                for c in range(Lc):  # contiguous rows: one DMA each
-                    dev_x[c, lo:hi].copy_(host_x[c, lo:hi], non_blocking=True)
+                for c in range(Lc):
+                    dev_x[c][lo:hi].copy_(host_x[c][lo:hi], non_blocking=True)
                 ev_in[j].record(h2d)
-        pipe.run([dev_x[c] for c in range(Lc)], [1.0] * Lc, gens[i], plan.n_cross, sum_buf, None,
+        pipe.run(dev_x, [1.0] * Lc, gens[i], plan.n_cross, sum_buf, None,
                  fxp_bits=args.fxp_bits, join=False, dec=dec, chunk_ready=ev_in, after_chunk=after)
 
     for i in range(warmup):

@@ -76,6 +76,7 @@ def test_bench_n_ranks_every_design(world, check_1m):
     assert "exchange_probe" not in line and line["exchange_variants"][0]["name"] == "sharded"
     # the headline with inputs and results in pinned host memory (H2D / D2H inclusive)
     hr = line["host_resident"]
+    assert "error" not in hr, hr
     assert hr["grad_elems_per_s"] > 0 and hr["pcie_bytes_per_rank_per_step"]["h2d"] == 4 * (8 // world) * 1000003, hr
     # every design's round-0 result equals the oracle's (and so N = 1's)
     assert line["check"]["decoded_digest"] == check_1m and line["designs_agree"] is True
