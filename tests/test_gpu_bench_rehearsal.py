@@ -32,12 +32,13 @@ def oracle_check(C: int, n: int, fxp_bits: int = 18) -> str:
     from oracle import secagg as o
 
     dev = torch.device("cuda", 0)
-    qs = []
-    for c in range(C):
+    s = np.zeros(n, dtype=np.uint64)
+    for c in range(C):  # accumulated client by client (no C x n stack at 100M)
         g = torch.Generator(device=dev).manual_seed(20260116 + c)
         x = (torch.randn(n, generator=g, device=dev, dtype=torch.float32) * 1e-2).cpu().numpy()
-        qs.append(o.quantize(x, None, fxp_bits))
-    dec = o.decode(o.server_sum(qs), fxp_bits)
+        s += o.quantize(x, None, fxp_bits)
+        del x
+    dec = o.decode(s, fxp_bits)
     idx = np.arange(n, dtype=np.uint64)
     h = (idx * np.uint64(2) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)  # bench.CHECK_MULT
     return f"{int(np.sum(dec.view(np.uint64) * h, dtype=np.uint64)):016x}"
@@ -157,28 +158,36 @@ def test_bench_8_ranks_failing_rank_names_itself():
     assert "rank 3 failed" in tail and "SFL_BENCH_INJECT: rank 3 fails at start-up" in tail, tail
 
 
-def test_full_size_check_n1_n8_and_oracle():
-    """The driver's configurations at the headline size (8 x 100M): the N = 1
-    line's round-0 check equals the oracle's (the bench's synthetic inputs,
-    quantized and summed by numpy: the masks cancel) and the N = 8 rehearsal's
-    (8 rank processes on this GPU, <1,7> lean launches, the 8-chunk pipelined
-    sharded server with gloo stand-ins of the reduce-scatter) -- the value
-    the driver's SCALE lines must all print."""
+@pytest.fixture(scope="module")
+def check_100m():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    return oracle_check(8, 100_000_000)
+
+
+def _full_size_line(*extra, timeout=150):
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    common = ["--steps", "1", "--warmup", "0", "--cpu-baseline-seconds", "0", "--variants", "none"]
-    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *common],
-                        capture_output=True, text=True, timeout=150, env=env, cwd=ROOT)
-    assert r1.returncode == 0, r1.stderr[-3000:]
-    (l1,) = [json.loads(x) for x in r1.stdout.splitlines() if x.startswith("{")]
-    r8 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--rehearse-one-gpu",
-                         "--watchdog-seconds", "200", *common],
-                        capture_output=True, text=True, timeout=230, env=env, cwd=ROOT)
-    assert r8.returncode == 0, r8.stderr[-3000:]
-    (l8,) = [json.loads(x) for x in r8.stdout.splitlines() if x.startswith("{")]
-    want = oracle_check(8, 100_000_000)
-    assert l1["check"]["decoded_digest"] == want
-    assert l8["check"]["decoded_digest"] == want and l8["config"]["clients_per_gpu"] == 1
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0",
+                        "--cpu-baseline-seconds", "0", "--variants", "none", "--host-resident-steps", "0", *extra],
+                       capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    (line,) = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    return line
+
+
+def test_full_size_check_n1_vs_oracle(check_100m):
+    """The driver's N = 1 configuration at the headline size (8 x 100M): the
+    line's round-0 digest equals the oracle's (the bench's synthetic inputs,
+    quantized and summed by numpy: the masks cancel)."""
+    assert _full_size_line()["check"]["decoded_digest"] == check_100m
+
+
+def test_full_size_check_n8_rehearsal_vs_oracle(check_100m):
+    """The N = 8 configuration at the headline size, rehearsed on this GPU (8
+    rank processes, <1,7> lean launches, the 8-chunk pipelined sharded server
+    with gloo stand-ins of the reduce-scatter): the same digest as the
+    oracle's and N = 1's -- the value the driver's SCALE lines must print."""
+    line = _full_size_line("--gpus", "8", "--rehearse-one-gpu", "--watchdog-seconds", "140")
+    assert line["check"]["decoded_digest"] == check_100m and line["config"]["clients_per_gpu"] == 1
