@@ -61,7 +61,7 @@ def test_bench_n_ranks_every_design(world, check_1m):
     t0 = time.time()
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                         "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
-                        "--cpu-baseline-seconds", "0", "--watchdog-seconds", "100"],
+                        "--host-resident-steps", "3", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "100"],
                        capture_output=True, text=True, timeout=115, env=env, cwd=ROOT)
     if r.returncode != 0:  # the lines that say why (ranks interleave their output), then the tail
         why = [ln for ln in r.stderr.splitlines()
@@ -126,7 +126,8 @@ def _rehearse(world, inject, *extra, timeout=115):
     env["SFL_BENCH_INJECT"] = inject
     return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                            "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
-                           "--cpu-baseline-seconds", "0", "--watchdog-seconds", "100", *extra],
+                           "--host-resident-steps", "0", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "100",
+                           *extra],
                           capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
 
 
