@@ -402,7 +402,7 @@ def launch_ranks(args) -> int:
         shutil.rmtree(log_dir, ignore_errors=True)
 
 
-def failing_ranks_report(log_dir: str, lines_per_rank: int = 40) -> str:
+def failing_ranks_report(log_dir: str, lines_per_rank: int = 60) -> str:
     """After a failed torchrun child: for every rank whose error file or
     stderr log holds a traceback, its last traceback (torchrun's error.json
     from @record first, else the tail of stderr.log from the last
@@ -425,9 +425,10 @@ def failing_ranks_report(log_dir: str, lines_per_rank: int = 40) -> str:
         if not text:
             with open(path, errors="replace") as f:
                 log = f.read()
-            # a Python exception, or a fatal signal's stacks (faulthandler is
-            # enabled in every rank)
-            i = max(log.rfind("Traceback (most recent call last)"), log.rfind("Fatal Python error"))
+            # a Python exception, a fatal signal's stacks (faulthandler is
+            # enabled in every rank) or the watchdog's stack dump at expiry
+            i = max(log.rfind("Traceback (most recent call last)"), log.rfind("Fatal Python error"),
+                    log.rfind("Timeout ("))
             if i < 0:
                 continue
             text = log[i:]
@@ -739,6 +740,9 @@ class Watchdog:
             self.phase, self.t_phase = phase, time.monotonic()
             if phase in self.pending:
                 self.pending.remove(phase)
+        if os.environ.get("SFL_BENCH_TRACE"):  # phase timeline on stderr (the rehearsal tests set it)
+            print(f"bench.py rank {self.rank}: phase {phase} at {self.t_phase - self.t0:.1f} s", file=sys.stderr,
+                  flush=True)
 
     def emit(self, line: dict) -> bool:
         """Print ``line`` (rank 0), once per process."""

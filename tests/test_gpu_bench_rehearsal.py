@@ -58,6 +58,7 @@ def test_bench_n_ranks_every_design(world, check_1m):
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
+    env["SFL_BENCH_TRACE"] = "1"  # phase timeline on stderr, reported on failure
     t0 = time.time()
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                         "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
@@ -65,9 +66,12 @@ def test_bench_n_ranks_every_design(world, check_1m):
                        capture_output=True, text=True, timeout=115, env=env, cwd=ROOT)
     if r.returncode != 0:  # the lines that say why (ranks interleave their output), then the tail
         why = [ln for ln in r.stderr.splitlines()
-               if any(k in ln for k in ("Error", "error:", "Traceback", "watchdog", "still running", "exitcode"))]
+               if any(k in ln for k in ("Error", "error:", "Traceback", "watchdog", "still running", "exitcode",
+                                        "rank 0: phase", "headline not"))]
+        rep = r.stderr[r.stderr.find("---- bench.py: rank"):] if "---- bench.py: rank" in r.stderr else ""
         pytest.fail(f"bench.py --gpus {world} --rehearse-one-gpu: rc {r.returncode} after {time.time() - t0:.0f} s\n"
-                    + "\n".join(why[:40]) + "\n--- stderr tail ---\n" + r.stderr[-2500:]
+                    + "\n".join(why[:60]) + "\n--- failing ranks ---\n" + rep[:8000]
+                    + "\n--- stderr tail ---\n" + r.stderr[-1500:]
                     + "\n--- stdout tail ---\n" + r.stdout[-1000:])
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
