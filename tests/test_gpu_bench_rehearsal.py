@@ -62,8 +62,8 @@ def test_bench_n_ranks_every_design(world, check_1m):
     t0 = time.time()
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                         "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
-                        "--host-resident-steps", "3", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "100"],
-                       capture_output=True, text=True, timeout=115, env=env, cwd=ROOT)
+                        "--host-resident-steps", "3", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "150"],
+                       capture_output=True, text=True, timeout=170, env=env, cwd=ROOT)
     if r.returncode != 0:  # the lines that say why (ranks interleave their output), then the tail
         why = [ln for ln in r.stderr.splitlines()
                if any(k in ln for k in ("Error", "error:", "Traceback", "watchdog", "still running", "exitcode",
@@ -123,14 +123,23 @@ def test_bench_n1_line(check_1m):
     assert d["check"]["decoded_digest"] == check_1m
 
 
-def _rehearse(world, inject, *extra, timeout=115):
+def _explain(r) -> str:
+    """A failed bench run's story: rank 0's phase timeline (SFL_BENCH_TRACE),
+    the launcher's per-rank tracebacks / watchdog dumps, the stderr tail."""
+    phases = [ln for ln in r.stderr.splitlines() if "rank 0: phase" in ln or "headline not" in ln]
+    rep = r.stderr[r.stderr.find("---- bench.py: rank"):] if "---- bench.py: rank" in r.stderr else ""
+    return "\n".join(phases) + "\n--- failing ranks ---\n" + rep[:8000] + "\n--- stderr tail ---\n" + r.stderr[-1500:]
+
+
+def _rehearse(world, inject, *extra, timeout=170):
     env = dict(os.environ)
+    env["SFL_BENCH_TRACE"] = "1"
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     env["SFL_BENCH_INJECT"] = inject
     return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                            "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
-                           "--host-resident-steps", "0", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "100",
+                           "--host-resident-steps", "0", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "150",
                            *extra],
                           capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
 
@@ -143,7 +152,7 @@ def test_bench_8_ranks_keeps_headline_when_designs_fail_or_hang():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     r = _rehearse(8, "fail:direct,hang:elements", "--variant-timeout", "8")
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _explain(r)
     (line,) = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert line["value"] > 0 and line["config"]["design"] == "sharded" and line["variants_incomplete"]
     got = {v["name"]: v for v in line["exchange_variants"]}
@@ -172,12 +181,13 @@ def check_100m():
 
 def _full_size_line(*extra, timeout=150):
     env = dict(os.environ)
+    env["SFL_BENCH_TRACE"] = "1"
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0",
                         "--cpu-baseline-seconds", "0", "--variants", "none", "--host-resident-steps", "0", *extra],
                        capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _explain(r)
     (line,) = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     return line
 
