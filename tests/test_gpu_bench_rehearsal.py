@@ -22,6 +22,19 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def rehearsal_env(env: dict) -> dict:
+    """Environment for W rank processes on this box's one GPU: the phase
+    timeline on stderr (SFL_BENCH_TRACE), and 2 hardware queues per process
+    instead of HIP's 4 (8 processes x 4-5 streams would ask the GPU's
+    scheduler for 32+ queues at once, which the driver's one-process-per-GPU
+    run never does)."""
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["SFL_BENCH_TRACE"] = "1"
+    env["GPU_MAX_HW_QUEUES"] = "2"
+    return env
+
+
 def oracle_check(C: int, n: int, fxp_bits: int = 18) -> str:
     """bench.py's round-0 result check from the oracle: the bench's synthetic
     inputs regenerated the same way (torch.Generator on the GPU), the masked
@@ -55,10 +68,7 @@ def check_1m():
 def test_bench_n_ranks_every_design(world, check_1m):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    env = dict(os.environ)
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
-        env.pop(k, None)
-    env["SFL_BENCH_TRACE"] = "1"  # phase timeline on stderr, reported on failure
+    env = rehearsal_env(dict(os.environ))
     t0 = time.time()
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                         "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
@@ -132,10 +142,7 @@ def _explain(r) -> str:
 
 
 def _rehearse(world, inject, *extra, timeout=170):
-    env = dict(os.environ)
-    env["SFL_BENCH_TRACE"] = "1"
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
-        env.pop(k, None)
+    env = rehearsal_env(dict(os.environ))
     env["SFL_BENCH_INJECT"] = inject
     return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                            "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
@@ -180,10 +187,7 @@ def check_100m():
 
 
 def _full_size_line(*extra, timeout=150):
-    env = dict(os.environ)
-    env["SFL_BENCH_TRACE"] = "1"
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
-        env.pop(k, None)
+    env = rehearsal_env(dict(os.environ))
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0",
                         "--cpu-baseline-seconds", "0", "--variants", "none", "--host-resident-steps", "0", *extra],
                        capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
