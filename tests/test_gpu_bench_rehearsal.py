@@ -86,6 +86,10 @@ def test_bench_n_ranks_every_design(world, check_1m):
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = lines[0]
+    # a complete run (no design declared hung by the watchdog), with rank 0's
+    # phase timeline in the message if not
+    assert not line.get("variants_incomplete") and "host_resident" in line, (
+        f"after {time.time() - t0:.0f} s: {line.get('exchange_variants')}\n" + _explain(r))
     # the headline is the reduce-scatter sharded server, measured first
     assert line["n_gpus"] == world and "rehearsal" in line and line["config"]["design"] == "sharded"
     assert "exchange_probe" not in line and line["exchange_variants"][0]["name"] == "sharded"
