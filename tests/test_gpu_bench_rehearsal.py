@@ -74,6 +74,7 @@ def test_bench_n_ranks_every_design(world, check_1m):
                         "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
                         "--host-resident-steps", "3", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "150"],
                        capture_output=True, text=True, timeout=170, env=env, cwd=ROOT)
+    _keep_stderr(f"every_design_w{world}", r, t0)
     if r.returncode != 0:  # the lines that say why (ranks interleave their output), then the tail
         why = [ln for ln in r.stderr.splitlines()
                if any(k in ln for k in ("Error", "error:", "Traceback", "watchdog", "still running", "exitcode",
@@ -137,6 +138,18 @@ def test_bench_n1_line(check_1m):
     assert d["check"]["decoded_digest"] == check_1m
 
 
+def _keep_stderr(name: str, r, t0: float, slow: float = 60.0) -> None:
+    """A failed or slow (> `slow` s) multi-rank run's whole stderr (every
+    rank's phase timeline and, when the watchdog cut it, every rank's stack
+    dump) to gpurun_out/rehearsal_stderr/ for reading afterwards."""
+    if r.returncode == 0 and time.time() - t0 < slow:
+        return
+    d = os.path.join(ROOT, "gpurun_out", "rehearsal_stderr")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, f"{name}_{int(time.time())}.err"), "w") as f:
+        f.write(f"rc {r.returncode} after {time.time() - t0:.1f} s\n" + r.stderr)
+
+
 def _explain(r) -> str:
     """A failed bench run's story: rank 0's phase timeline (SFL_BENCH_TRACE),
     the launcher's per-rank tracebacks / watchdog dumps, the stderr tail."""
@@ -148,11 +161,14 @@ def _explain(r) -> str:
 def _rehearse(world, inject, *extra, timeout=170):
     env = rehearsal_env(dict(os.environ))
     env["SFL_BENCH_INJECT"] = inject
-    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                            "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
                            "--host-resident-steps", "0", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "150",
                            *extra],
                           capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    _keep_stderr(f"rehearse_{inject.replace(':', '-').replace(',', '_')}", r, t0, slow=45.0)
+    return r
 
 
 def test_bench_8_ranks_keeps_headline_when_designs_fail_or_hang():
@@ -192,9 +208,11 @@ def check_100m():
 
 def _full_size_line(*extra, timeout=150):
     env = rehearsal_env(dict(os.environ))
+    t0 = time.time()
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0",
                         "--cpu-baseline-seconds", "0", "--variants", "none", "--host-resident-steps", "0", *extra],
                        capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    _keep_stderr("full_size" + ("_w8" if "--gpus" in extra else "_n1"), r, t0, slow=40.0)
     assert r.returncode == 0, _explain(r)
     (line,) = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     return line
