@@ -603,64 +603,118 @@ def collective_text(v: Variant) -> str:
     return "ncclReduce(uint64, sum) in place to rank 0"
 
 
-class GlooStandinComm:
+class HostStandinComm:
     """--rehearse-one-gpu only: RcclComm's contract (reduce_u64,
-    reduce_scatter_u64, alltoall_u64, gather_f64) through gloo host round trips, so N rank
-    processes can run every design's code path on ONE GPU (RCCL refuses two
-    ranks on one device: "Duplicate GPU detected").  Called on the comm
-    stream like RcclComm; ``send.cpu()`` waits for the chunk's launch.  Its
-    timings are host round trips, not xGMI: a rehearsal checks the N > 1
-    control flow, never the rate."""
+    reduce_scatter_u64, alltoall_u64, gather_f64) for N rank processes on
+    ONE GPU (RCCL refuses two ranks on one device: "Duplicate GPU detected"),
+    so every design's code path runs.  The data moves through a file-backed
+    shared mapping on this host -- every rank writes its host copy of the
+    send buffer into its slot, a gloo barrier, every rank reads what the
+    collective gives it, a second barrier before the slots are reused -- and
+    only the barriers' few bytes go through gloo's TCP.  (Round 4: with the
+    data itself on gloo's loopback TCP, a W = 8 rehearsal now and then sat
+    for minutes inside one all_reduce on every rank at once,
+    DESIGN.md §5.)  Called on the comm stream like RcclComm; ``send.cpu()``
+    waits for the chunk's launch.  Its timings are host copies, not xGMI: a
+    rehearsal checks the N > 1 control flow, never the rate."""
 
-    def __init__(self, rank: int, world: int):
-        self.rank, self.world = rank, world
+    def __init__(self, rank: int, world: int, group=None):
+        import tempfile
 
-    def reduce_u64(self, send, recv, root: int = 0):
         import torch.distributed as dist
 
-        host = send.cpu()
-        dist.reduce(host, dst=root, op=dist.ReduceOp.SUM)  # int64 addition wraps like uint64
+        self.rank, self.world, self.group = rank, world, group
+        box = [tempfile.mkdtemp(prefix="sfl_rehearsal_") if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        self.dir, self.cap, self.gen, self.mm = box[0], 0, 0, None
+
+    def _barrier(self):
+        import torch.distributed as dist
+
+        dist.barrier(group=self.group)
+
+    def _slots(self, nbytes: int):
+        """The (world, cap) byte view of the shared slots, grown (collectively:
+        every rank asks for the same size) when an op needs more."""
+        import numpy as np
+
+        if nbytes > self.cap:
+            self.cap = max(nbytes, 2 * self.cap)
+            path = os.path.join(self.dir, f"slots_{self.gen}")
+            self.gen += 1
+            if self.rank == 0:
+                with open(path, "wb") as f:
+                    f.truncate(self.world * self.cap)
+            self._barrier()
+            self.mm = np.memmap(path, dtype=np.uint8, mode="r+", shape=(self.world, self.cap))
+        return self.mm
+
+    def _post(self, t):
+        """This rank's host copy of ``t`` into its slot; then every rank's slots
+        are readable.  Returns (slots, nbytes)."""
+        import numpy as np
+
+        host = t.cpu().numpy()  # on the comm stream: waits for the chunk's launch
+        nb = host.nbytes
+        mm = self._slots(nb)
+        mm[self.rank, :nb] = host.reshape(-1).view(np.uint8)  # a shared mapping: no msync needed between processes
+        self._barrier()
+        return mm, nb
+
+    def reduce_u64(self, send, recv, root: int = 0):
+        import numpy as np
+        import torch
+
+        mm, nb = self._post(send)
         if self.rank == root:
-            (recv if recv is not None else send).copy_(host)
+            total = np.sum(mm[:, :nb].view(np.uint64), axis=0, dtype=np.uint64)  # wraps mod 2^64
+            (recv if recv is not None else send).copy_(torch.from_numpy(total.view(np.int64)))
+        self._barrier()
         return recv
 
     def reduce_scatter_u64(self, send, recv):
-        import torch.distributed as dist
+        import numpy as np
+        import torch
 
         if send.numel() != recv.numel() * self.world:
             raise ValueError("reduce_scatter: shard sizes")
-        host = send.cpu()
-        dist.all_reduce(host, op=dist.ReduceOp.SUM)
+        mm, nb = self._post(send)
         k = recv.numel()
-        recv.copy_(host[self.rank * k:(self.rank + 1) * k])
+        part = mm[:, :nb].view(np.uint64)[:, self.rank * k:(self.rank + 1) * k]
+        recv.copy_(torch.from_numpy(np.sum(part, axis=0, dtype=np.uint64).view(np.int64)))
+        self._barrier()
         return recv
 
     def alltoall_u64(self, send, recv):
+        import numpy as np
         import torch
-        import torch.distributed as dist
 
-        host = send.cpu()
-        parts = [torch.empty_like(host) for _ in range(self.world)]
-        dist.all_gather(parts, host)
-        k = host.numel() // self.world
+        mm, nb = self._post(send)
+        k = send.numel() // self.world
+        slots = mm[:, :nb].view(np.int64)
         for p in range(self.world):
             if p != self.rank:
-                recv[p * k:(p + 1) * k].copy_(parts[p][self.rank * k:(self.rank + 1) * k])
+                recv[p * k:(p + 1) * k].copy_(torch.from_numpy(np.array(slots[p, self.rank * k:(self.rank + 1) * k])))
+        self._barrier()
         return recv
 
     def gather_f64(self, send, recv, root: int = 0):
+        import numpy as np
         import torch
-        import torch.distributed as dist
 
-        host = send.cpu()
-        parts = [torch.empty_like(host) for _ in range(self.world)] if self.rank == root else None
-        dist.gather(host, parts, dst=root)
+        mm, nb = self._post(send)
         if self.rank == root:
-            recv.copy_(torch.cat(parts))
+            recv.copy_(torch.from_numpy(np.array(mm[:, :nb].view(np.float64)).reshape(-1)))
+        self._barrier()
         return recv
 
     def close(self):
-        pass
+        import shutil
+
+        self.mm = None
+        self._barrier()
+        if self.rank == 0:
+            shutil.rmtree(self.dir, ignore_errors=True)
 
 
 # ------------------------------------------------ failure containment (N > 1)
@@ -1280,7 +1334,7 @@ def main():
                     help="launcher rehearsal without a GPU: ranks join a gloo group, rank 0 prints one line")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, a gloo process group and the "
-                         "collectives through gloo host round trips (RCCL refuses two ranks on one GPU); runs "
+                         "collectives through a shared host mapping (RCCL refuses two ranks on one GPU); runs "
                          "every design's code path, its timings are not the product's")
     ap.add_argument("--watchdog-seconds", type=float, default=480.0,
                     help="a rank still running after this long exits: with the headline done, rank 0 first "
@@ -1339,7 +1393,7 @@ def rank_main(args):
     comm = None
     if multi and rehearse:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        comm = GlooStandinComm(rank, world)
+        comm = HostStandinComm(rank, world)
     elif multi:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         comm = RcclComm(rank, world, local_rank)
@@ -1417,8 +1471,8 @@ def rank_main(args):
                               "issue": int_ops}},
     }
     if rehearse:
-        out["rehearsal"] = ("--rehearse-one-gpu: every rank on cuda:0, collectives through gloo host round "
-                            "trips; the N > 1 control flow, not the product's rate")
+        out["rehearsal"] = ("--rehearse-one-gpu: every rank on cuda:0, collectives through a shared host mapping "
+                            "with gloo barriers; the N > 1 control flow, not the product's rate")
     out["cpu_baseline"] = cpu
     check_local = r.pop("check_local")
     out["check"] = {"round": 0, "decoded_digest": None, "note": CHECK_NOTE}

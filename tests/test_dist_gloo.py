@@ -143,3 +143,66 @@ def test_element_shard_slices(n, world):
         assert e0 == pos and 0 <= m <= k and k % 128 == 0
         pos += m
     assert pos == n
+
+
+def _standin_worker(rank, world, init, q):
+    import torch
+
+    from bench import HostStandinComm
+
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
+    comm = HostStandinComm(rank, world)
+    rng = np.random.default_rng(100 + rank)
+    ok = {}
+    k = 1001
+    for trial in range(2):  # the second round grows the shared slots
+        n = k * world * (trial + 1)
+        kk = n // world
+        send = torch.from_numpy(rng.integers(-2**62, 2**62, n, dtype=np.int64))
+        alls = [None] * world
+        dist.all_gather_object(alls, send.numpy().copy())  # the expectation, from gloo itself
+        total = np.sum(np.stack(alls).view(np.uint64), axis=0, dtype=np.uint64)
+        recv = torch.empty(kk, dtype=torch.int64)
+        comm.reduce_scatter_u64(send, recv)
+        ok[f"rs{trial}"] = bool(np.array_equal(recv.numpy().view(np.uint64), total[rank * kk:(rank + 1) * kk]))
+        got = torch.full((n,), -7, dtype=torch.int64)
+        comm.alltoall_u64(send, got)
+        exp = np.full(n, -7, dtype=np.int64)
+        for p in range(world):
+            if p != rank:
+                exp[p * kk:(p + 1) * kk] = alls[p][rank * kk:(rank + 1) * kk]
+        ok[f"a2a{trial}"] = bool(np.array_equal(got.numpy(), exp))
+        s2 = send.clone()
+        comm.reduce_u64(s2, None, root=1)
+        if rank == 1:
+            ok[f"red{trial}"] = bool(np.array_equal(s2.numpy().view(np.uint64), total))
+        f = torch.from_numpy(rng.standard_normal(kk))
+        fs = [None] * world
+        dist.all_gather_object(fs, f.numpy().copy())
+        g = torch.empty(world * kk, dtype=torch.float64) if rank == 0 else None
+        comm.gather_f64(f, g, root=0)
+        if rank == 0:
+            ok[f"gat{trial}"] = bool(np.array_equal(g.numpy(), np.concatenate(fs)))
+    comm.close()
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_standin_comm_matches_the_collectives(world):
+    """bench.HostStandinComm (the one-GPU rehearsal's stand-in for RcclComm:
+    data through a shared file mapping, gloo barriers) gives what the
+    collectives it stands in for give: reduce-scatter shards of the uint64
+    sum, the alltoall slots (own slot untouched), the in-place uint64
+    reduce to a root, the float64 gather -- also after its slots grow."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init = "file://" + os.path.join(tempfile.mkdtemp(prefix="sfl_gloo_"), "store")
+    procs = [ctx.Process(target=_standin_worker, args=(r, world, init, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+    for rank, ok in res:
+        assert ok and all(ok.values()), (rank, ok)

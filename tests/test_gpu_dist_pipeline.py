@@ -4,10 +4,11 @@ launches, the comm stream and its per-chunk events, the in-place reduce) on
 the one GPU of the test box.
 
 RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so the
-exchange here is a gloo-backed stand-in with RcclComm's ``reduce_u64``
-contract: on the comm stream, after the chunk's event, the partial sum is
-reduced to the root IN PLACE (recv=None) -- int64 addition wraps like the
-uint64 reduce.  Everything else is the product code path the N > 1 bench
+exchange here is bench.py's rehearsal stand-in with RcclComm's contract
+(``HostStandinComm``: the ranks' host copies through a shared file mapping,
+gloo barriers): on the comm stream, after the chunk's event, the partial
+sum is reduced to the root IN PLACE (recv=None) -- uint64 addition mod
+2^64.  Everything else is the product code path the N > 1 bench
 runs.  The root's buffer must equal the oracle's server sum bit for bit, and
 every client's digest the oracle's."""
 import os
@@ -17,22 +18,6 @@ import pytest
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
-
-
-class GlooReduce:
-    """RcclComm.reduce_u64 stand-in: host round trip through gloo."""
-
-    def __init__(self, rank, world):
-        self.rank, self.world = rank, world
-
-    def reduce_u64(self, send, recv, root: int = 0):
-        import torch.distributed as dist
-
-        host = send.cpu()  # on the current (comm) stream: waits for the chunk's launch
-        dist.reduce(host, dst=root, op=dist.ReduceOp.SUM)
-        if self.rank == root:
-            (recv if recv is not None else send).copy_(host, non_blocking=False)
-        return recv
 
 
 def _run_ranks(target, world, args):
@@ -86,7 +71,9 @@ def _worker(rank, world, init, n, chunks, offset, q):
         xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
         dev = torch.device("cuda", 0)
         plan = plan_rank(names, world, rank)
-        pipe = PipelinedMaskedSum(GlooReduce(rank, world), dev, n, chunks)
+        from bench import HostStandinComm
+
+        pipe = PipelinedMaskedSum(HostStandinComm(rank, world), dev, n, chunks)
         gens = [plan_generators(plan, seed_of, offset=offset + lo) for lo, _ in pipe.bounds]
         part = torch.empty(n, dtype=torch.int64, device=dev)
         dig = torch.zeros(len(plan.clients), dtype=torch.int64, device=dev)
@@ -116,47 +103,6 @@ def test_ranks_pipeline_and_in_place_reduce(world, chunks):
         assert fl == 0
 
 
-class GlooShardedServer:
-    """RcclComm's sharded-server contract (reduce_scatter_u64 / gather_f64)
-    through gloo host round trips, for W ranks on the one test GPU."""
-
-    def __init__(self, rank, world):
-        self.rank, self.world = rank, world
-
-    def reduce_scatter_u64(self, send, recv):
-        import torch.distributed as dist
-
-        host = send.cpu()  # on the comm stream: waits for the chunk's launch
-        dist.all_reduce(host, op=dist.ReduceOp.SUM)  # int64 addition wraps like uint64
-        k = recv.numel()
-        recv.copy_(host[self.rank * k:(self.rank + 1) * k], non_blocking=False)
-        return recv
-
-    def alltoall_u64(self, send, recv):
-        import torch
-        import torch.distributed as dist
-
-        host = send.cpu()
-        parts = [torch.empty_like(host) for _ in range(self.world)]
-        dist.all_gather(parts, host)
-        k = host.numel() // self.world
-        for p in range(self.world):
-            if p != self.rank:
-                recv[p * k:(p + 1) * k].copy_(parts[p][self.rank * k:(self.rank + 1) * k], non_blocking=False)
-        return recv
-
-    def gather_f64(self, send, recv, root: int = 0):
-        import torch
-        import torch.distributed as dist
-
-        host = send.cpu()
-        parts = [torch.empty_like(host) for _ in range(self.world)] if self.rank == root else None
-        dist.gather(host, parts, dst=root)
-        if self.rank == root:
-            recv.copy_(torch.cat(parts), non_blocking=False)
-        return recv
-
-
 def _worker_sharded(rank, world, init, n, chunks, offset, exchange, q):
     import torch
     import torch.distributed as dist
@@ -174,7 +120,9 @@ def _worker_sharded(rank, world, init, n, chunks, offset, exchange, q):
         xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
         dev = torch.device("cuda", 0)
         plan = plan_rank(names, world, rank)
-        pipe = PipelinedMaskedSum(GlooShardedServer(rank, world), dev, n, chunks, exchange=exchange)
+        from bench import HostStandinComm
+
+        pipe = PipelinedMaskedSum(HostStandinComm(rank, world), dev, n, chunks, exchange=exchange)
         gens = [plan_generators(plan, seed_of, offset=offset + lo) for lo, _ in pipe.bounds]
         part = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
         dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev)
