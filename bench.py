@@ -624,9 +624,14 @@ class HostStandinComm:
         import torch.distributed as dist
 
         self.rank, self.world, self.group = rank, world, group
-        box = [tempfile.mkdtemp(prefix="sfl_rehearsal_") if rank == 0 else None]
+        # /dev/shm keeps the slots in memory (a disk-backed /tmp file made the
+        # full-size W = 8 rehearsal write back GBs per step); each slot file
+        # is unlinked as soon as every rank has mapped it, so nothing is left
+        # behind however a rank ends
+        base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
+        box = [os.path.join(base, f"sfl_rehearsal_{os.getpid()}") if rank == 0 else None]
         dist.broadcast_object_list(box, src=0, group=group)
-        self.dir, self.cap, self.gen, self.mm = box[0], 0, 0, None
+        self.prefix, self.cap, self.gen, self.mm = box[0], 0, 0, None
 
     def _barrier(self):
         import torch.distributed as dist
@@ -640,13 +645,16 @@ class HostStandinComm:
 
         if nbytes > self.cap:
             self.cap = max(nbytes, 2 * self.cap)
-            path = os.path.join(self.dir, f"slots_{self.gen}")
+            path = f"{self.prefix}_{self.gen}"
             self.gen += 1
             if self.rank == 0:
                 with open(path, "wb") as f:
                     f.truncate(self.world * self.cap)
             self._barrier()
             self.mm = np.memmap(path, dtype=np.uint8, mode="r+", shape=(self.world, self.cap))
+            self._barrier()
+            if self.rank == 0:
+                os.unlink(path)  # the mappings keep the pages until every rank drops them
         return self.mm
 
     def _post(self, t):
@@ -709,12 +717,8 @@ class HostStandinComm:
         return recv
 
     def close(self):
-        import shutil
-
-        self.mm = None
+        self.mm = None  # the slot files are unlinked already: dropping the mapping frees them
         self._barrier()
-        if self.rank == 0:
-            shutil.rmtree(self.dir, ignore_errors=True)
 
 
 # ------------------------------------------------ failure containment (N > 1)

@@ -3,7 +3,8 @@ GPU of the test box (`bench.py --gpus W --rehearse-one-gpu`): the
 self-launcher, W torchrun ranks, every design's code path in run_design
 (client sharding with the pipelined sharded server, its gather, the reduce
 to rank 0, element sharding with and without the gather) and the max-over-
-ranks timing, with the collectives through gloo host round trips because
+ranks timing, with the collectives through a host stand-in (bench.HostStandinComm:
+a file mapping shared by the ranks, gloo barriers) because
 RCCL refuses two ranks on one GPU ("Duplicate GPU detected",
 tools/rccl_two_ranks_one_gpu.py).  RCCL itself runs at world 1 in
 tests/test_gpu_rccl.py; the data path of every rank is checked against the
@@ -228,7 +229,7 @@ def test_full_size_check_n1_vs_oracle(check_100m):
 def test_full_size_check_n8_rehearsal_vs_oracle(check_100m):
     """The N = 8 configuration at the headline size, rehearsed on this GPU (8
     rank processes, <1,7> lean launches, the 8-chunk pipelined sharded server
-    with gloo stand-ins of the reduce-scatter): the same digest as the
+    with host stand-ins of the reduce-scatter): the same digest as the
     oracle's and N = 1's -- the value the driver's SCALE lines must print."""
     line = _full_size_line("--gpus", "8", "--rehearse-one-gpu", "--watchdog-seconds", "140")
     assert line["check"]["decoded_digest"] == check_100m and line["config"]["clients_per_gpu"] == 1
