@@ -607,36 +607,64 @@ class HostStandinComm:
     """--rehearse-one-gpu only: RcclComm's contract (reduce_u64,
     reduce_scatter_u64, alltoall_u64, gather_f64) for N rank processes on
     ONE GPU (RCCL refuses two ranks on one device: "Duplicate GPU detected"),
-    so every design's code path runs.  The data moves through a file-backed
-    shared mapping on this host -- every rank writes its host copy of the
-    send buffer into its slot, a gloo barrier, every rank reads what the
-    collective gives it, a second barrier before the slots are reused -- and
-    only the barriers' few bytes go through gloo's TCP.  (Round 4: with the
-    data itself on gloo's loopback TCP, a W = 8 rehearsal now and then sat
-    for minutes inside one all_reduce on every rank at once,
-    DESIGN.md §5.)  Called on the comm stream like RcclComm; ``send.cpu()``
-    waits for the chunk's launch.  Its timings are host copies, not xGMI: a
-    rehearsal checks the N > 1 control flow, never the rate."""
+    so every design's code path runs.  Everything moves through memory shared
+    by the ranks on this host: every rank writes its host copy of the send
+    buffer into its slot, a barrier, every rank reads what the collective
+    gives it, a second barrier before the slots are reused.  The barrier is
+    in the shared memory too (each rank publishes an epoch in its own cache
+    line and waits for every rank's), so the data path touches no socket:
+    round 4's W = 8 rehearsals now and then sat for 30-50 s inside one gloo
+    all_reduce / barrier on every rank at once.  gloo only
+    sets the mappings up.  Called on the comm stream like RcclComm;
+    ``send.cpu()`` waits for the chunk's launch.  Its timings are host
+    copies, not xGMI: a rehearsal checks the N > 1 control flow, never the
+    rate."""
 
     def __init__(self, rank: int, world: int, group=None):
         import tempfile
 
+        import numpy as np
         import torch.distributed as dist
 
         self.rank, self.world, self.group = rank, world, group
         # /dev/shm keeps the slots in memory (a disk-backed /tmp file made the
-        # full-size W = 8 rehearsal write back GBs per step); each slot file
-        # is unlinked as soon as every rank has mapped it, so nothing is left
+        # full-size W = 8 rehearsal write back GBs per step); each file is
+        # unlinked as soon as every rank has mapped it, so nothing is left
         # behind however a rank ends
         base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
         box = [os.path.join(base, f"sfl_rehearsal_{os.getpid()}") if rank == 0 else None]
         dist.broadcast_object_list(box, src=0, group=group)
-        self.prefix, self.cap, self.gen, self.mm = box[0], 0, 0, None
+        self.prefix, self.cap, self.gen, self.mm, self.epoch = box[0], 0, 0, None, 0
+        self.ctl = self._shared((world, 8), np.int64)  # [r, 0]: rank r's barrier epoch
 
-    def _barrier(self):
+    def _shared(self, shape, dtype):
+        """A new zeroed mapping of ``shape`` shared by every rank (collective)."""
+        import numpy as np
         import torch.distributed as dist
 
+        path = f"{self.prefix}_{self.gen}"
+        self.gen += 1
+        if self.rank == 0:
+            with open(path, "wb") as f:
+                f.truncate(int(np.prod(shape)) * np.dtype(dtype).itemsize)
         dist.barrier(group=self.group)
+        mm = np.memmap(path, dtype=dtype, mode="r+", shape=shape)
+        dist.barrier(group=self.group)
+        if self.rank == 0:
+            os.unlink(path)  # the mappings keep the pages until every rank drops them
+        return mm
+
+    def _barrier(self):
+        """Every rank has reached the same epoch.  Each rank's epoch word has
+        one writer; x86 keeps stores in order, so a rank that sees another's
+        epoch also sees the slot bytes that rank wrote before it."""
+        self.epoch += 1
+        self.ctl[self.rank, 0] = self.epoch
+        col = self.ctl[:, 0]
+        spins = 0
+        while int(col.min()) < self.epoch:
+            spins += 1
+            time.sleep(0 if spins < 200 else 50e-6)
 
     def _slots(self, nbytes: int):
         """The (world, cap) byte view of the shared slots, grown (collectively:
@@ -645,16 +673,8 @@ class HostStandinComm:
 
         if nbytes > self.cap:
             self.cap = max(nbytes, 2 * self.cap)
-            path = f"{self.prefix}_{self.gen}"
-            self.gen += 1
-            if self.rank == 0:
-                with open(path, "wb") as f:
-                    f.truncate(self.world * self.cap)
-            self._barrier()
-            self.mm = np.memmap(path, dtype=np.uint8, mode="r+", shape=(self.world, self.cap))
-            self._barrier()
-            if self.rank == 0:
-                os.unlink(path)  # the mappings keep the pages until every rank drops them
+            self.mm = None
+            self.mm = self._shared((self.world, self.cap), np.uint8)
         return self.mm
 
     def _post(self, t):

@@ -70,12 +70,12 @@ def test_bench_n_ranks_every_design(world, check_1m):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     env = rehearsal_env(dict(os.environ))
-    t0 = time.time()
+    t0, before = time.time(), host_counters()
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                         "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
                         "--host-resident-steps", "3", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "150"],
                        capture_output=True, text=True, timeout=170, env=env, cwd=ROOT)
-    _keep_stderr(f"every_design_w{world}", r, t0)
+    _keep_stderr(f"every_design_w{world}", r, t0, before=before)
     if r.returncode != 0:  # the lines that say why (ranks interleave their output), then the tail
         why = [ln for ln in r.stderr.splitlines()
                if any(k in ln for k in ("Error", "error:", "Traceback", "watchdog", "still running", "exitcode",
@@ -139,16 +139,44 @@ def test_bench_n1_line(check_1m):
     assert d["check"]["decoded_digest"] == check_1m
 
 
-def _keep_stderr(name: str, r, t0: float, slow: float = 60.0) -> None:
+def host_counters() -> dict:
+    """Host-side counters that tell a stalled multi-rank run's story: the
+    cgroup's CPU throttling (cgroup v2 cpu.stat) and TCP retransmissions
+    (/proc/net/snmp) -- what a rank stuck in a socket wait points at."""
+    out = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for ln in f:
+                k, v = ln.split()
+                if k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec"):
+                    out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/proc/net/snmp") as f:
+            rows = [ln.split() for ln in f if ln.startswith("Tcp:")]
+        if len(rows) == 2:
+            tcp = dict(zip(rows[0][1:], rows[1][1:]))
+            out["tcp_retrans_segs"] = int(tcp.get("RetransSegs", 0))
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def _keep_stderr(name: str, r, t0: float, slow: float = 60.0, before: dict = None) -> None:
     """A failed or slow (> `slow` s) multi-rank run's whole stderr (every
     rank's phase timeline and, when the watchdog cut it, every rank's stack
-    dump) to gpurun_out/rehearsal_stderr/ for reading afterwards."""
+    dump) to gpurun_out/rehearsal_stderr/ for reading afterwards, headed by
+    the host counters' change over the run."""
     if r.returncode == 0 and time.time() - t0 < slow:
         return
+    after = host_counters()
+    delta = {k: after[k] - before[k] for k in after if before and k in before}
     d = os.path.join(ROOT, "gpurun_out", "rehearsal_stderr")
     os.makedirs(d, exist_ok=True)
     with open(os.path.join(d, f"{name}_{int(time.time())}.err"), "w") as f:
-        f.write(f"rc {r.returncode} after {time.time() - t0:.1f} s\n" + r.stderr)
+        f.write(f"rc {r.returncode} after {time.time() - t0:.1f} s; host counters over the run: {json.dumps(delta)}\n"
+                + r.stderr)
 
 
 def _explain(r) -> str:
@@ -162,13 +190,13 @@ def _explain(r) -> str:
 def _rehearse(world, inject, *extra, timeout=170):
     env = rehearsal_env(dict(os.environ))
     env["SFL_BENCH_INJECT"] = inject
-    t0 = time.time()
+    t0, before = time.time(), host_counters()
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
                            "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
                            "--host-resident-steps", "0", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "150",
                            *extra],
                           capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
-    _keep_stderr(f"rehearse_{inject.replace(':', '-').replace(',', '_')}", r, t0, slow=45.0)
+    _keep_stderr(f"rehearse_{inject.replace(':', '-').replace(',', '_')}", r, t0, slow=45.0, before=before)
     return r
 
 
