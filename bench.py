@@ -371,6 +371,11 @@ def launch_ranks(args) -> int:
 
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if args.rehearse_one_gpu:
+        # N ranks share one box's CPU quota (a 16-CPU cgroup on the test box,
+        # throttled during rehearsals: DESIGN.md §5); a rank's host work is
+        # small copies, so one OpenMP thread each, as torchrun's own default
+        env["OMP_NUM_THREADS"] = "1"
     tmp = None
     if args.cpu_baseline_seconds > 0:
         cpu = cpu_baseline(args.clients, args.fxp_bits, rank_cpu_seconds(args, args.gpus),
