@@ -49,218 +49,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# PCG64 draw-loop ceilings (tools/microbench/draw_issue.hip,
-# profiles/r01/draw_issue_microbench.txt), the draw loop alone with the
-# product kernel's operand layout and schedule; the first is measured live on
-# the bench's own box when the tool is built (draw_loop_ceilings), this
-# constant is the fallback:
-PCG_PAIR_DRAWS_2WAVE = 1.34e12  # pair draws (both ends accumulated), 2 waves/SIMD = the L=8 kernel's
-                                # occupancy ("dual pair28 E2", best of 1.29-1.34e12 run to run)
-PCG_ONE_DRAWS_8WAVE = 1.57e12   # one-sided draws at 8 waves/SIMD ("dual one7 E2")
-
-
-def pair_seed(u: int, v: int) -> int:
-    a, b = (u, v) if u < v else (v, u)
-    return (0x5ECA66 << 32) | (a << 16) | b
-
-
-def cpu_model() -> str:
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    import platform
-
-    return platform.processor() or "unknown"
-
-
-def cpu_baseline(C: int, fxp_bits: int, seconds: float, parallel: bool = True) -> dict:
-    """The numpy restatement (oracle/, kind "port") timed on this host on a
-    bounded sample of the same workload: C clients, n_sample elements each."""
-    import numpy as np
-
-    from oracle import secagg as o
-
-    names = [f"client{c}" for c in range(C)]
-    seeds = {a: {b: pair_seed(i, j) for j, b in enumerate(names) if b != a} for i, a in enumerate(names)}
-
-    def run(n):
-        xs = [np.random.default_rng(20260116 + c).standard_normal(n, dtype=np.float32) * np.float32(1e-2)
-              for c in range(C)]
-        t0 = time.perf_counter()
-        masked = o.secure_masked(xs, names, None, fxp_bits, seeds)
-        o.server_sum(masked)
-        return time.perf_counter() - t0
-
-    t_cal = run(200_000)
-    n = int(max(200_000, min(50_000_000, 200_000 * seconds / max(t_cal, 1e-6))))
-    t = run(n)
-    par = None
-    if parallel:
-        try:
-            par = cpu_baseline_parallel(C, fxp_bits, n)
-        except Exception as e:  # the single-threaded figure stands on its own
-            par = {"error": repr(e)}
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        cores = os.cpu_count()
-    return {"value": C * n / t, "unit": "grad elems/s", "cores": 1, "kind": "port",
-            "sample": f"{C} clients x {n} fp32 elems, oracle/secagg.py numpy (single-threaded), "
-                      f"{t:.1f} s; host has {cores} cores available",
-            "cpu_model": cpu_model(), "cores_available": cores,
-            "seconds": round(t, 3), "parallel": par}
-
-
-def _cpu_party(args):
-    """One client of the parallel CPU baseline: quantize + its C-1 pairwise
-    masks (oracle/secagg.py numpy, single-threaded), the masked vector written
-    into the shared server buffer.  Returns its timed region (monotonic)."""
-    c, C, n, fxp_bits, shm_name = args
-    from multiprocessing import shared_memory
-
-    import numpy as np
-
-    from oracle import secagg as o
-
-    names = [f"client{i}" for i in range(C)]
-    seeds = {b: pair_seed(c, j) for j, b in enumerate(names) if j != c}
-    x = np.random.default_rng(20260116 + c).standard_normal(n, dtype=np.float32) * np.float32(1e-2)
-    t0 = time.perf_counter()
-    m = o.mask_client(o.quantize(x, None, fxp_bits), names[c], seeds)
-    shm = shared_memory.SharedMemory(name=shm_name)
-    np.ndarray((C, n), dtype=np.uint64, buffer=shm.buf)[c] = m
-    t1 = time.perf_counter()
-    del m
-    shm.close()
-    return t0, t1
-
-
-def cpu_baseline_parallel(C: int, fxp_bits: int, n: int) -> dict:
-    """SURVEY.md §8d's second CPU figure: one process per client (C cores, as
-    the reference runs one party per process), masked vectors into shared
-    memory, then the server sum.  Forked before this process touches the GPU."""
-    import multiprocessing as mp
-    from multiprocessing import shared_memory
-
-    import numpy as np
-
-    from oracle import secagg as o
-
-    shm = shared_memory.SharedMemory(create=True, size=C * n * 8)
-    try:
-        with mp.get_context("fork").Pool(C) as pool:
-            spans = pool.map(_cpu_party, [(c, C, n, fxp_bits, shm.name) for c in range(C)])
-        masked = np.ndarray((C, n), dtype=np.uint64, buffer=shm.buf)
-        t0 = time.perf_counter()
-        o.server_sum(list(masked))
-        t_sum = time.perf_counter() - t0
-        del masked
-    finally:
-        shm.close()
-        shm.unlink()
-    t = max(b for _, b in spans) - min(a for a, _ in spans) + t_sum
-    return {"value": C * n / t, "unit": "grad elems/s", "cores": C, "kind": "port",
-            "sample": f"{C} client processes x {n} fp32 elems (oracle/secagg.py numpy), masked vectors in "
-                      f"shared memory, then the server sum; {t:.1f} s",
-            "seconds": round(t, 3)}
-
-
-PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r04", "r03", "r02", "r01")]  # newest first
-PMC_ELEMS = 100_000_000  # element positions per launch of the committed PMC passes
-
-
-def kernel_key(name: str):
-    """The instantiation a PMC row belongs to: (L, X, K) of a k_clients kernel
-    (K, the variant flags of sa_internal.h, is 0 in round-1 names that carry
-    none), otherwise the bare kernel name.  The variant decides the bytes:
-    k_clients<8, 0, 1> (kBipartite, masks only) moves 16 B per element
-    position, k_clients<8, 0, 4> (kSumOnly) 40 B."""
-    import re
-
-    m = re.search(r"k_clients<float, float, (\d+), (\d+)(?:, (\d+))?>", name)
-    if m:
-        return ("k_clients", int(m.group(1)), int(m.group(2)), int(m.group(3) or 0))
-    name = name.strip()
-    if name.startswith("void "):
-        name = name[5:]
-    return name.split("(")[0].strip()
-
-
-def pmc_traffic(kernel: str, elems_per_launch: int, pmc_elems: int = PMC_ELEMS) -> dict | None:
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (tools/gpu_profile.sh: separate FETCH_SIZE / WRITE_SIZE runs of
-    tools/kernel_bench.py, every per-rank shape at 100M element positions per
-    launch), scaled to this run's launch size (the kernel streams: its bytes
-    are linear in the element count).  Rows are matched on the kernel's full
-    instantiation (kernel_key).  Units are KiB; gfx950 reports FETCH_SIZE at
-    half the bytes of 16-B/lane streaming reads, so it is doubled
-    (MI355X_MICROARCH.md, HBM); both corrections were checked on the
-    k_sum_u64 calibration launch in the same runs (known bytes)."""
-    import csv
-
-    want = kernel_key(kernel)
-    for d in PMC_DIRS:
-        vals = {}
-        for counter, fname, scale in (("FETCH_SIZE", "pmc_fetch_size.csv", 2.0),
-                                      ("WRITE_SIZE", "pmc_write_size.csv", 1.0)):
-            path = os.path.join(d, fname)
-            if not os.path.exists(path):
-                break
-            with open(path) as f:
-                v = [float(r["Counter_Value"]) for r in csv.DictReader(f)
-                     if r["Counter_Name"] == counter and kernel_key(r["Kernel_Name"]) == want]
-            if not v:
-                break
-            vals[counter] = scale * 1024.0 * sum(v) / len(v) * elems_per_launch / pmc_elems
-        if len(vals) == 2:
-            return {"bytes": vals["FETCH_SIZE"] + vals["WRITE_SIZE"], "read": vals["FETCH_SIZE"],
-                    "write": vals["WRITE_SIZE"], "rows_matched": kernel_key(kernel),
-                    "source": os.path.relpath(d, ROOT) + "/pmc_{fetch,write}_size.csv",
-                    "scaled_from_elems": pmc_elems}
-    return None
-
-
-VALU_PEAK_WAVE_INSTR_PER_S = 1024 * 2.4e9 / 4  # 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles
-                                               # at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
-
-
-def pmc_valu(kernel: str, elems_per_launch: int, pmc_elems: int = PMC_ELEMS) -> dict | None:
-    """VALU wave instructions per launch of `kernel` from the committed SQ
-    census (tools/pmc_sq.sh: SQ_INSTS_VALU on tools/kernel_bench.py launches
-    of 100M element positions), matched on the full instantiation and scaled
-    to this run's launch size -- SURVEY.md 8(d)'s "achieved int-op rate"."""
-    import csv
-
-    want = kernel_key(kernel)
-    for d in PMC_DIRS:
-        path = os.path.join(d, "pmc_sq_census.csv")
-        if not os.path.exists(path):
-            continue
-        with open(path) as f:
-            v = [float(r["Counter_Value"]) for r in csv.DictReader(f)
-                 if r["Counter_Name"] == "SQ_INSTS_VALU" and kernel_key(r["Kernel_Name"]) == want]
-        if v:
-            return {"valu_wave_instr": sum(v) / len(v) * elems_per_launch / pmc_elems,
-                    "source": os.path.relpath(path, ROOT) + " (SQ_INSTS_VALU)", "scaled_from_elems": pmc_elems}
-    return None
-
-
-def traffic_field(pmc: dict | None, alg_bytes_per_launch: float):
-    """roofline.traffic from the PMC bytes: never a figure below the
-    algorithmic bytes without saying so (HBM traffic under the bytes the
-    launch must move means the rows belong to another kernel, or the
-    kernel skipped work) -- such a figure is withheld (None) with a note."""
-    if pmc is None:
-        return None, None
-    if pmc["bytes"] < 0.98 * alg_bytes_per_launch:
-        return None, dict(pmc, note=f"PMC bytes {pmc['bytes']:.4g} below the algorithmic "
-                                    f"{alg_bytes_per_launch:.4g} B per launch: withheld")
-    return pmc["bytes"], pmc
+from benchkit.baseline import cpu_baseline, pair_seed, rank_cpu_baseline, rank_cpu_seconds  # noqa: E402,F401
+from benchkit.containment import (Watchdog, control_group, inject_in_design, injected, publish_error,  # noqa: E402,F401
+                                  published_errors, run_contained, run_variants, variant_summary)
+from benchkit.launcher import failing_ranks_report, launch_ranks  # noqa: E402,F401
+from benchkit.roofline import (HBM_PEAK_GBPS, PCG_ONE_DRAWS_8WAVE, PCG_PAIR_DRAWS_2WAVE,  # noqa: E402,F401
+                               PMC_DIRS, PMC_ELEMS, VALU_PEAK_WAVE_INSTR_PER_S, draw_loop_ceilings,
+                               kernel_key, pmc_traffic, pmc_valu, traffic_field)
+from benchkit.standin import HostStandinComm  # noqa: E402,F401
 
 
 # k_clients' variant flags (sfl_amd/csrc/sa_internal.h): the instantiation a
@@ -358,146 +154,6 @@ def other_variants(args, head: Variant) -> list[Variant]:
     return [Variant(v) for v in names if v != head.name]
 
 
-def launch_ranks(args) -> int:
-    """`--gpus N` without an outer torchrun (WORLD_SIZE unset): measure the CPU
-    baseline here, then start the N rank processes as ONE child process
-    (torch.distributed.run with a c10d rendezvous on 127.0.0.1 port 0: the
-    store binds a port the kernel picks, no probe-then-bind race) and return
-    its exit code.  This process never touches the GPU (it imports no torch),
-    so nothing is exec'd from a process that initialised HIP."""
-    import subprocess
-    import tempfile
-    import uuid
-
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    if args.rehearse_one_gpu:
-        # N ranks share one box's CPU quota (a 16-CPU cgroup on the test box,
-        # throttled during rehearsals: DESIGN.md §5); a rank's host work is
-        # small copies, so one OpenMP thread each, as torchrun's own default
-        env["OMP_NUM_THREADS"] = "1"
-    tmp = None
-    if args.cpu_baseline_seconds > 0:
-        cpu = cpu_baseline(args.clients, args.fxp_bits, rank_cpu_seconds(args, args.gpus),
-                           parallel=args.gpus == 1 and not args.dry_run)
-        fd, tmp = tempfile.mkstemp(prefix="sfl_bench_cpu_", suffix=".json")
-        with os.fdopen(fd, "w") as f:
-            json.dump(cpu, f)
-        env["SFL_BENCH_CPU_BASELINE"] = tmp
-    # every rank's stderr also goes to <log_dir>/.../<rank>/stderr.log (and
-    # still to the console, prefixed by the rank), so a failing rank's
-    # traceback survives the interleaving of eight ranks' output; stdout is
-    # left alone (rank 0's JSON line stays a bare line)
-    log_dir = tempfile.mkdtemp(prefix="sfl_bench_ranks_")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
-           "--rdzv-backend", "c10d", "--rdzv-endpoint", "127.0.0.1:0", "--rdzv-id", f"sfl-bench-{uuid.uuid4().hex}",
-           "--local-addr", "127.0.0.1", "--log-dir", log_dir, "--redirects", "2", "--tee", "2",
-           os.path.abspath(__file__), *sys.argv[1:]]
-    try:
-        rc = subprocess.run(cmd, env=env).returncode
-        if rc != 0:
-            sys.stderr.write(failing_ranks_report(log_dir))
-            sys.stderr.flush()
-        return rc
-    finally:
-        if tmp:
-            os.unlink(tmp)
-        import shutil
-
-        shutil.rmtree(log_dir, ignore_errors=True)
-
-
-def failing_ranks_report(log_dir: str, lines_per_rank: int = 60) -> str:
-    """After a failed torchrun child: for every rank whose error file or
-    stderr log holds a traceback, its last traceback (torchrun's error.json
-    from @record first, else the tail of stderr.log from the last
-    'Traceback')."""
-    import glob
-
-    out = []
-    for path in sorted(glob.glob(os.path.join(log_dir, "**", "stderr.log"), recursive=True)):
-        rank_dir = os.path.dirname(path)
-        rank = os.path.basename(rank_dir)
-        text = ""
-        err_json = os.path.join(rank_dir, "error.json")
-        if os.path.exists(err_json):
-            try:
-                with open(err_json) as f:
-                    msg = json.load(f).get("message", {})
-                text = msg.get("extraInfo", {}).get("py_callstack", "") if isinstance(msg, dict) else str(msg)
-            except (OSError, ValueError):
-                text = ""
-        if not text:
-            with open(path, errors="replace") as f:
-                log = f.read()
-            # a Python exception, a fatal signal's stacks (faulthandler is
-            # enabled in every rank) or the watchdog's stack dump at expiry
-            i = max(log.rfind("Traceback (most recent call last)"), log.rfind("Fatal Python error"),
-                    log.rfind("Timeout ("))
-            if i < 0:
-                continue
-            text = log[i:]
-        tail = text.rstrip().splitlines()[-lines_per_rank:]
-        out.append(f"---- bench.py: rank {rank} failed; its last traceback ({os.path.relpath(path, log_dir)}) ----\n"
-                   + "\n".join(tail) + "\n")
-    if not out:
-        return f"---- bench.py: the rank processes failed, no rank left a traceback under {log_dir} ----\n"
-    return "".join(out)
-
-
-def _draw_issue(case: str, waves: int, local_rank: int | None) -> dict | None:
-    import subprocess
-
-    exe = os.path.join(ROOT, "tools", "microbench", "draw_issue")
-    if not os.path.exists(exe):
-        return None
-    env = dict(os.environ)
-    if local_rank is not None:  # this rank's GPU only (an index into the visible list)
-        vis = [v for v in env.get("HIP_VISIBLE_DEVICES", "").split(",") if v]
-        env["HIP_VISIBLE_DEVICES"] = vis[local_rank] if local_rank < len(vis) else str(local_rank)
-    try:
-        r = subprocess.run([exe, case, str(waves)], capture_output=True, text=True, timeout=120, env=env)
-        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
-        return json.loads(line)
-    except (subprocess.SubprocessError, IndexError, ValueError, OSError):
-        return None
-
-
-def draw_loop_ceilings(local_rank: int | None = None) -> dict:
-    """The PCG64 draw loop alone with the masking kernel's operand layout and
-    schedule (tools/microbench/draw_issue: median of 15 launches after 40
-    warm-up ones), measured on THIS rank's GPU in a child process before this
-    process touches the GPU, so roofline.valu compares the kernel with a
-    same-box ceiling (boards differ by a few % in clock under the power
-    limit): pair draws ("dual pair28 E2" at the 8-client kernel's 2
-    waves/SIMD) and one-sided draws ("dual one7 E2" at 8 waves/SIMD, the
-    cross streams' kind).  Missing entries if the tool is absent or fails."""
-    out = {}
-    for kind, case, w in (("pair", "dual pair28 E2", 2), ("one", "dual one7 E2", 8)):
-        r = _draw_issue(case, w, local_rank)
-        if r:
-            out[kind] = r
-    return out
-
-
-def rank_cpu_seconds(args, world: int) -> float:
-    """CPU-baseline budget: the full sample at N=1; a short single-threaded
-    one at N>1 so the scaling runs stay short (it delays rank 0 only)."""
-    return args.cpu_baseline_seconds if world == 1 else min(3.0, args.cpu_baseline_seconds)
-
-
-def rank_cpu_baseline(args, world: int, rank: int):
-    """rank 0's CPU baseline, always measured before this process touches the
-    GPU: handed over by the launcher (launch_ranks) or measured here."""
-    if rank != 0 or args.cpu_baseline_seconds <= 0:
-        return None
-    path = os.environ.get("SFL_BENCH_CPU_BASELINE")
-    if path and os.path.exists(path):
-        with open(path) as f:
-            return json.load(f)
-    return cpu_baseline(args.clients, args.fxp_bits, rank_cpu_seconds(args, world), parallel=world == 1)
-
-
 def dry_run(args, world: int, rank: int, cpu, wd: Watchdog) -> None:
     """Launcher rehearsal without a GPU (tests/test_bench_launcher.py): every
     rank joins a gloo group and reports its pid, then the N > 1 design
@@ -536,7 +192,7 @@ def dry_run(args, world: int, rank: int, cpu, wd: Watchdog) -> None:
         def summarise(x):
             return dict(variant_summary(x), workload=workload(args, world, Variant(x["name"])))
 
-        run_variants(ctx, dry_design, others, summarise, line, wd)
+        run_variants(ctx, dry_design, others, summarise, line, wd, settle=combine_check)
     else:
         line["check"]["decoded_digest"] = f"{check_local:016x}"
     wd.enter("done")
@@ -606,416 +262,6 @@ def collective_text(v: Variant) -> str:
                 "(k_decode), both on the comm stream" + (", float64 shards gathered to rank 0 (ncclSend/Recv)"
                                                         if v.gather else ""))
     return "ncclReduce(uint64, sum) in place to rank 0"
-
-
-class HostStandinComm:
-    """--rehearse-one-gpu only: RcclComm's contract (reduce_u64,
-    reduce_scatter_u64, alltoall_u64, gather_f64) for N rank processes on
-    ONE GPU (RCCL refuses two ranks on one device: "Duplicate GPU detected"),
-    so every design's code path runs.  Everything moves through memory shared
-    by the ranks on this host: every rank writes its host copy of the send
-    buffer into its slot, a barrier, every rank reads what the collective
-    gives it, a second barrier before the slots are reused.  The barrier is
-    in the shared memory too (each rank publishes an epoch in its own cache
-    line and waits for every rank's), so the data path touches no socket:
-    round 4's W = 8 rehearsals now and then sat for 30-50 s inside one gloo
-    all_reduce / barrier on every rank at once.  gloo only
-    sets the mappings up.  Called on the comm stream like RcclComm;
-    ``send.cpu()`` waits for the chunk's launch.  Its timings are host
-    copies, not xGMI: a rehearsal checks the N > 1 control flow, never the
-    rate."""
-
-    def __init__(self, rank: int, world: int, group=None):
-        import tempfile
-
-        import numpy as np
-        import torch.distributed as dist
-
-        self.rank, self.world, self.group = rank, world, group
-        # /dev/shm keeps the slots in memory (a disk-backed /tmp file made the
-        # full-size W = 8 rehearsal write back GBs per step); each file is
-        # unlinked as soon as every rank has mapped it, so nothing is left
-        # behind however a rank ends
-        base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
-        box = [os.path.join(base, f"sfl_rehearsal_{os.getpid()}") if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0, group=group)
-        self.prefix, self.cap, self.gen, self.mm, self.epoch = box[0], 0, 0, None, 0
-        self.ctl = self._shared((world, 8), np.int64)  # [r, 0]: rank r's barrier epoch
-
-    def _shared(self, shape, dtype):
-        """A new zeroed mapping of ``shape`` shared by every rank (collective)."""
-        import numpy as np
-        import torch.distributed as dist
-
-        path = f"{self.prefix}_{self.gen}"
-        self.gen += 1
-        if self.rank == 0:
-            with open(path, "wb") as f:
-                f.truncate(int(np.prod(shape)) * np.dtype(dtype).itemsize)
-        dist.barrier(group=self.group)
-        mm = np.memmap(path, dtype=dtype, mode="r+", shape=shape)
-        dist.barrier(group=self.group)
-        if self.rank == 0:
-            os.unlink(path)  # the mappings keep the pages until every rank drops them
-        return mm
-
-    def _barrier(self):
-        """Every rank has reached the same epoch.  Each rank's epoch word has
-        one writer; x86 keeps stores in order, so a rank that sees another's
-        epoch also sees the slot bytes that rank wrote before it."""
-        self.epoch += 1
-        self.ctl[self.rank, 0] = self.epoch
-        col = self.ctl[:, 0]
-        spins = 0
-        while int(col.min()) < self.epoch:
-            spins += 1
-            time.sleep(0 if spins < 200 else 50e-6)
-
-    def _slots(self, nbytes: int):
-        """The (world, cap) byte view of the shared slots, grown (collectively:
-        every rank asks for the same size) when an op needs more."""
-        import numpy as np
-
-        if nbytes > self.cap:
-            self.cap = max(nbytes, 2 * self.cap)
-            self.mm = None
-            self.mm = self._shared((self.world, self.cap), np.uint8)
-        return self.mm
-
-    def _post(self, t):
-        """This rank's host copy of ``t`` into its slot; then every rank's slots
-        are readable.  Returns (slots, nbytes)."""
-        import numpy as np
-
-        host = t.cpu().numpy()  # on the comm stream: waits for the chunk's launch
-        nb = host.nbytes
-        mm = self._slots(nb)
-        mm[self.rank, :nb] = host.reshape(-1).view(np.uint8)  # a shared mapping: no msync needed between processes
-        self._barrier()
-        return mm, nb
-
-    def reduce_u64(self, send, recv, root: int = 0):
-        import numpy as np
-        import torch
-
-        mm, nb = self._post(send)
-        if self.rank == root:
-            total = np.sum(mm[:, :nb].view(np.uint64), axis=0, dtype=np.uint64)  # wraps mod 2^64
-            (recv if recv is not None else send).copy_(torch.from_numpy(total.view(np.int64)))
-        self._barrier()
-        return recv
-
-    def reduce_scatter_u64(self, send, recv):
-        import numpy as np
-        import torch
-
-        if send.numel() != recv.numel() * self.world:
-            raise ValueError("reduce_scatter: shard sizes")
-        mm, nb = self._post(send)
-        k = recv.numel()
-        part = mm[:, :nb].view(np.uint64)[:, self.rank * k:(self.rank + 1) * k]
-        recv.copy_(torch.from_numpy(np.sum(part, axis=0, dtype=np.uint64).view(np.int64)))
-        self._barrier()
-        return recv
-
-    def alltoall_u64(self, send, recv):
-        import numpy as np
-        import torch
-
-        mm, nb = self._post(send)
-        k = send.numel() // self.world
-        slots = mm[:, :nb].view(np.int64)
-        for p in range(self.world):
-            if p != self.rank:
-                recv[p * k:(p + 1) * k].copy_(torch.from_numpy(np.array(slots[p, self.rank * k:(self.rank + 1) * k])))
-        self._barrier()
-        return recv
-
-    def gather_f64(self, send, recv, root: int = 0):
-        import numpy as np
-        import torch
-
-        mm, nb = self._post(send)
-        if self.rank == root:
-            recv.copy_(torch.from_numpy(np.array(mm[:, :nb].view(np.float64)).reshape(-1)))
-        self._barrier()
-        return recv
-
-    def close(self):
-        self.mm = None  # the slot files are unlinked already: dropping the mapping frees them
-        self._barrier()
-
-
-# ------------------------------------------------ failure containment (N > 1)
-#
-# The driver's N > 1 run is the only place the exchange designs meet xGMI, so
-# one bad design must not cost the line: the headline (the reduce-scatter
-# sharded server, the design with the most evidence) runs FIRST, every other
-# design runs inside `run_variants` (an exception is recorded in its
-# exchange_variants entry; the ranks agree over a gloo control group before
-# the next one), and the watchdog thread prints the line built so far when a
-# design hangs.  SFL_BENCH_INJECT rehearses each failure (tests only):
-#   fail:<design>[@<rank>]   run_design of <design> raises (on one rank or all)
-#   hang:<design>[@<rank>]   run_design of <design> never returns
-#   raise:rank<r>            rank r raises at start-up, before any collective
-#   corrupt:<design>[@<rank>] the design's round-0 result check is off by one bit
-
-def injected(kind: str, design: str | None, rank: int) -> bool:
-    """Whether SFL_BENCH_INJECT asks for failure ``kind`` here (see above)."""
-    spec = os.environ.get("SFL_BENCH_INJECT", "")
-    for item in filter(None, spec.split(",")):
-        k, _, rest = item.partition(":")
-        if k != kind:
-            continue
-        if kind == "raise":
-            if rest == f"rank{rank}":
-                return True
-            continue
-        name, _, r = rest.partition("@")
-        if name == design and (not r or int(r) == rank):
-            return True
-    return False
-
-
-def inject_in_design(v_name: str, rank: int) -> None:
-    if injected("fail", v_name, rank):
-        raise RuntimeError(f"SFL_BENCH_INJECT: injected failure in design {v_name!r} on rank {rank}")
-    if injected("hang", v_name, rank):
-        print(f"bench.py rank {rank}: SFL_BENCH_INJECT: design {v_name!r} hangs", file=sys.stderr, flush=True)
-        while True:
-            time.sleep(3600)
-
-
-class Watchdog:
-    """Bounds a rank's run and keeps its measurement.
-
-    * A design other than the headline that runs longer than
-      ``variant_timeout`` seconds (or the run nearing ``total`` seconds after
-      the headline finished) is declared hung: rank 0 prints the line built
-      so far with that design marked and ``variants_incomplete``, every rank
-      dumps its threads' stacks to stderr and exits 0 -- the headline stands.
-    * Before the headline has finished there is nothing to keep: at
-      ``total`` seconds ``faulthandler`` (a C thread, which fires even while
-      the main thread holds the GIL) dumps every stack and exits 1.
-
-    A Python thread, polled every 0.25 s: it runs while the main thread waits
-    in a GIL-releasing call (a ctypes RCCL call, a device synchronise, a
-    c10d wait), which is where a hung collective leaves it."""
-
-    def __init__(self, total: float, variant_timeout: float, rank: int):
-        import threading
-
-        self.total, self.variant_timeout, self.rank = total, variant_timeout, rank
-        self.t0 = time.monotonic()
-        self.phase, self.t_phase = "setup", self.t0
-        self.line = None        # rank 0's line so far, once the headline has finished
-        self.pending = []       # designs not yet run
-        self.lock = threading.Lock()
-        self.printed = False
-        if total > 0:
-            import faulthandler
-
-            faulthandler.dump_traceback_later(total, exit=True)
-            threading.Thread(target=self._loop, name="bench-watchdog", daemon=True).start()
-
-    def enter(self, phase: str) -> None:
-        with self.lock:
-            self.phase, self.t_phase = phase, time.monotonic()
-            if phase in self.pending:
-                self.pending.remove(phase)
-        if os.environ.get("SFL_BENCH_TRACE"):  # phase timeline on stderr (the rehearsal tests set it)
-            print(f"bench.py rank {self.rank}: phase {phase} at {self.t_phase - self.t0:.1f} s", file=sys.stderr,
-                  flush=True)
-
-    def emit(self, line: dict) -> bool:
-        """Print ``line`` (rank 0), once per process."""
-        with self.lock:
-            if self.printed:
-                return False
-            self.printed = True
-        print(json.dumps(line), flush=True)
-        return True
-
-    def _loop(self):
-        warned = False
-        while True:
-            time.sleep(0.25)
-            now = time.monotonic()
-            with self.lock:
-                phase, t_phase, line = self.phase, self.t_phase, self.line
-            left = self.total - (now - self.t0)
-            if line is not None and phase not in ("headline", "done") and (
-                    now - t_phase > self.variant_timeout or left < 10):
-                self._give_up(phase, now - t_phase)
-            if line is None and left < 3 and not warned:
-                warned = True
-                print(f"bench.py rank {self.rank}: headline not finished after {self.total - 3:.0f} s; "
-                      f"dumping every thread's stack and exiting", file=sys.stderr, flush=True)
-
-    def _give_up(self, phase: str, waited: float):
-        import copy
-        import faulthandler
-
-        with self.lock:
-            line = copy.deepcopy(self.line)
-            pending = list(self.pending)
-        msg = (f"design {phase!r} did not finish within {waited:.0f} s on rank {self.rank} (hung); every rank's "
-               f"stacks are on stderr; the headline and the designs before it stand")
-        errs = published_errors(phase) if self.rank == 0 else []
-        if errs:  # a rank that raised left its peers waiting in the design's collectives
-            msg += "; errors raised by ranks: " + "; ".join(errs)
-        print(f"bench.py rank {self.rank}: {msg}", file=sys.stderr, flush=True)
-        if self.rank == 0 and phase == "check":  # the headline's result check hung: the designs after it never ran
-            line["check"]["error"] = "hung"
-            line["check"]["detail"] = msg
-            line["variants_incomplete"] = True
-            self.emit(line)
-        elif self.rank == 0 and phase == "host_resident":  # after every design: only this field is lost
-            line["host_resident"] = {"error": "hung", "detail": msg}
-            self.emit(line)
-        elif self.rank == 0:
-            line.setdefault("exchange_variants", []).append({"name": phase, "error": "hung", "detail": msg})
-            line["exchange_variants"] += [{"name": p, "error": "skipped", "detail": f"not run: {phase!r} hung"}
-                                          for p in pending]
-            line["variants_incomplete"] = True
-            self.emit(line)
-        faulthandler.dump_traceback(all_threads=True)
-        sys.stderr.flush()
-        os._exit(0)
-
-
-def _store():
-    """The process group's c10d store (torchrun's TCPStore): independent of
-    the collectives, so a rank can leave a message there that rank 0 can read
-    while a design's collectives hang."""
-    try:
-        import torch.distributed as dist
-
-        if dist.is_initialized():
-            return dist.distributed_c10d._get_default_store()
-    except Exception:  # noqa: BLE001 -- best effort, the line does not depend on it
-        pass
-    return None
-
-
-def publish_error(design: str, rank: int, text: str) -> None:
-    s = _store()
-    if s is not None:
-        try:
-            s.set(f"sfl_bench_err/{design}/{rank}", text)
-        except Exception:  # noqa: BLE001
-            pass
-
-
-def published_errors(design: str, world: int | None = None) -> list[str]:
-    s = _store()
-    if s is None:
-        return []
-    world = world or int(os.environ.get("WORLD_SIZE", "1"))
-    out = []
-    for r in range(world):
-        key = f"sfl_bench_err/{design}/{r}"
-        try:
-            if s.check([key]):
-                out.append(s.get(key).decode(errors="replace"))
-        except Exception:  # noqa: BLE001
-            pass
-    return out
-
-
-def control_group(ctx):
-    """A gloo group for agreement between designs: CPU tensors, so it still
-    works when a design left the GPU streams or the RCCL communicator
-    unusable."""
-    import torch.distributed as dist
-
-    if ctx.get("ctrl") is None:
-        ctx["ctrl"] = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
-    return ctx["ctrl"]
-
-
-def run_variants(ctx, runner, variants, summarise, out: dict, wd: Watchdog) -> None:
-    """Every design after the headline, each contained: an exception on any
-    rank is printed there (traceback on stderr) and recorded in its entry of
-    out["exchange_variants"]; the ranks agree (gloo all_gather of the error
-    texts) before the next design.  A design that failed on EVERY rank left
-    no collective half-issued, so the next one runs; one that failed on some
-    ranks only may have left the others' exchange pending, so the remaining
-    designs are skipped and the line printed as it stands."""
-    import traceback
-
-    import torch.distributed as dist
-
-    args, rank = ctx["args"], ctx["rank"]
-    group = control_group(ctx)
-    with wd.lock:
-        wd.pending = [v.name for v in variants]
-    for i, v in enumerate(variants):
-        wd.enter(v.name)
-        err = None
-        try:
-            res = runner(ctx, v, args.variant_steps, min(5, args.warmup))
-            combine_check(ctx, res)
-        except Exception as e:  # noqa: BLE001 -- contained, reported in the line
-            err = f"rank {rank}: {e!r}"
-            print(f"bench.py rank {rank}: design {v.name!r} failed:", file=sys.stderr)
-            traceback.print_exc()
-            sys.stderr.flush()
-            publish_error(v.name, rank, err)
-        errs = [None] * ctx["world"]
-        dist.all_gather_object(errs, err, group=group)
-        failed = [e for e in errs if e is not None]
-        with wd.lock:
-            if not failed:
-                entry = summarise(res)
-                want = out.get("check", {}).get("decoded_digest")
-                if want is not None and entry.get("check_digest") is not None and entry["check_digest"] != want:
-                    entry["mismatch"] = f"round-0 result check {entry.get('check_digest')} != the headline's {want}"
-                    out["designs_agree"] = False
-                out["exchange_variants"].append(entry)
-                continue
-            out["exchange_variants"].append({"name": v.name, "error": "failed", "detail": "; ".join(failed)})
-            if len(failed) < ctx["world"]:
-                rest = [x.name for x in variants[i + 1:]]
-                out["exchange_variants"] += [{"name": p, "error": "skipped",
-                                              "detail": f"not run: {v.name!r} failed on some ranks only"}
-                                             for p in rest]
-                out["variants_incomplete"] = True
-                wd.pending = []
-                return
-    with wd.lock:
-        wd.pending = []
-
-
-def run_contained(ctx, phase: str, fn, out: dict, wd: Watchdog) -> None:
-    """One more measurement after the designs, contained like them: its
-    result (or the ranks' errors) goes to out[phase]; a hang is the
-    watchdog's (phase named)."""
-    import traceback
-
-    import torch.distributed as dist
-
-    wd.enter(phase)
-    err, res = None, None
-    try:
-        res = fn()
-    except Exception as e:  # noqa: BLE001 -- contained, reported in the line
-        err = f"rank {ctx['rank']}: {e!r}"
-        traceback.print_exc()
-        publish_error(phase, ctx["rank"], err)
-    errs = [None] * ctx["world"]
-    dist.all_gather_object(errs, err, group=control_group(ctx))
-    failed = [e for e in errs if e is not None]
-    with wd.lock:
-        out[phase] = {"error": "failed", "detail": "; ".join(failed)} if failed else res
-
-
-def variant_summary(x: dict) -> dict:
-    return {"name": x["name"], "value": x["value"], "ms_per_step": x["ms_per_step"], "steps": x["steps"],
-            "kernel_ms_per_step": x["kernel_ms_per_step"], "kernel": x["kernel"], "chunks": x["chunks"],
-            "xchg_ms": x["exchange"]["ms_per_step"], "bytes_per_rank_per_step": x["exchange"]["bytes_per_rank_per_step"],
-            "algbw_GBps": x["exchange"]["algbw_GBps"], "busbw_GBps": x["exchange"]["busbw_GBps"],
-            "collective": x["exchange"]["collective"], "check_digest": x.get("check_digest")}
 
 
 def dry_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
@@ -1378,7 +624,7 @@ def main():
             ap.error(f"--variants: unknown design {v!r} (choose from {', '.join(VARIANTS)})")
 
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dist):
-        sys.exit(launch_ranks(args))
+        sys.exit(launch_ranks(args, __file__))
     # a rank: an uncaught exception is written to torchrun's error file, so
     # the launcher's failure summary names this rank and shows its traceback
     from torch.distributed.elastic.multiprocessing.errors import record
@@ -1515,7 +761,7 @@ def rank_main(args):
         with wd.lock:
             wd.line = out if rank == 0 else {}
         settle_check(ctx, r, check_local, out, wd)
-        run_variants(ctx, run_design, other_variants(args, head), variant_summary, out, wd)
+        run_variants(ctx, run_design, other_variants(args, head), variant_summary, out, wd, settle=combine_check)
         if args.host_resident_steps > 0 and head.name == "sharded" and not out.get("variants_incomplete"):
             run_contained(ctx, "host_resident", lambda: run_host_resident(
                 ctx, args.host_resident_steps, min(3, args.warmup)), out, wd)

@@ -6,7 +6,7 @@ un-vendored third-party package ``secretflow-lite==1.13.0b0`` pinned at
 ``/root/reference/pyproject.toml:51`` and ``uv.lock:2008-2009``).  It is the
 checker the HIP path is compared against; it is never the thing measured or
 shipped.  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
-``cpu_baseline`` leg may import it.  The product path (``sfl_amd``) must never
+``cpu_baseline`` leg (``benchkit/baseline.py``) may import it.  The product path (``sfl_amd``) must never
 import this file — ``tests/test_boundary.py`` enforces that.
 
 Where the algorithm is pinned (all paths relative to /root/reference):

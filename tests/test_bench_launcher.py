@@ -134,7 +134,7 @@ def test_n_gt_1_line_names_every_exchange_design_and_a_safe_launch():
     ports = {x["master_port"] for x in line["ranks"]}
     assert len(ports) == 1 and None not in ports
     assert 0 < line["watchdog_seconds"] < 600
-    src = open(BENCH).read()
+    src = open(os.path.join(ROOT, "benchkit", "launcher.py")).read()
     assert ".bind(" not in src and "--master-port" not in src.split("def launch_ranks")[1].split("def ")[0]
     # a subset, and the headline taken from the flags
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--cpu-baseline-seconds", "0",

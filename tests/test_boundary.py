@@ -131,6 +131,17 @@ def test_product_never_imports_the_oracle():
                 assert "oracle/" not in src.replace("oracle/_ref", ""), f
 
 
+def test_bench_runs_the_oracle_only_in_its_cpu_baseline_leg():
+    """bench.py's measured path never touches the oracle: its only importer
+    under bench.py / benchkit/ is the cpu_baseline leg (benchkit/baseline.py)."""
+    srcs = {"bench.py": os.path.join(ROOT, "bench.py")}
+    for f in os.listdir(os.path.join(ROOT, "benchkit")):
+        if f.endswith(".py"):
+            srcs[f"benchkit/{f}"] = os.path.join(ROOT, "benchkit", f)
+    users = {k for k, p in srcs.items() if re.search(r"^\s*(from|import)\s+oracle", open(p).read(), re.M)}
+    assert users == {"benchkit/baseline.py"}
+
+
 def test_missing_library_fails_loudly(tmp_path, monkeypatch):
     import importlib
 
