@@ -26,6 +26,7 @@ class HostStandinComm:
 
     def __init__(self, rank: int, world: int, group=None):
         import tempfile
+        import uuid
 
         import numpy as np
         import torch.distributed as dist
@@ -36,7 +37,7 @@ class HostStandinComm:
         # unlinked as soon as every rank has mapped it, so nothing is left
         # behind however a rank ends
         base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
-        box = [os.path.join(base, f"sfl_rehearsal_{os.getpid()}") if rank == 0 else None]
+        box = [os.path.join(base, f"sfl_rehearsal_{os.getpid()}_{uuid.uuid4().hex[:12]}") if rank == 0 else None]
         dist.broadcast_object_list(box, src=0, group=group)
         self.prefix, self.cap, self.gen, self.mm, self.epoch = box[0], 0, 0, None, 0
         self.ctl = self._shared((world, 8), np.int64)  # [r, 0]: rank r's barrier epoch
