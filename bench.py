@@ -746,8 +746,9 @@ def rank_main(args):
                               "issue": int_ops}},
     }
     if rehearse:
-        out["rehearsal"] = ("--rehearse-one-gpu: every rank on cuda:0, collectives through a shared host mapping "
-                            "with gloo barriers; the N > 1 control flow, not the product's rate")
+        out["rehearsal"] = ("--rehearse-one-gpu: every rank on cuda:0, collectives and their barriers through a "
+                            "shared host mapping (benchkit/standin.py); the N > 1 control flow, not the "
+                            "product's rate")
     out["cpu_baseline"] = cpu
     check_local = r.pop("check_local")
     out["check"] = {"round": 0, "decoded_digest": None, "note": CHECK_NOTE}
