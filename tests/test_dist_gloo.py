@@ -191,7 +191,7 @@ def _standin_worker(rank, world, init, q):
 @pytest.mark.parametrize("world", [2, 3])
 def test_host_standin_comm_matches_the_collectives(world):
     """bench.HostStandinComm (the one-GPU rehearsal's stand-in for RcclComm:
-    data through a shared file mapping, gloo barriers) gives what the
+    data and barriers through a shared mapping) gives what the
     collectives it stands in for give: reduce-scatter shards of the uint64
     sum, the alltoall slots (own slot untouched), the in-place uint64
     reduce to a root, the float64 gather -- also after its slots grow."""

@@ -4,7 +4,7 @@ self-launcher, W torchrun ranks, every design's code path in run_design
 (client sharding with the pipelined sharded server, its gather, the reduce
 to rank 0, element sharding with and without the gather) and the max-over-
 ranks timing, with the collectives through a host stand-in (bench.HostStandinComm:
-a file mapping shared by the ranks, gloo barriers) because
+a mapping shared by the ranks, barriers included) because
 RCCL refuses two ranks on one GPU ("Duplicate GPU detected",
 tools/rccl_two_ranks_one_gpu.py).  RCCL itself runs at world 1 in
 tests/test_gpu_rccl.py; the data path of every rank is checked against the

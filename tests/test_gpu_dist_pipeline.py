@@ -5,8 +5,8 @@ the one GPU of the test box.
 
 RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so the
 exchange here is bench.py's rehearsal stand-in with RcclComm's contract
-(``HostStandinComm``: the ranks' host copies through a shared file mapping,
-gloo barriers): on the comm stream, after the chunk's event, the partial
+(``benchkit.standin.HostStandinComm``: the ranks' host copies and barriers
+through a shared mapping): on the comm stream, after the chunk's event, the partial
 sum is reduced to the root IN PLACE (recv=None) -- uint64 addition mod
 2^64.  Everything else is the product code path the N > 1 bench
 runs.  The root's buffer must equal the oracle's server sum bit for bit, and
