@@ -346,3 +346,14 @@ def test_position_digest_matches_numpy_and_sees_permutations():
     assert (bench.position_digest(t[:k], 0) + bench.position_digest(t[k:], k)) % 2**64 == want
     y = np.concatenate([x[k:2 * k], x[:k], x[2 * k:]])  # two shards swapped
     assert bench.position_digest(torch.from_numpy(y), 0) != want
+
+
+def test_importing_the_bench_loads_no_torch():
+    """The self-launcher process must not touch the GPU before it starts its
+    rank processes (nothing may be exec'd from a process that initialised
+    HIP): importing bench.py and benchkit/ loads no torch."""
+    code = ("import sys; sys.path.insert(0, %r); import bench, benchkit.launcher, benchkit.containment, "
+            "benchkit.standin, benchkit.roofline, benchkit.baseline; "
+            "assert 'torch' not in sys.modules, sorted(m for m in sys.modules if m.startswith('torch'))[:5]" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
