@@ -58,16 +58,35 @@ def oracle_check(C: int, n: int, fxp_bits: int = 18) -> str:
     return f"{int(np.sum(dec.view(np.uint64) * h, dtype=np.uint64)):016x}"
 
 
+def has_gpu() -> bool:
+    """A GPU is visible -- asked without initialising HIP in this process
+    (device_count does not; is_available does, on this image)."""
+    return torch.cuda.device_count() > 0
+
+
+def oracle_check_in_child(C: int, n: int) -> str:
+    """oracle_check computed in a child process, so that THIS process (the
+    test runner, which starts the rank processes) holds no GPU context while
+    the W rank processes run: W + 1 processes on the one GPU (9 at W = 8)
+    is the suspected cause of the rehearsals that ran ~10x slower (DESIGN.md
+    §5); conftest.py runs this module first for the same reason."""
+    code = ("import sys; sys.path[:0] = [%r, %r]; from test_gpu_bench_rehearsal import oracle_check; "
+            "print(oracle_check(%d, %d))" % (os.path.join(ROOT, "tests"), ROOT, C, n))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=170, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return r.stdout.split()[-1]
+
+
 @pytest.fixture(scope="module")
 def check_1m():
-    if not torch.cuda.is_available():
+    if not has_gpu():
         pytest.skip("no GPU")
-    return oracle_check(8, 1000003)
+    return oracle_check_in_child(8, 1000003)
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_n_ranks_every_design(world, check_1m):
-    if not torch.cuda.is_available():
+    if not has_gpu():
         pytest.skip("no GPU")
     env = rehearsal_env(dict(os.environ))
     t0, before = time.time(), host_counters()
@@ -120,7 +139,7 @@ def test_bench_n1_line(check_1m):
     """The driver's N = 1 bench path at a small size: one JSON line with the
     contract's fields; one launch per step timed by one event pair around
     the timed region (kernel time <= wall time per step)."""
-    if not torch.cuda.is_available():
+    if not has_gpu():
         pytest.skip("no GPU")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--elems", "1000003", "--steps", "5",
                         "--warmup", "2", "--cpu-baseline-seconds", "0"],
@@ -205,7 +224,7 @@ def test_bench_8_ranks_keeps_headline_when_designs_fail_or_hang():
     `direct` raising on every rank is recorded with its error and the run
     goes on; `elements` hanging makes rank 0 print the line so far once the
     variant timeout passes, `elements+gather` marked skipped, exit 0."""
-    if not torch.cuda.is_available():
+    if not has_gpu():
         pytest.skip("no GPU")
     r = _rehearse(8, "fail:direct,hang:elements", "--variant-timeout", "8")
     assert r.returncode == 0, _explain(r)
@@ -220,7 +239,7 @@ def test_bench_8_ranks_keeps_headline_when_designs_fail_or_hang():
 def test_bench_8_ranks_failing_rank_names_itself():
     """A rank that fails puts its own traceback at the end of the launcher's
     stderr (per-rank logs + torchrun's error file), not 8 ranks' banners."""
-    if not torch.cuda.is_available():
+    if not has_gpu():
         pytest.skip("no GPU")
     r = _rehearse(8, "raise:rank3")
     assert r.returncode != 0
@@ -230,9 +249,9 @@ def test_bench_8_ranks_failing_rank_names_itself():
 
 @pytest.fixture(scope="module")
 def check_100m():
-    if not torch.cuda.is_available():
+    if not has_gpu():
         pytest.skip("no GPU")
-    return oracle_check(8, 100_000_000)
+    return oracle_check_in_child(8, 100_000_000)
 
 
 def _full_size_line(*extra, timeout=150):
