@@ -17,11 +17,11 @@ def golden_dir():
     return os.path.join(ROOT, "tests", "golden")
 
 
-# Run first: the one-GPU N > 1 rehearsals put W rank processes on the box's
-# one GPU, so the test process must not hold a GPU context of its own yet
-# (W + 1 processes at W = 8 is the suspected cause of rehearsals running ~10x
-# slower); those tests never initialise HIP here themselves.
-_FIRST = ("test_gpu_bench_rehearsal.py",)
+# Run first: these put W rank processes on the box's one GPU, so the test
+# process must not hold a GPU context of its own yet (W + 1 processes at
+# W = 8 is the suspected cause of rehearsals running ~10x slower, DESIGN.md
+# §5); these modules never initialise HIP in the test process themselves.
+_FIRST = ("test_gpu_bench_rehearsal.py", "test_gpu_dist_pipeline.py")
 
 
 def pytest_collection_modifyitems(session, config, items):
