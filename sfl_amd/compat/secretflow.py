@@ -1,40 +1,46 @@
 """Reference-side import path: the HIP ``SecureAggregator`` for code written
-against ``secretflow`` (missing 5).
+against ``secretflow``.
 
 Callers import ``from secretflow.security import SecureAggregator``
 (``tests/ml/nn/fl/strategy/test_moon_torch.py:17``,
 ``sfl/security/aggregation/stateful_fedgen_aggregator.py:20``) and hand it
-secretflow devices and device objects: ``PYU`` objects carrying ``.party``,
-``PYUObject`` objects carrying ``.device`` whose value the driver fetches
-with ``sf.reveal`` (simulation mode), and results that come back as objects
-on the server device.  This module accepts exactly those shapes, duck-typed
-(secretflow itself is not installed here):
+secretflow devices (``PYU``: ``.party``, ``pyu(fn, num_returns=k)(*args)``
+runs ``fn`` in that party's process) and device objects (``.device``,
+``.to(dev)``).  This class keeps the reference protocol's placement
+(``docs/developer/algorithm/secure_aggregation.ipynb:227-258``):
 
-* ``SecureAggregator(device, participants, fxp_bits=18)`` -- the reference
-  constructor; devices map to ``sfl_amd.device.PYU`` by party name, each on
-  the GPU ``gpu_of(party)`` picks (default: every party on GPU 0, the
-  single-node simulation);
-* ``sum(data, axis)`` / ``average(data, axis, weights)`` -- data are
-  secretflow-shaped objects (or already ``sfl_amd`` ones); their values
-  are fetched with ``reveal`` (default: ``secretflow.reveal`` when
-  importable), weights may be plain numbers / arrays or device objects on
-  the matching party (``stateful_fedgen_aggregator.py:74-78`` puts them on
-  the client's device);
-* the result is wrapped back onto the server device with ``wrap(device,
-  value)`` (default: ``device(lambda v: v)(value)``, which is how a
-  secretflow ``PYU`` creates a ``PYUObject`` it owns).
+* **set-up** -- one masker per participant, created by the participant's
+  own device (``party(new_masker)``); the driver reveals the DH *public*
+  keys only and hands them back to every participant (``party(agree)``).
+  No private key, seed or generator state ever reaches the driver;
+* **mask** -- ``d.device(mask_payload, num_returns=2)(masker, d, w)`` runs
+  the quantize + mask on the party's GPU (``sa_mask``); a device-object
+  weight is used through its own device, as
+  ``stateful_fedgen_aggregator.py:74-85`` does;
+* **move** -- only the masked uint64 payload leaves a client, with
+  ``.to(server)`` (``sparse_plain_aggregator.py:86``); a device-object
+  weight is moved to the server for ``sum(w)``;
+* **sum + decode** -- ``server(sum_decode)(*masked, ...)`` on the server's
+  GPU (``sa_sum_u64`` + ``sa_decode``); the result is the server-owned
+  device object the reference returns.
 
-``install(module)`` rebinds ``module.SecureAggregator`` (e.g.
-``secretflow.security.aggregation`` or ``secretflow.security``), so existing
-call sites pick up the HIP path unchanged; INTEGRATION.md §5 shows it.
+Nothing here reveals a client's data: ``tests/test_compat_secretflow.py``
+runs every party in a spawned process behind a ``reveal`` that raises on
+any client-owned value but a public key.
+
+``install()`` rebinds ``SecureAggregator`` in ``secretflow.security`` and
+``secretflow.security.aggregation`` (both import paths the reference uses).
+It must run before any module that SUBCLASSES the class is imported
+(``StatefulFedGenAggregator`` fixes its base at class definition); it
+raises if such a subclass already exists.
 """
 
 from __future__ import annotations
 
+import sys
 from typing import Callable, List, Optional
 
-from ..device import PYU, PYUObject, reveal as _reveal_local
-from ..security.aggregation import SecureAggregator as _HipSecureAggregator
+from ..security.aggregation import party as P
 
 
 def _default_reveal():
@@ -43,86 +49,102 @@ def _default_reveal():
 
         return sf.reveal
     except ImportError:
-        return None
+        from ..device import reveal
 
-
-def _default_wrap(device, value):
-    return device(lambda v: v)(value)
+        return reveal
 
 
 class SecureAggregator:
-    """secretflow-shaped front of the HIP secure aggregator."""
+    """secretflow-shaped HIP secure aggregator (masks inside each party)."""
 
     def __init__(self, device, participants: List, fxp_bits: int = 18, *,
-                 reveal: Optional[Callable] = None, wrap: Optional[Callable] = None,
-                 gpu_of: Optional[Callable[[str], int]] = None, **kwargs):
-        self._sf_device = device
-        self._sf_participants = list(participants)
+                 reveal: Optional[Callable] = None, gpu_of: Optional[Callable[[str], int]] = None,
+                 seeds: Optional[dict] = None):
+        assert participants, "participants should not be empty"
+        names = [_party(p) for p in participants]
+        assert len(set(names)) == len(names), f"duplicate participants: {names}"
+        _party(device)
+        self._device = device
+        self._participants = list(participants)
+        self._fxp_bits = int(fxp_bits)
         self._reveal = reveal or _default_reveal()
-        self._wrap = wrap or _default_wrap
-        gpu_of = gpu_of or (lambda party: 0)
-        self._pyu = {}
-        for d in [device] + self._sf_participants:
-            party = _party(d)
-            if party not in self._pyu:
-                self._pyu[party] = PYU(party, gpu_of(party))
-        self._inner = _HipSecureAggregator(self._pyu[_party(device)],
-                                           [self._pyu[_party(p)] for p in self._sf_participants],
-                                           fxp_bits, **kwargs)
+        self._gpu_of = gpu_of or (lambda party: 0)
+        self.last_masked = None
+        # one masker per participant, created in (and owned by) its process
+        maskers = {nm: p(P.new_masker)(nm, self._fxp_bits) for nm, p in zip(names, self._participants)}
+        keys = self._reveal([p(P.public_key)(maskers[nm]) for nm, p in zip(names, self._participants)])
+        keys = {nm: int(k) for nm, k in zip(names, keys)}
+        self._maskers = {}
+        for nm, p in zip(names, self._participants):
+            mine = None
+            if seeds is not None:
+                mine = {}
+                for peer in names:
+                    if peer != nm:
+                        s = seeds.get((nm, peer), seeds.get((peer, nm)))
+                        if s is None:
+                            raise ValueError(f"missing seed for pair ({nm}, {peer})")
+                        mine[peer] = s
+            self._maskers[nm] = p(P.agree)(maskers[nm], keys, mine)
 
     @property
     def device(self):
-        return self._sf_device
+        return self._device
 
     @property
     def participants(self):
-        return list(self._sf_participants)
+        return list(self._participants)
 
-    @property
-    def inner(self) -> _HipSecureAggregator:
-        """The sfl_amd aggregator doing the work (digests, wire images)."""
-        return self._inner
-
+    # ------------------------------------------------------------------ API
     def sum(self, data: List, axis=None):
-        out = self._inner.sum(self._objects(data), axis=axis)
-        return self._wrap(self._sf_device, _reveal_local(out))
+        return self._aggregate(data, axis, None, average=False)
 
     def average(self, data: List, axis=None, weights=None):
-        if weights is not None and not _is_device_object(weights):
-            assert len(weights) == len(data), (
-                f"Length of the weights does not match the data: {len(weights)} vs {len(data)}.")
-            for i, w in enumerate(weights):
-                # a device-object weight must live on its data's party
-                # (stateful_fedgen_aggregator.py:74-78), checked before it is revealed
-                if _is_device_object(w) and _is_device_object(data[i]):
-                    assert _party(w.device) == _party(data[i].device), (
-                        "Device of weight does not match the corresponding data device.")
-            weights = [self._value(w) if _is_device_object(w) else w for w in weights]
-        out = self._inner.average(self._objects(data), axis=axis, weights=weights)
-        return self._wrap(self._sf_device, _reveal_local(out))
+        return self._aggregate(data, axis, weights, average=True)
 
     # ------------------------------------------------------------ internals
-    def _value(self, obj):
-        if isinstance(obj, PYUObject):
-            return obj.data
-        if self._reveal is None:
-            raise RuntimeError("secretflow device objects need a reveal function (pass reveal=sf.reveal)")
-        return self._reveal(obj)
-
-    def _objects(self, data):
+    def _aggregate(self, data, axis, weights, average: bool):
         assert data, "Data to aggregate should not be None or empty!"
-        out = []
+        if axis not in (0, None):
+            raise NotImplementedError("SecureAggregator aggregates over parties (axis=0)")
+        owners = []
         for d in data:
-            if isinstance(d, PYUObject):
-                out.append(d)
-                continue
             if not _is_device_object(d):
                 raise TypeError(f"expect a device object (with .device), got {type(d)}")
-            party = _party(d.device)
-            if party not in self._pyu:
+            owner = _party(d.device)
+            if owner not in self._maskers:
                 raise AssertionError(f"{d.device} is not a participant")
-            out.append(PYUObject(self._pyu[party], self._value(d)))
-        return out
+            owners.append(owner)
+        assert len(set(owners)) == len(owners), "each party may contribute one object"
+        assert set(owners) == set(self._maskers), (
+            "every participant must contribute (pairwise masks only cancel without dropout, "
+            "secure_aggregation.ipynb:242)")
+        ws = [None] * len(data)
+        if weights is not None:
+            if _is_device_object(weights):
+                raise TypeError("weights must be a per-party list")
+            assert len(weights) == len(data), (
+                f"Length of the weights does not match the data: {len(weights)} vs {len(data)}.")
+            ws = list(weights)
+            for i, w in enumerate(ws):
+                if _is_device_object(w):
+                    # used through its own device (stateful_fedgen_aggregator.py:74-85)
+                    assert _party(w.device) == owners[i], (
+                        "Device of weight does not match the corresponding data device.")
+        masked, advanced = [], {}
+        for d, w, owner in zip(data, ws, owners):
+            m, nxt = d.device(P.mask_payload, num_returns=2)(self._maskers[owner], d, w, self._gpu_of(owner))
+            advanced[owner] = nxt
+            masked.append(m.to(self._device))
+        # the streams moved on in every party (a round that failed part-way in
+        # an eager runtime raised above and leaves the old maskers in place)
+        self._maskers.update(advanced)
+        self.last_masked = masked  # server-owned: what the server received
+        server_ws = None
+        if average and weights is not None:
+            server_ws = [w.to(self._device) if _is_device_object(w) else w for w in ws]
+        return self._device(P.sum_decode)(*masked, weights=server_ws, average=average,
+                                          gpu=self._gpu_of(_party(self._device)))
 
 
 def _party(device) -> str:
@@ -136,11 +158,44 @@ def _is_device_object(x) -> bool:
     return hasattr(x, "device") and hasattr(getattr(x, "device"), "party")
 
 
-def install(module) -> None:
-    """Rebind ``module.SecureAggregator`` to the HIP aggregator, e.g.::
+_TARGETS = ("secretflow.security", "secretflow.security.aggregation",
+            "secretflow.security.aggregation.secure_aggregator")
 
-        import secretflow.security.aggregation as agg
+
+def install(*modules) -> list:
+    """Rebind ``SecureAggregator`` to the HIP aggregator.
+
+    With no argument: ``secretflow.security`` and
+    ``secretflow.security.aggregation`` (imported here), plus
+    ``secretflow.security.aggregation.secure_aggregator`` when loaded.  Run
+    it before importing code that subclasses the class, e.g.::
+
         from sfl_amd.compat import secretflow as hip
-        hip.install(agg)            # every later SecureAggregator(...) runs on MI355X
-    """
-    module.SecureAggregator = SecureAggregator
+        hip.install()                       # first
+        from sfl.security.aggregation.stateful_fedgen_aggregator import StatefulFedGenAggregator
+
+    Raises ``RuntimeError`` when a subclass of the replaced class already
+    exists (its base would stay the old class).  Returns the modules rebound."""
+    import importlib
+
+    if not modules:
+        found = []
+        for name in _TARGETS:
+            mod = sys.modules.get(name)
+            if mod is None and name != _TARGETS[-1]:
+                mod = importlib.import_module(name)
+            if mod is not None:
+                found.append(mod)
+        modules = tuple(found)
+    stale = []
+    for mod in modules:
+        old = getattr(mod, "SecureAggregator", None)
+        if isinstance(old, type) and old is not SecureAggregator:
+            stale += [c for c in old.__subclasses__() if c not in stale]
+    if stale:
+        names = ", ".join(f"{c.__module__}.{c.__qualname__}" for c in stale)
+        raise RuntimeError(f"install() ran after {names} subclassed the replaced SecureAggregator; "
+                           "call it before importing those modules")
+    for mod in modules:
+        mod.SecureAggregator = SecureAggregator
+    return list(modules)

@@ -68,10 +68,16 @@ DeviceObject = PYUObject
 
 
 def _local(x, dev: PYU):
+    """Resolve device objects in ``x`` -- nested in lists, tuples and dicts
+    too, as secretflow flattens a call's arguments -- to their values."""
     if isinstance(x, PYUObject):
         if x.device != dev:
             raise ValueError(f"{x.device} object used on {dev}; move it with .to() first")
         return x.data
+    if isinstance(x, (list, tuple)):
+        return type(x)(_local(v, dev) for v in x)
+    if isinstance(x, dict):
+        return {k: _local(v, dev) for k, v in x.items()}
     return x
 
 

@@ -1,0 +1,296 @@
+"""The secure aggregation split at the party boundary: what runs inside each
+participant's process and what runs inside the server's.
+
+The reference's ``SecureAggregator`` (un-vendored ``secretflow-lite``) keeps
+one ``_Masker`` per participant on that participant's own device; only DH
+public keys reach the driver, and only masked vectors leave a client
+(``docs/developer/algorithm/secure_aggregation.ipynb:227-239``: "each
+participant outputs" ``y_u``; ``sfl/security/aggregation/sparse_plain_aggregator.py:86``:
+``data = [d.to(self.device) for d in data]``).  The functions below are those
+per-device steps, written so a secretflow device can run them remotely:
+
+* every argument and result is a plain picklable value (a :class:`Masker`,
+  host arrays, a :class:`MaskedPayload`);
+* the masker is threaded through functionally -- ``mask_payload`` returns
+  the advanced masker as a second result (``num_returns=2``) -- so the
+  generator positions persist across rounds in the party's object store
+  without an actor and without the driver ever holding the state;
+* per-element work runs on the party's GPU through ``libsfl_sa`` (``sa_mask``
+  on the client, ``sa_sum_u64`` + ``sa_decode`` on the server); numpy's
+  rejection of a raw PCG64 0 is resolved on the client before its vector
+  leaves (``sa_pcg64_find_zero`` / ``sa_stream_shift``), as the reference's
+  ``Generator.integers`` does inside ``_Masker``.
+
+``sfl_amd.compat.secretflow.SecureAggregator`` drives these through
+secretflow-shaped devices; ``tests/test_compat_secretflow.py`` runs them in a
+spawned process per party.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .masker import Masker
+
+_F32, _F64, _I64 = np.dtype(np.float32), np.dtype(np.float64), np.dtype(np.int64)
+
+
+@dataclass
+class MaskedPayload:
+    """One client's masked contribution: what crosses the wire to the server.
+
+    ``u64`` is every layer's masked uint64 vector packed in layer order (the
+    reference ships the per-layer arrays; the packing is the same elements
+    with one header).  ``digest`` is the XOR of its 64-bit words, checked by
+    the server after the transfer."""
+    party: str
+    u64: np.ndarray
+    sizes: list
+    shapes: list
+    container: str          # "array" | "list" | "tuple"
+    as_torch: bool
+    digest: int
+    fxp_bits: int
+    positions: dict = field(default_factory=dict)  # peer -> stream position the round started at
+
+
+# --------------------------------------------------------------- key set-up
+def new_masker(party: str, fxp_bits: int = 18) -> Masker:
+    """Runs on the participant: a fresh DH key pair (its private half never
+    leaves this process)."""
+    return Masker(str(party), int(fxp_bits))
+
+
+def public_key(masker: Masker) -> int:
+    """Runs on the participant: the only value of its masker the driver sees."""
+    return int(masker.public_key)
+
+
+def agree(masker: Masker, peer_keys: dict, seeds: dict | None = None) -> Masker:
+    """Runs on the participant: pairwise seeds from the revealed public keys
+    (``seeds``: explicit ``{peer: seed | (state, inc)}`` for tests)."""
+    if seeds is None:
+        masker.agree({str(k): int(v) for k, v in peer_keys.items()})
+    else:
+        for peer in peer_keys:
+            if peer == masker.party:
+                continue
+            s = seeds[peer]
+            if isinstance(s, (tuple, list)):
+                masker.set_state(peer, *s)
+            else:
+                masker.set_seed(peer, int(s))
+    return masker
+
+
+# ------------------------------------------------------------- client side
+def _layers(payload):
+    if isinstance(payload, tuple):
+        return list(payload), "tuple"
+    if isinstance(payload, list):
+        return list(payload), "list"
+    return [payload], "array"
+
+
+def _host_weight(w):
+    if w is None:
+        return None
+    try:
+        import torch
+
+        if isinstance(w, torch.Tensor):
+            return w.detach().cpu().numpy()
+    except ImportError:  # pragma: no cover
+        pass
+    return w
+
+
+def mask_payload(masker: Masker, payload, weight=None, gpu: int | None = 0):
+    """Runs on the participant: quantize ``payload * weight`` and add the
+    pairwise masks (``sa_mask`` on this party's GPU ``gpu``).
+
+    Returns ``(MaskedPayload, masker)``, the masker advanced past this round's
+    draws (numpy's rejections included)."""
+    from .secure_aggregator import _compute_dtype, _np_dtype, _shape
+
+    layers, container = _layers(payload)
+    weight = _host_weight(weight)
+    shapes = [_shape(a) for a in layers]
+    sizes = [int(np.prod(sh)) if sh else 1 for sh in shapes]
+    as_torch = _is_torch(layers[0]) if layers else False
+    plan = []
+    for a, sh in zip(layers, shapes):
+        ldt = _np_dtype(a)
+        ct = _compute_dtype(ldt, weight, masker.fxp_bits)
+        if ct not in (_F32, _F64, _I64):
+            raise NotImplementedError(f"arithmetic type {ct} (data {ldt}) is not supported")
+        if ldt.kind in "biu" and ldt != _I64 and ct.kind == "i":
+            raise NotImplementedError(f"integer data of type {ldt} is not supported")
+        xt = ldt if ldt in (_F32, _F64, _I64) else (_I64 if ldt.kind in "biu" else _F64)
+        wvec = None
+        if weight is not None and np.ndim(weight):
+            wvec = np.ascontiguousarray(np.broadcast_to(np.asarray(weight), sh).astype(ct)).reshape(-1)
+        plan.append((xt, ct, wvec))
+
+    # consecutive layers draw consecutive stream positions (the reference's
+    # per-layer rng.integers calls): layers of one element / arithmetic type
+    # under a scalar weight are masked as ONE vector -- bit-identical
+    groups, cur = [], None
+    for li, (xt, ct, wvec) in enumerate(plan):
+        key = (xt, ct)
+        if cur is not None and cur[0] == key and wvec is None and cur[2] is None:
+            cur[1].append(li)
+        else:
+            cur = [key, [li], wvec]
+            groups.append(cur)
+
+    start = {p: masker.position(p) for p in masker.peers}
+    out = np.empty(sum(sizes), dtype=np.uint64)
+    bounds = np.cumsum([0] + sizes)
+    digest = 0
+    for (xt, ct), lis, wvec in groups:
+        lo, hi = int(bounds[lis[0]]), int(bounds[lis[-1] + 1])
+        if hi == lo:
+            continue
+        xs = [layers[li] for li in lis]
+        wscalar = 1.0
+        if weight is not None and not np.ndim(weight):
+            wscalar = float(weight) if ct.kind == "f" else int(weight)
+        vec, extra = _mask_vector(masker, xs, xt, ct, wscalar, wvec, gpu)
+        out[lo:hi] = vec
+        masker.consume(hi - lo)
+        for peer, k in extra.items():
+            masker.skip(peer, k)
+    if out.size:
+        digest = int(np.bitwise_xor.reduce(out))
+    return (MaskedPayload(masker.party, out, sizes, shapes, container, as_torch, digest, masker.fxp_bits, start),
+            masker)
+
+
+def _is_torch(a) -> bool:
+    try:
+        import torch
+
+        return isinstance(a, torch.Tensor)
+    except ImportError:  # pragma: no cover
+        return False
+
+
+def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, wvec, gpu):
+    """One launch group on the party's GPU: ``sa_mask`` over the packed
+    layers ``xs`` from the masker's current stream positions; a flagged raw
+    0 is moved onto numpy's stream (``sa_stream_shift``).  Returns the host
+    uint64 vector and ``{peer: extra raw draws}``."""
+    import torch
+
+    from ... import _lib as L
+    from ... import kernels as K
+
+    if gpu is None:
+        raise RuntimeError("the party has no GPU: libsfl_sa masks on the device")
+    dev = torch.device("cuda", gpu)
+    tdt = {_F32: torch.float32, _F64: torch.float64, _I64: torch.int64}
+    parts = []
+    for a in xs:
+        if isinstance(a, torch.Tensor):
+            parts.append(a.detach().reshape(-1).to(device=dev, dtype=tdt[xt]))
+        else:
+            parts.append(torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=xt).reshape(-1)).to(dev))
+    x = parts[0] if len(parts) == 1 else torch.cat(parts)
+    x = x.contiguous()
+    if x.data_ptr() % 16:
+        x = x.clone()
+    n = x.numel()
+    wv = None if wvec is None else torch.from_numpy(wvec).to(dev)
+    with torch.cuda.device(dev):
+        out = torch.empty(n, dtype=K.U64, device=dev)
+        flags = torch.zeros(1, dtype=torch.int32, device=dev)
+        streams = masker.streams()
+        K.mask(x, out, streams, weight=wscalar, weight_vec=wv, compute_dtype=tdt[ct],
+               fxp_bits=masker.fxp_bits, flags=flags)
+        extra = {}
+        if int(flags.item()) & L.SA_FLAG_PRG_REJECT:
+            found = K.rejected_draws_many([g for g, _, _ in streams], n, dev)
+            for peer, (gen, sign, _), (pts, total) in zip(masker.peers, streams, found):
+                for k, shift in pts:
+                    K.stream_shift(out, gen, sign, k, shift)
+                if total > n:
+                    extra[peer] = total - n
+        host = K.as_u64(out)
+    return host, extra
+
+
+# ------------------------------------------------------------- server side
+def sum_decode(*payloads: MaskedPayload, weights=None, average: bool = False, gpu: int | None = 0):
+    """Runs on the server: check each payload's digest, sum the masked
+    vectors mod 2^64 (the masks cancel) and decode ``int64(S) / 2^fxp`` as
+    float64, divided by C or ``sum(weights)`` (element-wise for per-element
+    weights) for the average.  Returns the reference's shapes: an array, or a
+    list / tuple of per-layer arrays (torch tensors on the server GPU when
+    the parties held torch tensors)."""
+    assert payloads, "Data to aggregate should not be None or empty!"
+    p0 = payloads[0]
+    names = [p.party for p in payloads]
+    assert len(set(names)) == len(names), "each party may contribute one object"
+    for p in payloads:
+        if (p.sizes, p.shapes, p.container, p.fxp_bits) != (p0.sizes, p0.shapes, p0.container, p0.fxp_bits):
+            raise ValueError("parties hold arrays of different shapes")
+    fxp_bits = p0.fxp_bits
+    n = int(sum(p0.sizes))
+    divisor, divisor_vec = 1.0, None
+    if average:
+        if weights is None:
+            divisor = float(len(payloads))
+        else:
+            weights = [_host_weight(w) for w in weights]
+            assert len(weights) == len(payloads), (
+                f"Length of the weights does not match the data: {len(weights)} vs {len(payloads)}.")
+            if all(np.ndim(w) == 0 for w in weights):
+                divisor = float(sum(weights))
+            else:
+                divisor_vec = [np.concatenate([np.broadcast_to(np.asarray(w), sh).astype(np.float64).reshape(-1)
+                                               for sh in p0.shapes]) if n else np.zeros(0)
+                               for w in weights]
+    dec = _sum_decode_vectors([p.u64 for p in payloads], [p.digest for p in payloads], fxp_bits, divisor,
+                              divisor_vec, gpu, p0.as_torch)
+    bounds = np.cumsum([0] + list(p0.sizes))
+    layers = [dec[int(bounds[i]):int(bounds[i + 1])].reshape(sh) for i, sh in enumerate(p0.shapes)]
+    if p0.container == "array":
+        return layers[0]
+    return tuple(layers) if p0.container == "tuple" else layers
+
+
+class DigestMismatch(RuntimeError):
+    """A masked vector changed between the client and the server."""
+
+
+def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_torch):
+    import torch
+
+    from ... import kernels as K
+
+    if gpu is None:
+        raise RuntimeError("the server has no GPU: libsfl_sa sums on the device")
+    dev = torch.device("cuda", gpu)
+    n = int(u64s[0].size)
+    with torch.cuda.device(dev):
+        vecs = [torch.from_numpy(np.ascontiguousarray(u).view(np.int64)).to(dev, non_blocking=False) for u in u64s]
+        out = torch.empty(n, dtype=torch.float64, device=dev)
+        if n:
+            dig = torch.zeros(len(vecs), dtype=K.U64, device=dev)
+            for i, v in enumerate(vecs):
+                K.xor_digest(v, dig[i:i + 1])
+            s = torch.empty(n, dtype=K.U64, device=dev)
+            K.sum_u64(vecs, s)
+            dv = None
+            if divisor_vec is not None:
+                dv = K.sum_f64([torch.from_numpy(w).to(dev) for w in divisor_vec],
+                               torch.empty(n, dtype=torch.float64, device=dev))
+            K.decode(s, out, fxp_bits=fxp_bits, divisor=divisor, divisor_vec=dv)
+            got = K.as_u64(dig).tolist()
+            for i, (g, want) in enumerate(zip(got, digests)):
+                if int(g) != int(want) & ((1 << 64) - 1):
+                    raise DigestMismatch(f"masked vector {i}: digest {int(g):016x}, sent {int(want):016x}")
+    return out if as_torch else out.cpu().numpy()

@@ -1,93 +1,328 @@
-"""The secretflow-shaped import path (sfl_amd.compat.secretflow): duck-typed
-stand-ins for secretflow's PYU / PYUObject / sf.reveal, as the reference's
-callers hand them to ``SecureAggregator(device, participants, fxp_bits)``.
+"""The secretflow drop-in (sfl_amd.compat.secretflow) against a secretflow
+stand-in with real party isolation (tests/fake_secretflow.py): every party is
+a spawned process, the driver holds opaque handles, and ``reveal`` raises on
+any client-owned value but a public key.
 
-CPU: device mapping, ``install`` rebinding, argument checks.  GPU: the
-AggregatorBase-style sums / averages through the adapter equal the oracle's
-bit for bit, weights given as device objects on the client parties
-(stateful_fedgen_aggregator.py:74-78)."""
-import types
+What is checked, per the reference's protocol
+(docs/developer/algorithm/secure_aggregation.ipynb:227-258;
+sfl/security/aggregation/sparse_plain_aggregator.py:86,96;
+stateful_fedgen_aggregator.py:20-33,74-85):
+
+* each participant's masker is created by -- and stays in -- its own process;
+  the driver reveals the DH public keys and nothing else of a client, and
+  holds no Masker / DiffieHellman object;
+* the masked vector each client sends equals the oracle's (explicit seeds),
+  round after round (stream positions persist inside the parties);
+* the 7 AggregatorBase cases (tests/security/aggregation/test_aggregator_base.py:21-160)
+  come out bit-exact vs the oracle, with device-object weights used on their
+  own party;
+* ``install()`` rebinds secretflow.security AND .aggregation; a subclass
+  defined after it (the reference's StatefulFedGenAggregator pattern)
+  aggregates through the drop-in; one defined before makes install() raise.
+
+CPU: the party processes run the oracle's arithmetic in place of the two
+device steps (tests/party_oracle_backend.py); GPU: the HIP steps
+(``sa_mask`` in each client process, ``sa_sum_u64`` + ``sa_decode`` in the
+server's)."""
+import gc
+import importlib.util
+import json
+import os
 
 import numpy as np
 import pytest
 
 torch = pytest.importorskip("torch")
 
+import fake_secretflow as fs  # noqa: E402
 from oracle import secagg as o  # noqa: E402
 
-
-class FakePYU:
-    """secretflow.PYU shape: .party, __call__(fn) -> fn run 'on' the party."""
-
-    def __init__(self, party):
-        self.party = party
-
-    def __call__(self, fn):
-        return lambda *a: FakeObj(self, fn(*a))
-
-    def __repr__(self):
-        return f"FakePYU({self.party})"
+HERE = os.path.dirname(os.path.abspath(__file__))
+CONTRACT = json.load(open(os.path.join(HERE, "golden", "aggregator_contract.json")))
+NAMES = ["alice", "bob"]
+REF_SUBCLASS = "/root/reference/sfl/security/aggregation/stateful_fedgen_aggregator.py"
 
 
-class FakeObj:
-    """secretflow.PYUObject shape: .device and an opaque reference."""
+def _oracle_backend_init():
+    import party_oracle_backend
 
-    def __init__(self, device, value):
-        self.device = device
-        self._ref = {"value": value}
+    party_oracle_backend.install()
 
 
-def fake_reveal(obj):
-    return obj._ref["value"]
+def _cluster(oracle_backend: bool):
+    init = _oracle_backend_init if oracle_backend else None
+    return fs.Cluster(NAMES + ["carol"], private=NAMES, init=init)
 
 
-def test_adapter_maps_devices_and_installs():
+@pytest.fixture(scope="module")
+def cpu_cluster():
+    c = _cluster(True)
+    yield c
+    c.close()
+
+
+def _seeds():
+    s = o.seeds_for(NAMES)
+    return s, {(a, b): s[a][b] for a in NAMES for b in NAMES if a != b}
+
+
+def _put(dev, value):
+    return dev(lambda v: v)(value)
+
+
+def _case_inputs(case):
+    a, b = case["a"], case["b"]
+    if isinstance(a[0][0], list):  # a list of layers
+        return [np.array(x) for x in a], [np.array(x) for x in b]
+    return np.array(a), np.array(b)
+
+
+def _flat(v):
+    return np.concatenate([np.asarray(x, dtype=np.float64).reshape(-1) for x in v]) if isinstance(v, (list, tuple)) \
+        else np.asarray(v, dtype=np.float64).reshape(-1)
+
+
+def _cat(v):
+    """Layers packed in order, element type kept (the oracle quantizes by it)."""
+    return np.concatenate([np.asarray(x).reshape(-1) for x in v]) if isinstance(v, list) else np.asarray(v).reshape(-1)
+
+
+def _run_contract(cluster, agg, seeds, weights_on_device: bool):
+    """The 7 AggregatorBase cases in order on one aggregator; the stream
+    positions advance by each case's element count."""
+    alice, bob, carol = (cluster.pyu(n) for n in NAMES + ["carol"])
+    offset = 0
+    for name in ("sum_single", "sum_list", "avg_single", "avg_list", "avg_weights", "avg_list_weights",
+                 "avg_same_shape_weights"):
+        case = CONTRACT[name]
+        xa, xb = _case_inputs(case)
+        da, db = _put(alice, xa), _put(bob, xb)
+        w = None
+        if "weights" in case:
+            w = np.array(case["weights"]) if name == "avg_same_shape_weights" else list(case["weights"])
+        if name.startswith("sum"):
+            out = agg.sum([da, db], axis=0)
+        elif w is not None and weights_on_device and name != "avg_same_shape_weights":
+            out = agg.average([da, db], axis=0, weights=[_put(alice, w[0]), _put(bob, w[1])])
+        else:
+            out = agg.average([da, db], axis=0, weights=w)
+        assert out.device == carol
+        got = fs.reveal(out)  # server-owned: revealable
+        # oracle, same seeds and stream positions
+        xs = [_cat(xa), _cat(xb)]
+        if name.startswith("sum"):
+            exp, _, masked = o.secure_sum(xs, NAMES, seeds=seeds, offset=offset)
+        else:
+            ow = None
+            if w is not None:
+                ow = [np.broadcast_to(w[0], np.shape(xa)).reshape(-1), np.broadcast_to(w[1], np.shape(xb)).reshape(-1)] \
+                    if name == "avg_same_shape_weights" else w
+            exp, _, masked = o.secure_average(xs, NAMES, weights=ow, seeds=seeds, offset=offset)
+        assert np.array_equal(_flat(got), exp), name
+        # what the server received is each client's masked vector, bit for bit
+        recv = [fs.reveal(m) for m in agg.last_masked]
+        for r, m in zip(recv, masked):
+            assert np.array_equal(r.u64, np.asarray(m, dtype=np.uint64).reshape(-1)), name
+        # and the reference's contract values
+        expect = case.get("expect")
+        if expect is None:
+            expect = np.average([np.array(case["a"]), np.array(case["b"])], axis=0, weights=np.array(case["weights"]))
+        if isinstance(got, list):
+            for g, e in zip(got, expect):
+                np.testing.assert_almost_equal(g, np.array(e), decimal=case["decimal"])
+        else:
+            np.testing.assert_almost_equal(got, np.array(expect), decimal=case["decimal"])
+        offset += xs[0].size
+
+
+def _driver_holds(*names):
+    return [type(x).__name__ for x in gc.get_objects() if type(x).__name__ in names]
+
+
+def test_masking_stays_inside_each_party(cpu_cluster):
     from sfl_amd.compat import secretflow as hip
 
-    alice, bob, carol = FakePYU("alice"), FakePYU("bob"), FakePYU("carol")
-    agg = hip.SecureAggregator(carol, [alice, bob], reveal=fake_reveal, gpu_of={"alice": 0, "bob": 0, "carol": 0}.get)
-    assert agg.device is carol and agg.participants == [alice, bob]
-    assert [p.party for p in agg.inner.participants] == ["alice", "bob"]
-    assert agg.inner.device.party == "carol"
-    m = types.ModuleType("secretflow_security_aggregation")
-    hip.install(m)
-    assert m.SecureAggregator is hip.SecureAggregator
+    c = cpu_cluster
+    seeds, pair = _seeds()
+    c.reveals.clear()
+    agg = hip.SecureAggregator(c.pyu("carol"), [c.pyu(n) for n in NAMES], reveal=fs.reveal, seeds=pair)
+    # set-up revealed exactly the two public keys
+    assert c.reveals == [("alice", "int"), ("bob", "int")]
+    _run_contract(c, agg, seeds, weights_on_device=True)
+    assert c.reveals[:2] == [("alice", "int"), ("bob", "int")]
+    assert all(p == "carol" for p, _ in c.reveals[2:]), c.reveals
+    assert _driver_holds("Masker", "DiffieHellman") == []
+    assert "Masker" in c.types_held("alice") and "Masker" in c.types_held("bob")
+    assert "Masker" not in c.types_held("carol")
+    # the stand-in really refuses a client's datum
+    with pytest.raises(fs.RevealRefused):
+        fs.reveal(_put(c.pyu("alice"), np.ones(3)))
+
+
+def test_dh_agreement_inside_the_parties(cpu_cluster):
+    """No explicit seeds: the pair seeds come from a DH exchange of public
+    keys; the sum still equals the oracle's (the masks cancel)."""
+    from sfl_amd.compat import secretflow as hip
+
+    c = cpu_cluster
+    c.reveals.clear()
+    agg = hip.SecureAggregator(c.pyu("carol"), [c.pyu(n) for n in NAMES], reveal=fs.reveal)
+    rng = np.random.default_rng(11)
+    xs = [(rng.standard_normal(1000) * 0.1).astype(np.float32) for _ in NAMES]
+    for rnd in range(2):
+        out = agg.average([_put(c.pyu(n), x) for n, x in zip(NAMES, xs)], axis=0, weights=[3, 5])
+        exp = o.decode(o.server_sum([o.quantize(x, w) for x, w in zip(xs, [3, 5])]), divisor=8)
+        assert np.array_equal(fs.reveal(out), exp)
+        recv = [fs.reveal(m).u64 for m in agg.last_masked]
+        # masked vectors are not the quantized ones (the masks are there) ...
+        assert not np.array_equal(recv[0], o.quantize(xs[0], 3))
+    assert [p for p, _ in c.reveals if p != "carol"] == ["alice", "bob"]
+    assert _driver_holds("Masker", "DiffieHellman") == []
+
+
+def test_argument_checks_before_any_party_work(cpu_cluster):
+    from sfl_amd.compat import secretflow as hip
+
+    c = cpu_cluster
+    alice, bob, carol = (c.pyu(n) for n in NAMES + ["carol"])
+    agg = hip.SecureAggregator(carol, [alice, bob], reveal=fs.reveal)
     with pytest.raises(TypeError):
         hip.SecureAggregator(object(), [alice])
     with pytest.raises(AssertionError, match="empty"):
         agg.sum([], axis=0)
+    data = [_put(alice, np.ones(3)), _put(bob, np.ones(3))]
     with pytest.raises(AssertionError, match="not a participant"):
-        agg.sum([FakeObj(FakePYU("mallory"), np.zeros(3))], axis=0)
-    # a device-object weight on another party than its data is refused before
-    # anything is revealed (stateful_fedgen_aggregator.py:74-78)
-    data = [alice(lambda: np.ones(3))(), bob(lambda: np.ones(3))()]
+        agg.sum([_put(carol, np.zeros(3)), data[1]], axis=0)
     with pytest.raises(AssertionError, match="Device of weight does not match"):
-        agg.average(data, axis=0, weights=[bob(lambda: 1)(), bob(lambda: 2)()])
+        agg.average(data, axis=0, weights=[_put(bob, 1), _put(bob, 2)])
     with pytest.raises(AssertionError, match="Length of the weights"):
         agg.average(data, axis=0, weights=[1])
+    with pytest.raises(AssertionError, match="every participant"):
+        agg.sum([data[0]], axis=0)
+
+
+# ------------------------------------------------------------------ install()
+_SUBCLASS_SRC = '''
+from secretflow.security import SecureAggregator
+
+
+class FedGenLike(SecureAggregator):
+    """The reference's subclass pattern (stateful_fedgen_aggregator.py:23-59)."""
+
+    def __init__(self, device, participants, server_actor, fxp_bits=18):
+        super().__init__(device, participants, fxp_bits)
+        self.server_actor = server_actor
+
+    def average(self, data, axis=None, weights=None):
+        avg = super().average(data, axis, None)
+        return self._device(lambda x: {"model_params": x})(avg)
+'''
+
+
+def _define_subclass():
+    ns = {}
+    exec(compile(_SUBCLASS_SRC, "<fedgen_like>", "exec"), ns)
+    return ns["FedGenLike"]
+
+
+def test_install_rebinds_both_import_paths(monkeypatch):
+    from sfl_amd.compat import secretflow as hip
+
+    mods = fs.installed_into(monkeypatch)
+    rebound = hip.install()
+    assert mods["secretflow.security"].SecureAggregator is hip.SecureAggregator
+    assert mods["secretflow.security.aggregation"].SecureAggregator is hip.SecureAggregator
+    assert len(rebound) == 2
+    assert issubclass(_define_subclass(), hip.SecureAggregator)
+
+
+def test_install_after_a_subclass_raises(monkeypatch):
+    from sfl_amd.compat import secretflow as hip
+
+    fs.installed_into(monkeypatch)
+    early = _define_subclass()  # subclasses the placeholder
+    with pytest.raises(RuntimeError, match="FedGenLike"):
+        hip.install()
+    assert not issubclass(early, hip.SecureAggregator)
+
+
+def test_subclass_defined_after_install_aggregates(monkeypatch, cpu_cluster):
+    from sfl_amd.compat import secretflow as hip
+
+    fs.installed_into(monkeypatch)
+    hip.install()
+    c = cpu_cluster
+    agg = _define_subclass()(c.pyu("carol"), [c.pyu(n) for n in NAMES], server_actor=None)
+    x = [np.arange(6, dtype=np.float32).reshape(2, 3) * (k + 1) for k in range(2)]
+    out = agg.average([_put(c.pyu(n), v) for n, v in zip(NAMES, x)], axis=0)
+    got = fs.reveal(out)["model_params"]
+    exp = o.decode(o.server_sum([o.quantize(v.reshape(-1)) for v in x]), divisor=2)
+    assert np.array_equal(got.reshape(-1), exp)
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SUBCLASS), reason="reference checkout absent")
+def test_reference_stateful_fedgen_aggregator_after_install(monkeypatch, cpu_cluster):
+    """The reference's own StatefulFedGenAggregator source, loaded after
+    install() into the stand-in secretflow package: its base is the drop-in
+    and its weight-less average runs through the parties."""
+    from sfl_amd.compat import secretflow as hip
+
+    fs.installed_into(monkeypatch)
+    hip.install()
+    spec = importlib.util.spec_from_file_location("ref_stateful_fedgen_aggregator", REF_SUBCLASS)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    cls = mod.StatefulFedGenAggregator
+    assert issubclass(cls, hip.SecureAggregator)
+    c = cpu_cluster
+    agg = cls(c.pyu("carol"), [c.pyu(n) for n in NAMES], server_actor=None)
+    x = [[np.full((2, 2), 0.25 * (k + 1), np.float32), np.arange(3, dtype=np.float32)] for k in range(2)]
+    out = agg.average([_put(c.pyu(n), v) for n, v in zip(NAMES, x)], axis=0)
+    got = fs.reveal(out)
+    assert isinstance(got, list) and len(got) == 2
+    flat = [np.concatenate([a.reshape(-1) for a in v]) for v in x]
+    exp = o.decode(o.server_sum([o.quantize(v) for v in flat]), divisor=2)
+    assert np.array_equal(_flat(got), exp)
+
+
+# ----------------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def gpu_cluster():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = _cluster(False)
+    yield c
+    c.close()
 
 
 @pytest.mark.gpu
-def test_adapter_aggregates_like_the_oracle():
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+def test_gpu_contract_masks_in_each_party_process(gpu_cluster):
+    """HIP sa_mask in alice's and bob's processes, sa_sum_u64 + sa_decode in
+    carol's: the 7 AggregatorBase cases and every received masked vector
+    bit-exact vs the oracle; only public keys revealed from the clients."""
     from sfl_amd.compat import secretflow as hip
 
-    names = ["alice", "bob", "carol"]
-    seeds = o.seeds_for(names)
-    pair = {(a, b): seeds[a][b] for a in names for b in names if a != b}
-    devs = [FakePYU(n) for n in names]
-    server = FakePYU("server")
-    agg = hip.SecureAggregator(server, devs, reveal=fake_reveal, seeds=pair)
-    rng = np.random.default_rng(5)
-    xs = [(rng.standard_normal((4, 6)) * 0.1).astype(np.float32) for _ in names]
-    objs = [d(lambda x=x: x)() for d, x in zip(devs, xs)]
-    s = agg.sum(objs, axis=0)
-    assert isinstance(s, FakeObj) and s.device is server
-    exp, _, _ = o.secure_sum([x.reshape(-1) for x in xs], names, seeds=seeds)
-    assert np.array_equal(fake_reveal(s).reshape(-1), exp)
-    w = [d(lambda k=k: 10 * (k + 1))() for k, d in enumerate(devs)]  # weights on the clients' devices
-    avg = agg.average(objs, axis=0, weights=w)
-    exp, _, _ = o.secure_average([x.reshape(-1) for x in xs], names, weights=[10, 20, 30], seeds=seeds,
-                                 offset=xs[0].size)
-    assert np.array_equal(fake_reveal(avg).reshape(-1), exp)
+    c = gpu_cluster
+    seeds, pair = _seeds()
+    c.reveals.clear()
+    agg = hip.SecureAggregator(c.pyu("carol"), [c.pyu(n) for n in NAMES], reveal=fs.reveal, seeds=pair)
+    _run_contract(c, agg, seeds, weights_on_device=True)
+    assert [p for p, _ in c.reveals if p != "carol"] == ["alice", "bob"]
+    assert _driver_holds("Masker", "DiffieHellman") == []
+
+
+@pytest.mark.gpu
+def test_gpu_subclass_after_install_and_rounds(monkeypatch, gpu_cluster):
+    from sfl_amd.compat import secretflow as hip
+
+    fs.installed_into(monkeypatch)
+    hip.install()
+    c = gpu_cluster
+    agg = _define_subclass()(c.pyu("carol"), [c.pyu(n) for n in NAMES], server_actor=None)
+    rng = np.random.default_rng(3)
+    for _ in range(3):
+        x = [(rng.standard_normal((64, 33)) * 0.05).astype(np.float32) for _ in NAMES]
+        out = agg.average([_put(c.pyu(n), v) for n, v in zip(NAMES, x)], axis=0)
+        got = fs.reveal(out)["model_params"]
+        exp = o.decode(o.server_sum([o.quantize(v.reshape(-1)) for v in x]), divisor=2)
+        assert np.array_equal(got.reshape(-1), exp)
