@@ -299,31 +299,49 @@ def dry_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
             "check_local": check}
 
 
-CHECK_NOTE = ("sum over i of bits(decoded[i]) * (2i + 1) * 0x9E3779B97F4A7C15 mod 2^64 over the decoded float64 "
+CHECK_NOTE = ("sum over i of mix64(bits(decoded[i])) * (2i + 1) * 0x9E3779B97F4A7C15 mod 2^64 (mix64 = "
+              "splitmix64's finalizer, so no bit of the digest is structurally zero) over the decoded float64 "
               "aggregate of round 0 (all C clients, every element), recomputed after the timed region by one more "
               "untimed step of the same design: every design and every N must print the same value (the same "
               "inputs, seeds and stream positions)")
 
 
 CHECK_MULT = 0x9E3779B97F4A7C15  # odd: the position weight of element i is (2i + 1) * CHECK_MULT mod 2^64
+MIX1, MIX2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB  # splitmix64's finalizer
+
+
+def _s64(c: int) -> int:
+    """The same 64 bits as a signed int64 (torch has no uint64 arithmetic)."""
+    return c - (1 << 64) if c >> 63 else c
+
+
+def mix64(z):
+    """splitmix64's finalizer on an int64 tensor, bit for bit the uint64
+    function (logical shifts by masking; int64 products wrap like uint64).
+    A decoded value k / 2^18 with |k| < 2^16 has >= 36 trailing zero bits in
+    its float64 pattern; after mix64 every bit depends on every input bit."""
+    z = (z ^ ((z >> 30) & ((1 << 34) - 1))) * _s64(MIX1)
+    z = (z ^ ((z >> 27) & ((1 << 37) - 1))) * _s64(MIX2)
+    return z ^ ((z >> 31) & ((1 << 33) - 1))
 
 
 def position_digest(t, base: int) -> int:
-    """sum_i bits(t[i]) * (2 (base + i) + 1) * CHECK_MULT mod 2^64 over a
-    float64 device vector whose element i is element base + i of the
+    """sum_i mix64(bits(t[i])) * (2 (base + i) + 1) * CHECK_MULT mod 2^64
+    over a float64 device vector whose element i is element base + i of the
     aggregate: position-weighted, so a shard decoded into the wrong place
-    changes it (an XOR or plain sum would not see a permutation).  In slices
-    of 2^26 elements to bound the temporaries; int64 products and sums wrap
-    like uint64."""
+    changes it (an XOR or plain sum would not see a permutation), and mixed,
+    so all 64 bits of the digest carry information (raw bits of decoded
+    fixed-point values end in >= 36 zeros, which made the position weight act
+    only mod 2^28).  In slices of 2^26 elements to bound the temporaries."""
     import torch
 
-    mult = CHECK_MULT - (1 << 64)  # the same 64 bits as a signed int64
+    mult = _s64(CHECK_MULT)
     out, n, step = 0, t.numel(), 1 << 26
     bits = t.view(torch.int64)
     for lo in range(0, n, step):
         hi = min(n, lo + step)
         h = (torch.arange(base + lo, base + hi, device=t.device, dtype=torch.int64) * 2 + 1) * mult
-        out = (out + int((bits[lo:hi] * h).sum().item())) & ((1 << 64) - 1)
+        out = (out + int((mix64(bits[lo:hi]) * h).sum().item())) & ((1 << 64) - 1)
     return out
 
 

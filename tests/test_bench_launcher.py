@@ -326,26 +326,58 @@ def test_cross_only_counts_match_the_registry():
 
 
 def test_position_digest_matches_numpy_and_sees_permutations():
-    """bench.position_digest (the round-0 result check): sum of bits(x[i]) *
-    (2(base+i)+1) * CHECK_MULT mod 2^64, additive over slices at their global
-    offsets (how the ranks' parts combine), and changed by swapping two
-    shards (an XOR or a plain sum would not be)."""
+    """bench.position_digest (the round-0 result check): sum of
+    mix64(bits(x[i])) * (2(base+i)+1) * CHECK_MULT mod 2^64, additive over
+    slices at their global offsets (how the ranks' parts combine), and
+    changed by swapping two shards (an XOR or a plain sum would not be)."""
     import numpy as np
     import torch
 
     import bench
+    from test_gpu_bench_rehearsal import digest_np, mix64_np
 
+    # mix64 is splitmix64's finalizer bit for bit (int64 tensor vs uint64 numpy)
     rng = np.random.default_rng(3)
+    z = rng.integers(0, 2**64, 4096, dtype=np.uint64)
+    z[:4] = [0, 1, 2**63, 2**64 - 1]
+    assert np.array_equal(bench.mix64(torch.from_numpy(z.view(np.int64))).numpy().view(np.uint64), mix64_np(z))
     x = (rng.integers(-2**15, 2**15, 1_000_003) / 2.0**18).astype(np.float64)
-    idx = np.arange(x.size, dtype=np.uint64)
-    want = int(np.sum(x.view(np.uint64) * ((idx * np.uint64(2) + np.uint64(1)) * np.uint64(bench.CHECK_MULT)),
-                      dtype=np.uint64))
+    want = digest_np(x)
     t = torch.from_numpy(x)
     assert bench.position_digest(t, 0) == want
     k = 400_001
     assert (bench.position_digest(t[:k], 0) + bench.position_digest(t[k:], k)) % 2**64 == want
     y = np.concatenate([x[k:2 * k], x[:k], x[2 * k:]])  # two shards swapped
     assert bench.position_digest(torch.from_numpy(y), 0) != want
+
+
+def test_position_digest_has_64_live_bits():
+    """decoded fixed-point values k / 2^18 (|k| < 2^16)
+    have >= 36 trailing zero bits in their float64 patterns, so a digest of
+    the raw bits was one too and swapping two elements 2^27 apart (weights
+    differing by 2^28 * CHECK_MULT) could not change it.  With mix64 neither
+    holds."""
+    import numpy as np
+    import torch
+
+    import bench
+
+    rng = np.random.default_rng(7)
+    for _ in range(4):
+        x = (rng.integers(-2**15, 2**15, 100_003) / 2.0**18).astype(np.float64)
+        assert np.all(np.bitwise_and(x.view(np.uint64), np.uint64(2**36 - 1)) == 0)  # the raw patterns
+        d = bench.position_digest(torch.from_numpy(x), 0)
+        assert d & (2**36 - 1) != 0
+    # elements a and b swapped between positions i and i + 2^27: the parts at
+    # those global positions (base) differ, as the full vectors' digests would
+    a, b = torch.tensor([0.125 + 3 / 2**18], dtype=torch.float64), torch.tensor([-7 / 2**18], dtype=torch.float64)
+    i, j = 12345, 12345 + 2**27
+    before = (bench.position_digest(a, i) + bench.position_digest(b, j)) % 2**64
+    after = (bench.position_digest(b, i) + bench.position_digest(a, j)) % 2**64
+    assert before != after
+    # (the old raw-bit digest could not see it: the difference was a multiple of 2^64)
+    raw = lambda v, base: int(v.view(torch.int64)) * (2 * base + 1) * bench.CHECK_MULT  # noqa: E731
+    assert (raw(a, i) + raw(b, j) - raw(b, i) - raw(a, j)) % 2**64 == 0
 
 
 def test_importing_the_bench_loads_no_torch():

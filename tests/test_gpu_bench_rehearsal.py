@@ -15,6 +15,7 @@ import subprocess
 import sys
 import time
 
+import numpy as np
 import pytest
 
 torch = pytest.importorskip("torch")
@@ -53,9 +54,26 @@ def oracle_check(C: int, n: int, fxp_bits: int = 18) -> str:
         s += o.quantize(x, None, fxp_bits)
         del x
     dec = o.decode(s, fxp_bits)
-    idx = np.arange(n, dtype=np.uint64)
+    return f"{digest_np(dec):016x}"
+
+
+def mix64_np(z):
+    """splitmix64's finalizer in numpy uint64 (bench.mix64's definition)."""
+    z = np.asarray(z, dtype=np.uint64).copy()
+    z ^= z >> np.uint64(30)
+    z *= np.uint64(0xBF58476D1CE4E5B9)
+    z ^= z >> np.uint64(27)
+    z *= np.uint64(0x94D049BB133111EB)
+    z ^= z >> np.uint64(31)
+    return z
+
+
+def digest_np(dec, base: int = 0) -> int:
+    """bench.position_digest restated in numpy: sum_i mix64(bits(dec[i])) *
+    (2 (base + i) + 1) * 0x9E3779B97F4A7C15 mod 2^64."""
+    idx = np.arange(base, base + dec.size, dtype=np.uint64)
     h = (idx * np.uint64(2) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)  # bench.CHECK_MULT
-    return f"{int(np.sum(dec.view(np.uint64) * h, dtype=np.uint64)):016x}"
+    return int(np.sum(mix64_np(np.ascontiguousarray(dec, dtype=np.float64).view(np.uint64)) * h, dtype=np.uint64))
 
 
 def has_gpu() -> bool:
