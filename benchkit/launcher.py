@@ -25,6 +25,12 @@ def launch_ranks(args, script: str) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if args.rehearse_one_gpu:
+        # W rank processes on the one GPU plus a caller that holds a GPU
+        # context of its own ran ~10x slower and tripped the watchdog
+        # (DESIGN.md §5): refuse that setting instead of rehearsing in it
+        holders = gpu_context_holders([os.getpid(), os.getppid()])
+        if holders:
+            raise SystemExit(rehearsal_refusal(holders, args.gpus))
         # N ranks share one box's CPU quota (a 16-CPU cgroup on the test box,
         # throttled during rehearsals: DESIGN.md §5); a rank's host work is
         # small copies, so one OpenMP thread each, as torchrun's own default
@@ -58,6 +64,36 @@ def launch_ranks(args, script: str) -> int:
         import shutil
 
         shutil.rmtree(log_dir, ignore_errors=True)
+
+
+KFD = "/dev/kfd"
+
+
+def gpu_context_holders(pids, device: str = KFD) -> list:
+    """The processes among ``pids`` that have ``device`` open -- a process
+    with a HIP context holds /dev/kfd -- read from /proc without touching
+    the GPU (unreadable or vanished processes count as not holding it)."""
+    out = []
+    for pid in pids:
+        try:
+            fds = os.listdir(f"/proc/{pid}/fd")
+        except OSError:
+            continue
+        for fd in fds:
+            try:
+                if os.readlink(f"/proc/{pid}/fd/{fd}") == device:
+                    out.append(pid)
+                    break
+            except OSError:
+                continue
+    return out
+
+
+def rehearsal_refusal(holders, world: int) -> str:
+    return (f"--rehearse-one-gpu: process(es) {holders} (this launcher or its caller) already hold a GPU context; "
+            f"with {world} rank processes that puts {world + len(holders)} processes on the one GPU, the setting "
+            "in which rehearsals ran ~10x slower and hit the watchdog (DESIGN.md §5). Start the rehearsal from a "
+            "process that has not initialised HIP (pytest: the rehearsal modules run first, tests/conftest.py).")
 
 
 def failing_ranks_report(log_dir: str, lines_per_rank: int = 60) -> str:

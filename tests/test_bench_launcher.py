@@ -389,3 +389,18 @@ def test_importing_the_bench_loads_no_torch():
             "assert 'torch' not in sys.modules, sorted(m for m in sys.modules if m.startswith('torch'))[:5]" % ROOT)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_gpu_context_guard_reads_proc(tmp_path):
+    """benchkit.launcher.gpu_context_holders (the --rehearse-one-gpu guard):
+    finds a process by an open device node in /proc/<pid>/fd, here a file
+    standing in for /dev/kfd, without touching the GPU."""
+    from benchkit.launcher import gpu_context_holders, rehearsal_refusal
+
+    dev = tmp_path / "kfd"
+    dev.write_bytes(b"")
+    assert gpu_context_holders([os.getpid()], str(dev)) == []
+    with open(dev) as f:
+        assert gpu_context_holders([os.getpid(), os.getppid(), 2**22 + 7], str(dev)) == [os.getpid()]
+        del f
+    assert "10x slower" in rehearsal_refusal([123], 8)
