@@ -738,8 +738,16 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
     // ---- mask expansion, stream-outer, two streams per asm block where the
     // schedule pairs them; group g+1's constants are scalar-loaded during
     // group g's first draw
-    ZeroAcc zh = zero_acc_init();  // the paired draws' raw == 0 test (sa_draw2.h)
-    uint64_t zs = 0;               // the single draws' (SA_PCG_DRAW_ASM)
+    // the raw == 0 tests, one lane mask per element slot k of the lane so
+    // that a draw for an element past n (the wave's last tile draws for
+    // every lane) is not counted: numpy draws exactly n
+    ZeroAcc zh[kE];   // the paired draws' (sa_draw2.h)
+    uint64_t zs[kE];  // the single draws' (SA_PCG_DRAW_ASM)
+#pragma unroll
+    for (int k = 0; k < kE; k++) {
+      zh[k] = zero_acc_init();
+      zs[k] = 0;
+    }
     if constexpr (P > 0) {
       using SO = SchedOf<L, X, K>;  // the schedule (a static constexpr: usable in the lambdas)
       Inc ni[2], nj[2];  // next group's plain-step / tile-jump addends
@@ -785,16 +793,16 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
           if constexpr (G.qb < 0) {  // singles never first-touch: their clients are preset
             uint32_t s0 = (uint32_t)sa.p01, s1 = (uint32_t)(sa.p01 >> 32);
             if constexpr (G.va >= 0 && G.va_add)
-              pcg_draw_pair_a(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zs, ak[G.ua], ak[G.va]);
+              pcg_draw_pair_a(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zs[k], ak[G.ua], ak[G.va]);
             else if constexpr (G.va >= 0)
-              pcg_draw_pair(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zs, ak[G.ua], ak[G.va]);
+              pcg_draw_pair(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zs[k], ak[G.ua], ak[G.va]);
             else
-              pcg_draw_one(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zs, ak[G.ua]);
+              pcg_draw_one(s0, s1, sa.s2, sa.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], zs[k], ak[G.ua]);
             sa.p01 = ((uint64_t)s1 << 32) | s0;
           } else {
             State& sb = st[G.qb];
 #define SA_DRAW2_PAIR(fn)                                                                                 \
-  fn<G.F>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], ib, m[1], zh,   \
+  fn<G.F>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0], ib, m[1], zh[k],\
           ak[G.ua], ak[G.va], ak[G.ub], ak[G.vb], bua, bva, bub, bvb)
             if constexpr (G.va >= 0 && G.va_add && G.vb_add)
               SA_DRAW2_PAIR(pcg_draw2_pair_aa);
@@ -807,17 +815,34 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
 #undef SA_DRAW2_PAIR
             else if constexpr (G.ua == G.ub)
               pcg_draw2_one_same<G.F>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia,
-                                      m[0], ib, m[1], zh, ak[G.ua], bua);
+                                      m[0], ib, m[1], zh[k], ak[G.ua], bua);
             else
               pcg_draw2_one<G.F>(sa.p01, sa.s2, sa.s3, sb.p01, sb.s2, sb.s3, mk[0], mk[1], mk[2], mk[3], ia, m[0],
-                                 ib, m[1], zh, ak[G.ua], ak[G.ub], bua, bub);
+                                 ib, m[1], zh[k], ak[G.ua], ak[G.ub], bua, bub);
           }
           if (k == 0 && g + 1 < SO::value.n && !(SA_ABLATE & 128)) fetch(g + 1);
         }
       }, std::make_integer_sequence<int, SO::value.n>{});
     }
 
-    if (__builtin_expect(zero_acc_hit(zh) || zs != 0, 0)) zmin = 0;
+    {
+      uint64_t z0 = (uint64_t)zh[0] | zs[0], z1 = (uint64_t)zh[1] | zs[1];
+      static_assert(kE == 2, "one mask per element slot");
+      static_assert(std::is_same<ZeroAcc, uint64_t>::value, "sa_draw2.h's lane-mask form of the zero test");
+      if (__builtin_expect((z0 | z1) != 0, 0)) {
+        if (base + wave_off + 64 * kE > n) {
+          // the wave's last tile: lanes whose elements are >= n drew too.
+          // Lane l holds elements e + 2l, e + 2l + 1 (e = base + wave_off), so
+          // with r = n - e slot 0 is valid for l < ceil(r/2), slot 1 for
+          // l < floor(r/2): scalar masks, no per-lane compare
+          const uint64_t r = n - (base + wave_off);  // 1 .. 127 here
+          const uint32_t r0 = (uint32_t)((r + 1) >> 1), r1 = (uint32_t)(r >> 1);
+          z0 &= r0 >= 64 ? ~0ull : (1ull << r0) - 1;
+          z1 &= (1ull << r1) - 1;
+        }
+        if (z0 | z1) zmin = 0;
+      }
+    }
 
     // ---- finish: add the quantized value (or the prior pass), digest, sums
     kargs_t* ka = fenced_args();
