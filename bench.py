@@ -54,8 +54,9 @@ from benchkit.containment import (Watchdog, control_group, inject_in_design, inj
                                   published_errors, run_contained, run_variants, variant_summary)
 from benchkit.launcher import failing_ranks_report, launch_ranks  # noqa: E402,F401
 from benchkit.roofline import (HBM_PEAK_GBPS, PCG_ONE_DRAWS_8WAVE, PCG_PAIR_DRAWS_2WAVE,  # noqa: E402,F401
-                               PMC_DIRS, PMC_ELEMS, VALU_PEAK_WAVE_INSTR_PER_S, draw_loop_ceilings,
-                               kernel_key, pmc_traffic, pmc_valu, traffic_field)
+                               PMC_DIRS, PMC_ELEMS, VALU_PEAK_WAVE_INSTR_PER_S, committed_kernel_ms,
+                               draw_loop_ceilings, exchange_model, kernel_key, pmc_traffic, pmc_valu,
+                               traffic_field)
 from benchkit.standin import HostStandinComm  # noqa: E402,F401
 
 
@@ -183,6 +184,7 @@ def dry_run(args, world: int, rank: int, cpu, wd: Watchdog) -> None:
             "variant_timeout_seconds": args.variant_timeout}
     if multi:
         line["designs_agree"] = True
+        line["roofline"] = {"exchange": r["exchange"]["model"]}
         line["exchange_variants"] = [dict(variant_summary(r), workload=workload(args, world, head))]
         with wd.lock:
             wd.line = line if rank == 0 else {}
@@ -264,6 +266,16 @@ def collective_text(v: Variant) -> str:
     return "ncclReduce(uint64, sum) in place to rank 0"
 
 
+def dry_exchange_model(design: str, world: int, args) -> dict | None:
+    """--dry-run: the exchange model with the committed per-rank kernel time
+    (no GPU here): what the driver's node should measure for this N."""
+    kms, src = committed_kernel_ms(args.clients, world, args.elems)
+    m = exchange_model(design, world, args.elems, kms, None, 8, "dry-run")
+    if m is not None:
+        m["kernel_ms_source"] = src or "none committed for this shape"
+    return m
+
+
 def dry_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> dict:
     """--dry-run's stand-in for run_design (no GPU): every step is one gloo
     all_reduce of a small CPU tensor among the ranks, timed like a design
@@ -295,7 +307,8 @@ def dry_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     return {"name": v.name, "ms_per_step": ms, "value": args.clients * args.elems / max(ms / 1e3, 1e-9),
             "steps": steps, "warmup": warmup, "kernel_ms_per_step": 0.0, "chunks": 1, "kernel": "none (dry run)",
             "exchange": {"ms_per_step": ms, "bytes_per_rank_per_step": 4096, "algbw_GBps": None, "busbw_GBps": None,
-                         "collective": "dry run: one gloo all_reduce of 4 KiB per step"},
+                         "collective": "dry run: one gloo all_reduce of 4 KiB per step",
+                         "model": dry_exchange_model(v.name, world, args)},
             "check_local": check}
 
 
@@ -569,6 +582,8 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
                         "max(kernel, exchange) + one chunk of fill/drain")}
         if world == 1:
             res["exchange"]["note"] = "world 1 (--dist rehearsal): the collectives move no data between GPUs"
+        res["exchange"]["model"] = exchange_model(v.name, world, N, kern_ms, xchg_ms, len(pipe.bounds),
+                                                  "rehearsal" if ctx.get("rehearse") else "measured")
     if keep:
         ctx["kept"] = {"xs": xs, "plan": plan, "gens": gens}
     else:
@@ -775,6 +790,8 @@ def rank_main(args):
         # the headline is in hand: from here on a failed or hung design (or
         # check) is recorded in the line and cannot cost it
         out["exchange"] = r["exchange"]
+        # the exchange against the links: says by itself whether N is link- or kernel-bound
+        out["roofline"]["exchange"] = r["exchange"].get("model")
         out["exchange_variants"] = [variant_summary(r)]
         out["variant_timeout_seconds"] = args.variant_timeout
         with wd.lock:

@@ -281,4 +281,14 @@ def variant_summary(x: dict) -> dict:
             "kernel_ms_per_step": x["kernel_ms_per_step"], "kernel": x["kernel"], "chunks": x["chunks"],
             "xchg_ms": x["exchange"]["ms_per_step"], "bytes_per_rank_per_step": x["exchange"]["bytes_per_rank_per_step"],
             "algbw_GBps": x["exchange"]["algbw_GBps"], "busbw_GBps": x["exchange"]["busbw_GBps"],
-            "collective": x["exchange"]["collective"], "check_digest": x.get("check_digest")}
+            "collective": x["exchange"]["collective"], "check_digest": x.get("check_digest"),
+            "exchange_model": _model_brief(x["exchange"].get("model"))}
+
+
+def _model_brief(m):
+    """A design's exchange model in its variant entry (the full one is the
+    headline's roofline.exchange)."""
+    if not m:
+        return None
+    return {k: m[k] for k in ("bytes_per_link_per_step", "link_ms_at_peak", "link_frac", "predicted_ms_per_step",
+                              "bound", "mode")}

@@ -148,3 +148,79 @@ def draw_loop_ceilings(local_rank: int | None = None) -> dict:
         if r:
             out[kind] = r
     return out
+
+
+# ---------------------------------------------------------------------------
+# N > 1: the exchange step against the xGMI links
+# ---------------------------------------------------------------------------
+XGMI_LINK_GBPS_PER_DIRECTION = 76.5
+XGMI_SOURCE = ("the task brief's MI355X node figure, 7 xGMI links x ~153 GB/s per GPU, read as both directions "
+               "of a link together (76.5 GB/s each way; if 153 is per direction every link_frac halves); "
+               "MI355X_MICROARCH.md states no xGMI figure")
+
+
+def exchange_model(design: str, world: int, n_elems: int, kernel_ms: float, xchg_ms: float, chunks: int,
+                   mode: str = "measured") -> dict | None:
+    """The N > 1 step as DESIGN.md §5 models it: per rank, the masking
+    kernel of its shape, and the exchange's bytes on its busiest directed
+    xGMI link, with chunk j's exchange overlapping chunk j+1's masking:
+
+        predicted_ms_per_step = max(kernel, link) + min(kernel, link) / chunks
+
+    ``link`` = bytes on the busiest directed link / the per-link peak.  The
+    replaced transfer is the reference's masked-vector ``.to(server)``
+    (sfl/distributed/op_strategy.py:131-141, sparse_plain_aggregator.py:86).
+    ``mode``: "measured" (the driver's node), "rehearsal" (one GPU, host
+    stand-ins: the fields are the model's, the timings not xGMI's) or
+    "dry-run" (no GPU).  None at world 1 or without an exchange."""
+    if world <= 1 or design == "elements":
+        return None
+    n = int(n_elems)
+    if design in ("sharded", "direct"):
+        per_link = 8 * n / world
+        what = ("every rank's uint64 partial-sum shard for each peer crosses one link (all W-1 links of a GPU "
+                "busy, both directions): 8N/W bytes per directed link")
+    elif design == "sharded+gather":
+        per_link = 16 * n / world
+        what = ("8N/W bytes of uint64 shard per directed link, then the float64 shards gathered into rank 0 "
+                "(another 8N/W on each of its in-links)")
+    elif design == "elements+gather":
+        per_link = 8 * n / world
+        what = "no exchange for the sum; the float64 slices gathered into rank 0: 8N/W bytes per in-link"
+    elif design == "reduce":
+        per_link = 8 * n
+        what = "ncclReduce to rank 0: the full 8N-byte partial sum passes each link of the reduction ring"
+    else:
+        return None
+    peak = XGMI_LINK_GBPS_PER_DIRECTION
+    link_ms = per_link / (peak * 1e9) * 1e3
+    chunks = max(1, int(chunks))
+    if kernel_ms is None:
+        predicted = None
+    else:
+        predicted = max(kernel_ms, link_ms) + min(kernel_ms, link_ms) / chunks
+    achieved = per_link / (xchg_ms / 1e3) / 1e9 if xchg_ms and xchg_ms > 0 else None
+    return {"mode": mode, "bytes_per_link_per_step": per_link, "schedule": what,
+            "peak_GBps_per_link_direction": peak, "peak_source": XGMI_SOURCE,
+            "link_ms_at_peak": link_ms, "kernel_ms_per_step": kernel_ms, "exchange_ms_per_step": xchg_ms,
+            "achieved_GBps_per_link": achieved, "link_frac": achieved / peak if achieved else None,
+            "predicted_ms_per_step": predicted,
+            "bound": None if kernel_ms is None else ("link" if link_ms > kernel_ms else "kernel"),
+            "note": ("exchange_ms_per_step is the comm stream's time per step (HIP events, max over ranks); "
+                     "achieved_GBps_per_link = bytes_per_link_per_step / that time")}
+
+
+def committed_kernel_ms(clients: int, world: int, n_elems: int) -> tuple[float | None, str | None]:
+    """Rank 0's masking-kernel time per step for C clients over W GPUs from
+    the newest committed tools/kernel_bench.py run (scaled linearly from its
+    element count), for --dry-run's exchange model; (None, None) if absent."""
+    for d in PMC_DIRS:
+        path = os.path.join(d, "kernel_bench_shapes.json")
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            kb = json.load(f)
+        for c in kb.get("cases", []):
+            if c.get("C") == clients and c.get("W") == world and c.get("path") == "fused":
+                return c["ms_median"] * n_elems / kb["elems"], os.path.relpath(path, ROOT)
+    return None, None

@@ -404,3 +404,27 @@ def test_gpu_context_guard_reads_proc(tmp_path):
         assert gpu_context_holders([os.getpid(), os.getppid(), 2**22 + 7], str(dev)) == [os.getpid()]
         del f
     assert "10x slower" in rehearsal_refusal([123], 8)
+
+
+def test_dry_run_n8_line_carries_the_exchange_model():
+    """at N > 1 the line says by itself whether the step
+    is link- or kernel-bound -- roofline.exchange with the bytes per link,
+    the assumed per-link peak and its source, and the predicted step from
+    the rank's kernel time (--dry-run: the committed per-rank kernel time)."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--dry-run", "--cpu-baseline-seconds", "0",
+                        "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    m = line["roofline"]["exchange"]
+    assert m["mode"] == "dry-run" and m["bytes_per_link_per_step"] == 8 * 100_000_000 / 8
+    assert m["peak_GBps_per_link_direction"] > 0 and "xGMI" in m["peak_source"]
+    assert m["kernel_ms_per_step"] and m["predicted_ms_per_step"] >= max(m["kernel_ms_per_step"], m["link_ms_at_peak"])
+    assert m["bound"] in ("link", "kernel")
+    models = {v["name"]: v["exchange_model"] for v in line["exchange_variants"]}
+    assert models["elements"] is None and models["reduce"]["bytes_per_link_per_step"] == 8 * 100_000_000
+    import benchkit.roofline as R
+
+    assert R.exchange_model("sharded", 1, 10, 1.0, 1.0, 8) is None
+    mm = R.exchange_model("direct", 4, 10**8, 0.9, 3.0, 8, "rehearsal")
+    assert mm["link_frac"] == pytest.approx(2e8 / 3e-3 / 1e9 / R.XGMI_LINK_GBPS_PER_DIRECTION)
