@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SA_ABI_VERSION 2
+#define SA_ABI_VERSION 3
 
 /* status codes */
 #define SA_OK 0
@@ -246,24 +246,24 @@ int sa_xor_u64(const uint64_t* v, uint64_t n, uint64_t* digest, void* stream);
 #define SA_DP_PARTIALS 1024 /* doubles of scratch for sa_sumsq_f32 */
 
 typedef struct sa_dp {
-  const double* sumsq;       /* device: sum of x^2 over the clipping group (sa_sumsq_f32) */
-  const double* sumsq_layer; /* device, optional: this layer's sum of squares */
-  float l2_norm_clip;
+  const double* sumsq;       /* device: the clipping group's squared norm (sa_sumsq_f32) */
+  const double* sumsq_layer; /* device, optional: this layer's squared norm */
+  double l2_norm_clip;       /* the reference's python float (the clip divides in float64) */
   float noise_std;   /* sigma */
   float num_updates; /* divisor of the noise (> 0) */
-  uint32_t reserved;
   uint64_t key;      /* Philox key */
   uint64_t counter0; /* noise index of element 0 (multiple of 4) */
 } sa_dp;
 
-/* *sumsq (+)= this layer's squared L2 norm as the reference forms it
- * (mechanism_fl.py:132-135 on float32 arrays): sum x[i]^2 by a
- * deterministic fixed-order float64 reduction, rounded to float32, then
- * np.linalg.norm's float32 sqrt and ** 2 in float32; accumulating layers add
- * in float32 (the reference's python sum), the float32 value held in the
- * double.  (The reference's float32 BLAS dot accumulates in float32; here
- * the dot is exact to float64 before its one rounding -- DESIGN.md §4.)
- * `partials` is caller scratch of SA_DP_PARTIALS doubles.  ABI version 2. */
+/* *sumsq (+)= this layer's squared L2 norm as the reference forms it under
+ * its numpy 1.23.5 (mechanism_fl.py:132-135 on float32 arrays):
+ * np.linalg.norm is a float32 dot and a float32 sqrt (here the dot is the
+ * deterministic fixed-order float64 sum of x[i]^2 rounded once to float32;
+ * the reference's BLAS sdot adds in float32 in its own order);
+ * `** 2` of that float32 scalar with a python int is float64 in numpy 1.x
+ * (scalar-scalar operations promote without value-based casting), so the
+ * square is exact; python's sum adds the layers in float64 from 0.
+ * `partials` is caller scratch of SA_DP_PARTIALS doubles.  ABI version 3. */
 int sa_sumsq_f32(const float* x, uint64_t n, double* partials, double* sumsq, int accumulate, void* stream);
 
 /* out = clip-and-noise(x) (out may alias x). */

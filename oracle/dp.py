@@ -6,7 +6,12 @@ it).
   :71 (global norm), :81-84 (per-layer scale), :104-108 (global scale),
   :112-127 (noise / num_updates, np.add), :132-135 (global_norm: float32
   np.linalg.norm per layer, ** 2, python sum, np.sqrt), with numpy 1.23.5's
-  scalar promotion (the reference's pin, uv.lock:1189-1190).  One deviation:
+  scalar promotion (the reference's pin, uv.lock:1189-1190): an operation
+  between two scalars promotes by type alone (no value-based casting), so a
+  python int / float meets a float32 scalar as int64 / float64 -- ``** 2``,
+  the python sum, ``np.sqrt`` of it and ``clip / norm`` are all float64;
+  value-based casting applies only with an array (the float32 array times
+  the float64 scale stays float32).  One deviation:
   the layer's dot is the exact float64 sum rounded once to float32, where
   the reference's BLAS sdot accumulates in float32 in its own order
   (|difference| <= n * 2^-24 of the dot in the worst case).
@@ -60,39 +65,45 @@ def gauss(key: int, counter0: int, n: int) -> np.ndarray:
     return z.reshape(-1)[off:off + n]
 
 
-def layer_sq_norm(a) -> np.float32:
-    """One layer's ``np.linalg.norm(a) ** 2`` as the reference evaluates it on
-    a float32 array (mechanism_fl.py:133, numpy 1.23.5): the float32 dot --
-    here the exact float64 sum rounded once (the reference's BLAS sdot adds
-    in float32 in its own order) -- np.sqrt in float32, then
-    ``** 2`` in float32."""
+def layer_norm32(a) -> np.float32:
+    """``np.linalg.norm(a)`` of a float32 array (numpy 1.23.5: ``sqrt(x.dot(x))``
+    in float32) -- the dot here the exact float64 sum rounded once (the
+    reference's BLAS sdot adds in float32 in its own order)."""
     dot = np.float32(np.sum(np.asarray(a, dtype=np.float64).reshape(-1) ** 2))
-    norm = np.sqrt(dot, dtype=np.float32)
-    return np.float32(norm * norm)
+    return np.sqrt(dot, dtype=np.float32)
 
 
-def global_sq(inputs) -> np.float32:
+def layer_sq_norm(a) -> np.float64:
+    """One layer's ``np.linalg.norm(a) ** 2`` (mechanism_fl.py:133) under numpy
+    1.23.5: the float32 norm ``** 2`` (a python int) is a scalar-scalar
+    operation, promoted to float64 -- the exact square."""
+    n = np.float64(layer_norm32(a))
+    return n * n
+
+
+def global_sq(inputs) -> np.float64:
     """``sum([np.linalg.norm(i) ** 2 for i in inputs])``: python's sum from 0
-    over float32 scalars stays float32 (mechanism_fl.py:133)."""
-    t = np.float32(0)
+    over the float64 squares, in order (mechanism_fl.py:133)."""
+    t = np.float64(0)
     for a in inputs:
-        t = np.float32(t + layer_sq_norm(a))
+        t = t + layer_sq_norm(a)
     return t
 
 
 def clip_scale(sumsq, clip: float, sumsq_layer=None) -> np.float32:
     """min(1, clip / norm) as mechanism_fl.py:71-84,104-108 computes it under
-    numpy 1.23.5: ``sumsq`` / ``sumsq_layer`` the float32 squared norms
-    (global_sq, layer_sq_norm); norm = np.sqrt in float32; the per-layer
-    denominator np.sqrt(layer_norm * norm) in float32; a python-float clip
-    divided by a float32 scalar is a float64 division (value-based casting
-    of two scalars); multiplying the float32 array rounds it to float32."""
-    norm_all = np.sqrt(np.float32(sumsq), dtype=np.float32)
+    numpy 1.23.5, all in float64 scalars: norm_all = np.sqrt(sumsq) (float64,
+    ``global_norm``); per layer the denominator np.sqrt(layer_norm *
+    norm_all) with layer_norm = np.sqrt(layer square) (= the float32 norm,
+    exactly); the python-float clip divided in float64.  ``inputs[i] *
+    scale`` then rounds the float64 scale to float32 (value-based casting: an
+    array times a scalar keeps the array's float32)."""
+    norm_all = np.sqrt(np.float64(sumsq))
     denom = norm_all
     if sumsq_layer is not None:
-        denom = np.sqrt(np.float32(np.sqrt(np.float32(sumsq_layer), dtype=np.float32) * norm_all), dtype=np.float32)
+        denom = np.sqrt(np.sqrt(np.float64(sumsq_layer)) * norm_all)
     with np.errstate(divide="ignore", invalid="ignore"):
-        r = np.float64(np.float32(clip)) / np.float64(denom)
+        r = np.float64(float(clip)) / denom
     return np.float32(r) if r < 1.0 else np.float32(1)
 
 

@@ -24,7 +24,7 @@ SA_F32, SA_F64, SA_I64 = 0, 1, 2
 SA_FLAG_PRG_REJECT = 1
 SA_UNIQUE_ID_BYTES = 128
 SA_DP_PARTIALS = 1024
-ABI_VERSION = 2  # include/sfl_sa.h SA_ABI_VERSION (2: sa_sumsq_f32 forms the reference's float32 norm)
+ABI_VERSION = 3  # include/sfl_sa.h SA_ABI_VERSION (3: the DP norm / clip follow numpy 1.23.5's float64 scalars)
 TUNING_ABI_OFFSET = 1000  # sa_abi_version() of an SA_ABLATE / SA_TIMING build
 
 # every symbol include/sfl_sa.h declares (checked by tests/test_boundary.py)
@@ -73,8 +73,8 @@ class LocalClient(C.Structure):
 
 class DP(C.Structure):
     """sa_dp: GaussianModelDP pre-step parameters."""
-    _fields_ = [("sumsq", C.c_void_p), ("sumsq_layer", C.c_void_p), ("l2_norm_clip", C.c_float),
-                ("noise_std", C.c_float), ("num_updates", C.c_float), ("reserved", C.c_uint32),
+    _fields_ = [("sumsq", C.c_void_p), ("sumsq_layer", C.c_void_p), ("l2_norm_clip", C.c_double),
+                ("noise_std", C.c_float), ("num_updates", C.c_float),
                 ("key", C.c_uint64), ("counter0", C.c_uint64)]
 
 

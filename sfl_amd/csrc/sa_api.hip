@@ -361,18 +361,29 @@ static int launch_cross_group(const sa_mask_stream* ms, int cnt, uint64_t n, uin
   return fn(a, stream);
 }
 
+// the masks-only launch sizes for `count` one-sided streams: the largest
+// instantiated count (kCrossCounts) that fits the remaining streams
+static int cross_launch_size(int remaining) {
+  for (int c : kCrossCounts)
+    if (c <= remaining) return c;
+  return 1;
+}
+
+// every masks-only kernel the schedule of `count` streams needs exists
+// (checked before anything is launched: see sa_fused_clients)
+static bool cross_plan_instantiated(int count) {
+  for (int j = 0; j < count; j += cross_launch_size(count - j))
+    if (!find_clients_kernel(SA_F32, SA_F32, 1, cross_launch_size(count - j), kLean1 | kSumOnly | kCrossOnly))
+      return false;
+  return true;
+}
+
 // sum_out += the masks of `count` one-sided streams, in launches of the
 // largest instantiated count (kCrossCounts) that fits the remaining streams.
 static int launch_cross(const sa_mask_stream* ms, int count, uint64_t n, uint64_t* sum_out, uint32_t* flags,
                         void* stream) {
   for (int j = 0; j < count;) {
-    const int r = count - j;
-    int cnt = 1;
-    for (int c : kCrossCounts)
-      if (c <= r) {
-        cnt = c;
-        break;
-      }
+    const int cnt = cross_launch_size(count - j);
     const int rc = launch_cross_group(ms + j, cnt, n, sum_out, flags, stream);
     if (rc) return rc;
     j += cnt;
@@ -434,10 +445,23 @@ extern "C" int sa_fused_clients(const sa_local_client* clients, int n_clients, i
         else
           rest[nr++] = cross[c * n_cross + j];
       }
+    // all-or-nothing: SA_ERR_UNSUPPORTED tells the caller nothing ran (it
+    // then masks client by client into the same sum_out), so every kernel
+    // of the schedule is looked up BEFORE the first launch, and a failure
+    // after it is reported as SA_ERR_HIP (sum_out partly written)
+    if (!cross_plan_instantiated(nr)) {
+      sa_set_error("sa_fused_clients: no masks-only kernel for part of %d cross streams", nr);
+      return SA_ERR_UNSUPPORTED;
+    }
     const int rc = sa_fused_clients(clients, L, x_type, n, fxp_bits, pair_gens, pair_sign, first, X1, sum_out,
                                     accumulate, nullptr, flags, stream);
     if (rc) return rc;
-    return n == 0 ? SA_OK : launch_cross(rest, nr, n, sum_out, flags, stream);
+    const int rc2 = n == 0 ? SA_OK : launch_cross(rest, nr, n, sum_out, flags, stream);
+    if (rc2 == SA_ERR_UNSUPPORTED) {
+      sa_set_error("sa_fused_clients: masks-only launch failed after the first launch (sum_out partly written)");
+      return SA_ERR_HIP;
+    }
+    return rc2;
   }
   if (!aligned16(sum_out)) {
     sa_set_error("sa_fused_clients: sum_out must be 16-byte aligned");

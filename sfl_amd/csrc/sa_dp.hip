@@ -14,41 +14,68 @@ namespace sa {
 
 int occupancy_blocks(const void* kernel);  // sa_api.hip
 
-// per-block partial sums of x^2 in fp64 -> partials[blockIdx.x]
+// per-block partial sums of x^2 in fp64 -> partials[blockIdx.x].  Two
+// non-temporal 16-byte loads in flight per lane at a 1,024-block grid: the
+// fastest of the forms tools/microbench/sumsq_rate.hip timed on MI355X
+// (0.065 ms for 100M floats with the final step, 0.77 of HBM, where round
+// 4's one load per lane took 0.077 ms; larger grids and a last-block fused
+// final step -- whose device-wide fence costs ~45 us -- were slower).  The
+// grid depends on n only, so the partials, and the float64 sum, are the
+// same on every board and every run.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSumsqUnroll = 2;
+
+__device__ __forceinline__ double sq4(f32x4 v) {
+  return (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+}
+
+__device__ __forceinline__ double block_sum256(double acc) {
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  __shared__ double w[4];
+  if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  return (w[0] + w[1]) + (w[2] + w[3]);
+}
+
 __global__ void __launch_bounds__(256) k_sumsq_partial(const float* __restrict__ x, uint64_t n,
                                                        double* __restrict__ partials) {
   double acc = 0.0;
   const uint64_t n4 = n / 4;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    const float4 v = reinterpret_cast<const float4*>(x)[i];
-    acc += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (kSumsqUnroll - 1) * stride < n4; i += kSumsqUnroll * stride) {
+    f32x4 v[kSumsqUnroll];
+#pragma unroll
+    for (int u = 0; u < kSumsqUnroll; u++) v[u] = __builtin_nontemporal_load(x4 + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < kSumsqUnroll; u++) acc += sq4(v[u]);
   }
+  for (; i < n4; i += stride) acc += sq4(__builtin_nontemporal_load(x4 + i));
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
     const double v = x[n4 * 4 + threadIdx.x];
     acc += v * v;
   }
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  __shared__ double w[4];
-  if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) partials[blockIdx.x] = (w[0] + w[1]) + (w[2] + w[3]);
+  const double b = block_sum256(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = b;
 }
 
 // fixed-order sum of the partials (deterministic), then the layer's squared
-// norm as the reference forms it in float32 (mechanism_fl.py:132-135,
-// numpy 1.23.5 on float32 arrays): np.linalg.norm -> sqrt(float32 x.x), ** 2
-// in float32, and the layers' values summed in float32 (python sum from 0)
-// -> *out (or += *out in float32), a float32 value held in a double
-__global__ void __launch_bounds__(64) k_sumsq_final(const double* __restrict__ partials, int k, double* out,
-                                                    int accumulate) {
+// norm as the reference forms it (mechanism_fl.py:132-135 under numpy
+// 1.23.5): np.linalg.norm of a float32 array is sqrt(float32 x.x) in
+// float32; `** 2` of that float32 scalar with a python int is a float64
+// square (numpy 1.x promotes scalar-scalar operations without value-based
+// casting), exact; python's sum adds the layers in float64 from 0 ->
+// *out (or *out + sq)
+__global__ void __launch_bounds__(256) k_sumsq_final(const double* __restrict__ partials, int k, double* out,
+                                                     int accumulate) {
   double acc = 0.0;
-  for (int j = threadIdx.x; j < k; j += 64) acc += partials[j];
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  for (int j = threadIdx.x; j < k; j += 256) acc += partials[j];
+  acc = block_sum256(acc);
   if (threadIdx.x == 0) {
-    const float norm = sqrt_f32_rn((float)acc);  // np.linalg.norm: float32 dot, float32 sqrt
-    const float sq = __fmul_rn(norm, norm);      // ** 2
-    *out = accumulate ? (double)__fadd_rn((float)*out, sq) : (double)sq;
+    const float norm = sqrt_f32_rn((float)acc);        // np.linalg.norm: float32 dot, float32 sqrt
+    const double sq = __dmul_rn((double)norm, norm);  // ** 2: float64, exact
+    *out = accumulate ? __dadd_rn(*out, sq) : sq;
   }
 }
 
@@ -58,7 +85,8 @@ struct DpArgs {
   uint64_t n;
   const double* sumsq;
   const double* sumsq_layer;
-  float clip, sigma, updates, inv;  // inv: exact_recip_pow2(updates) or 0
+  double clip;                   // python float (the clip divides in float64)
+  float sigma, updates, inv;     // inv: exact_recip_pow2(updates) or 0
   uint64_t key, block0;
 };
 
@@ -102,15 +130,14 @@ extern "C" int sa_sumsq_f32(const float* x, uint64_t n, double* partials, double
     sa_set_error("sa_sumsq_f32: bad arguments (x must be 16-byte aligned)");
     return SA_ERR_ARG;
   }
-  const int maxb = occupancy_blocks((const void*)&k_sumsq_partial);
-  if (maxb <= 0) return SA_ERR_HIP;
+  // the grid depends on n only (not on the device's occupancy): the same
+  // partials, so the same float64 sum, on every board
   uint64_t want = (n / 4 + 255) / 256;
   if (want < 1) want = 1;
-  int grid = (int)(want < (uint64_t)maxb ? want : (uint64_t)maxb);
-  if (grid > SA_DP_PARTIALS) grid = SA_DP_PARTIALS;
+  const int grid = (int)(want < (uint64_t)SA_DP_PARTIALS ? want : (uint64_t)SA_DP_PARTIALS);
   hipLaunchKernelGGL(k_sumsq_partial, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, n, partials);
   SA_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_sumsq_final, dim3(1), dim3(64), 0, (hipStream_t)stream, partials, grid, sumsq,
+  hipLaunchKernelGGL(k_sumsq_final, dim3(1), dim3(256), 0, (hipStream_t)stream, partials, grid, sumsq,
                      accumulate);
   SA_HIP_CHECK(hipGetLastError());
   return SA_OK;

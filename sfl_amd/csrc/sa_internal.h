@@ -98,7 +98,8 @@ struct KArgs {
   uint32_t masked_mask;
   // GaussianModelDP pre-step fused into quantize (single-client fp32 only)
   int32_t dp_on;
-  float dp_clip, dp_sigma, dp_updates, dp_inv;  // dp_inv: exact_recip_pow2(dp_updates) or 0
+  float dp_sigma, dp_updates, dp_inv;  // dp_inv: exact_recip_pow2(dp_updates) or 0
+  double dp_clip;                      // python float: the reference divides by it in float64
   const double* dp_sumsq;
   const double* dp_sumsq_layer;
   uint64_t dp_key, dp_block0;  // Philox key; counter block of element 0

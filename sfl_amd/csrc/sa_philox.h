@@ -109,25 +109,25 @@ __device__ __forceinline__ float dp_apply(float x, float scale, float z, float s
   return __fadd_rn(__fmul_rn(x, scale), inv != 0.0f ? __fmul_rn(zs, inv) : __fdiv_rn(zs, updates));
 }
 
-// scale = min(1, clip / norm) in float32 (mechanism_fl.py:107); with a layer
-// sum of squares, min(1, clip / sqrt(norm_layer * norm_all)) (:81-84).
-// The clip scale as GaussianModelDP computes it under the reference's numpy
-// 1.23.5 (mechanism_fl.py:71-84,104-108,132-135), from sa_sumsq_f32's float32
-// squared norms: norm = np.sqrt(float32 sum) in float32; the per-layer
-// denominator np.sqrt(layer_norm * norm) in float32; clip / denom with a
-// python-float clip is a float64 division (value-based casting of two
-// scalars); the float32 array times that float64 scalar rounds it to float32.
+// scale = min(1, clip / norm) (mechanism_fl.py:107); with a layer squared
+// norm, min(1, clip / sqrt(norm_layer * norm_all)) (:81-84).
 // float32 sqrt correctly rounded, as numpy's np.sqrt on float32: the float64
 // square root rounded to float32 (innocuous double rounding for sqrt: 53 >=
 // 2*24 + 2); gfx950's v_sqrt_f32 is 1 ulp, which the reference would see as
 // a different clip scale.
-__device__ __forceinline__ float sqrt_f32_rn(float x) { return (float)sqrt((double)x); }
+__device__ __forceinline__ float sqrt_f32_rn(float x) { return (float)__dsqrt_rn((double)x); }
 
-__device__ __forceinline__ float dp_scale(const double* sumsq, const double* sumsq_layer, float clip) {
-  const float norm_all = sqrt_f32_rn((float)*sumsq);
-  float denom = norm_all;
-  if (sumsq_layer) denom = sqrt_f32_rn(__fmul_rn(sqrt_f32_rn((float)*sumsq_layer), norm_all));
-  const double r = __ddiv_rn((double)clip, (double)denom);
+// numpy 1.23.5, scalars only from the squared norms on (sa_sumsq_f32: float64
+// values): norm_all = np.sqrt(float64 sum); per layer np.sqrt(layer_norm *
+// norm_all) with layer_norm = np.sqrt(its float64 square) (the float32 norm,
+// exactly); clip / denom in float64; min(1, r); the float32 array times
+// that float64 scalar (value-based casting: the scalar rounds to float32).
+// Device double sqrt / div are the correctly rounded IEEE operations.
+__device__ __forceinline__ float dp_scale(const double* sumsq, const double* sumsq_layer, double clip) {
+  const double norm_all = __dsqrt_rn(*sumsq);
+  double denom = norm_all;
+  if (sumsq_layer) denom = __dsqrt_rn(__dmul_rn(__dsqrt_rn(*sumsq_layer), norm_all));
+  const double r = __ddiv_rn(clip, denom);
   return r < 1.0 ? (float)r : 1.0f;
 }
 #endif

@@ -255,7 +255,8 @@ def make_dp(sumsq: torch.Tensor, *, l2_norm_clip: float, noise_std: float, num_u
 
 
 def sumsq_f32(x: torch.Tensor, out: torch.Tensor, partials: torch.Tensor, *, accumulate: bool = False) -> torch.Tensor:
-    """out[0] (+)= sum(x^2) in float64 (deterministic)."""
+    """out[0] (+)= the layer's squared norm as the reference forms it (the
+    float32 np.linalg.norm, squared in float64; sa_sumsq_f32)."""
     _require_gpu(x, out, partials)
     if x.dtype != torch.float32 or out.dtype != torch.float64 or partials.numel() < L.SA_DP_PARTIALS:
         raise ValueError("sumsq_f32: float32 x, float64 out, SA_DP_PARTIALS float64 partials")

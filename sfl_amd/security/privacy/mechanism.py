@@ -8,7 +8,9 @@ sqrt(||layer|| * ||all||))`` with ``is_clip_each_layer``) and
 ``N(0, sigma^2) / num_updates`` is added, ``sigma = noise_multiplier *
 l2_norm_clip * l2_norm_clip`` exactly as the reference writes it.
 
-Device work: ``sa_sumsq_f32`` (deterministic float64 norm), then
+Device work: ``sa_sumsq_f32`` (each layer's norm as the reference forms it:
+np.linalg.norm's float32 norm, squared and summed over the layers in
+float64 as numpy 1.23.5 does for these scalars), then
 ``sa_dp_perturb_f32`` (this class's ``__call__``: the perturbed arrays are
 materialised, as the reference returns them).  ``sa_mask_dp`` runs the
 same clip + noise inside the masking kernel, bit-identical; the loopback
@@ -61,7 +63,8 @@ class GaussianModelDP:
         return t.clone() if t.data_ptr() % 16 else t
 
     def sumsq(self, xs: List[torch.Tensor]) -> torch.Tensor:
-        """Device float64 sum of squares over all of ``xs`` (the global norm^2)."""
+        """``sum([np.linalg.norm(x) ** 2 for x in xs])`` on the device
+        (mechanism_fl.py:133): float32 layer norms, float64 squares and sum."""
         out = torch.zeros(1, dtype=torch.float64, device=self.device)
         part = torch.empty(L.SA_DP_PARTIALS, dtype=torch.float64, device=self.device)
         for x in xs:
@@ -101,8 +104,10 @@ class GaussianModelDP:
         return out
 
     def global_norm(self, inputs) -> float:
+        """``np.sqrt(sum(norm ** 2))`` in float64, as the reference's
+        ``global_norm`` returns it under numpy 1.23.5 (mechanism_fl.py:132-135)."""
         xs = [self._flat(a) for a in inputs]
-        return float(np.sqrt(self.sumsq(xs).item()))
+        return float(np.sqrt(np.float64(self.sumsq(xs).item())))
 
 
 class DPStrategyFL:

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(declared) == set(L.EXPORTED)
-    assert lib.sa_abi_version() == 2
+    assert lib.sa_abi_version() == 3
 
 
 def test_library_is_built_for_gfx950():

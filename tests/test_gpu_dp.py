@@ -34,16 +34,18 @@ def _sumsq(x):
 
 @pytest.mark.parametrize("n", [1, 3, 4, 1027, 1_000_003])
 def test_sumsq_deterministic_and_accurate(n):
-    """sa_sumsq_f32 = the layer's np.linalg.norm(x) ** 2 in float32 as the
-    reference forms it (oracle layer_sq_norm), deterministic; accumulating
-    two layers adds in float32 (the reference's python sum)."""
+    """sa_sumsq_f32 = the layer's np.linalg.norm(x) ** 2 as the reference
+    forms it under numpy 1.23.5 (oracle layer_sq_norm: the float32 norm
+    squared in float64), deterministic; accumulating two layers adds in
+    float64 (the reference's python sum)."""
     x = torch.randn(n, device=DEV)
     a, b = _sumsq(x), _sumsq(x)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     xh = x.cpu().numpy()
     assert a.item() == float(D.layer_sq_norm(xh))
-    assert np.float32(a.item()) == a.item()  # a float32 value
+    nrm = np.sqrt(a.item())
+    assert np.float32(nrm) == nrm and nrm * nrm == a.item()  # the exact square of a float32 norm
     from sfl_amd import _lib as L
 
     part = torch.empty(L.SA_DP_PARTIALS, dtype=torch.float64, device=DEV)
