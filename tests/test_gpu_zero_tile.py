@@ -143,3 +143,88 @@ def test_every_stream_of_the_timed_shapes_at_exact_positions(world, pos, big_inp
             if got != want:
                 missed.append((j, n, got))
     assert not missed, f"world {world} (<{Lc},{X}>) zero at element {k}: (stream, n, flag) wrong: {missed}"
+
+
+def _flag_matrix(K, L, launch, n_streams, k):
+    """For each stream j: forced zero at element k; flag expected with
+    n = k + 1, none with n = k.  ``launch(j, zero, n, flags)`` runs the
+    launch set with stream j replaced.  Returns the wrong (j, n, flag)."""
+    zero = L.PCG64.of(*forced_zero_state_at(k))
+    dev = torch.device("cuda", 0)
+    flags = torch.zeros(1, dtype=torch.int32, device=dev)
+    missed = []
+    for j in range(n_streams):
+        for n, want in ((k + 1, True), (k, False)):
+            flags.zero_()
+            launch(j, zero, n, flags)
+            torch.cuda.synchronize()
+            got = bool(int(flags.item()) & L.SA_FLAG_PRG_REJECT)
+            if got != want:
+                missed.append((j, n, got))
+    return missed
+
+
+@pytest.mark.parametrize("pos", sorted(POSITIONS))
+def test_config5_rank_schedule_every_stream_at_exact_positions(pos, big_input):
+    """Config 5 at 8 GPUs, rank 0: 4 local clients, 6 internal pairs and 4 x
+    28 cross streams -- the multi-launch schedule the bench times (a fused
+    <4,4,4> launch, then 3 masks-only <1,32,14> launches adding into the sum).
+    Every one of the 118 streams (past the chunk join: every 5th) at the
+    exact element."""
+    K, L = _gpu()
+    from bench import pair_seed
+    from sfl_amd.parallel_sum import plan_generators, plan_rank
+
+    names = [f"client{c}" for c in range(32)]
+    plan = plan_rank(names, 8, 0)
+    Lc, X = len(plan.clients), len(plan.cross) // len(plan.clients)
+    assert (Lc, X) == (4, 28)
+    pg0, ps, cross0 = plan_generators(plan, pair_seed)
+    k = POSITIONS[pos]
+    s = torch.empty(k + 1, dtype=torch.int64, device=big_input.device)
+    streams = list(range(len(pg0) + len(cross0)))
+    if pos == "past_chunk_join":
+        streams = streams[::5] + [streams[-1]]
+
+    def launch(j, zero, n, flags):
+        pg, cross = list(pg0), list(cross0)
+        jj = streams[j]
+        if jj < len(pg):
+            pg[jj] = zero
+        else:
+            g, sign, peer = cross[jj - len(pg)]
+            cross[jj - len(pg)] = (zero, sign, peer)
+        K.fused_clients([big_input[:n]] * Lc, [1.0] * Lc, pg, ps, cross, X, s[:n], flags=flags)
+
+    missed = _flag_matrix(K, L, launch, len(streams), k)
+    assert not missed, f"config-5 rank schedule, zero at element {k}: (stream, n, flag) wrong: {missed}"
+
+
+@pytest.mark.parametrize("pos", sorted(POSITIONS))
+def test_bipartite_block_every_stream_at_exact_positions(pos, big_input):
+    """The masks-only sa_fused_bipartite launch (k_clients<8,0,1>: the 16 pairs
+    between two quads of co-located clients; config 5 on one GPU runs 24 of
+    them per step): each of its 16 streams at the exact element."""
+    import ctypes as C
+
+    K, L = _gpu()
+    names = [f"client{c}" for c in range(8)]
+    seeds = o.seeds_for(names)
+    gens0 = [L.pcg64_from_seed(seeds[names[i]][names[4 + j]]) for i in range(4) for j in range(4)]
+    signs = (C.c_int8 * 16)(*[1 if (i + j) % 2 else -1 for i in range(4) for j in range(4)])
+    clients = (L.LocalClient * 8)()
+    for c in range(8):
+        clients[c].x, clients[c].weight, clients[c].masked_out = None, 1.0, None
+    k = POSITIONS[pos]
+    s = torch.zeros(k + 1, dtype=torch.int64, device=big_input.device)
+
+    def launch(j, zero, n, flags):
+        gens = list(gens0)
+        gens[j] = zero
+        L.check(L.lib().sa_fused_bipartite(clients, L.SA_F32, n, 18, (L.PCG64 * 16)(*gens), signs,
+                                           C.c_void_p(s.data_ptr()), 1, C.c_void_p(flags.data_ptr()),
+                                           C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                "sa_fused_bipartite")
+
+    missed = _flag_matrix(K, L, launch, 16, k)
+    assert not missed, f"bipartite block, zero at element {k}: (stream, n, flag) wrong: {missed}"
