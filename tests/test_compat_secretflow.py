@@ -326,3 +326,114 @@ def test_gpu_subclass_after_install_and_rounds(monkeypatch, gpu_cluster):
         got = fs.reveal(out)["model_params"]
         exp = o.decode(o.server_sum([o.quantize(v.reshape(-1)) for v in x]), divisor=2)
         assert np.array_equal(got.reshape(-1), exp)
+
+
+# ------------------------------------------------------------ payload fuzz
+def _random_payload(rng, n_layers, shapes, dtypes):
+    out = []
+    for sh, dt in zip(shapes, dtypes):
+        if dt == np.int64:
+            out.append(rng.integers(-2**20, 2**20, size=sh).astype(np.int64))
+        else:
+            out.append((rng.standard_normal(sh) * 10 ** rng.uniform(-3, 2)).astype(dt))
+    return out
+
+
+def _random_weight(rng, kind, shape):
+    if kind == "none":
+        return None
+    if kind == "int":
+        return int(rng.integers(1, 500))
+    if kind == "float":
+        return float(rng.uniform(0.1, 50))
+    if kind == "np_float64":
+        return np.float64(rng.uniform(0.1, 50))
+    if kind == "np_int64":
+        return np.int64(rng.integers(1, 500))
+    if kind == "array":  # per-element weights (CHANGELOG.md:994), broadcast to every layer
+        return rng.uniform(0.5, 5, size=shape).astype(np.float64)
+    raise ValueError(kind)
+
+
+def _expected_masked(layers, w, name, seeds, offset, fxp_bits=18):
+    """The oracle per layer (each layer its own numpy arithmetic type), the
+    layers' quantized values concatenated and masked from ``offset`` (the
+    reference's per-layer rng.integers calls draw consecutive positions)."""
+    q = np.concatenate([o.quantize(a, None if w is None else (np.broadcast_to(w, a.shape) if np.ndim(w) else w),
+                                   fxp_bits).reshape(-1) for a in layers])
+    return o.mask_client(q, name, seeds[name], offset)
+
+
+def test_payload_fuzz_vs_oracle(cpu_cluster):
+    """party.mask_payload / sum_decode over random payloads through the
+    spawned-party drop-in: list / tuple / single arrays, float32 / float64 /
+    int64 layers mixed in one payload, every weight kind (python int / float,
+    numpy scalars under numpy 1.23.5 value-based casting, per-element arrays,
+    device-object weights) -- every received masked vector and the result
+    bit-exact vs the oracle, stream positions carried across 12 rounds."""
+    _payload_fuzz(cpu_cluster, 2026, 12)
+
+
+@pytest.mark.gpu
+def test_gpu_payload_fuzz_vs_oracle(gpu_cluster):
+    """The same fuzz with the HIP steps in the party processes (sa_mask with
+    every compute type and weight form, sa_sum_u64 / sa_sum_f64 / sa_decode)."""
+    _payload_fuzz(gpu_cluster, 77, 18)
+
+
+def _payload_fuzz(c, seed, rounds):
+    from sfl_amd.compat import secretflow as hip
+
+    seeds, pair = _seeds()
+    agg = hip.SecureAggregator(c.pyu("carol"), [c.pyu(n) for n in NAMES], reveal=fs.reveal, seeds=pair)
+    rng = np.random.default_rng(seed)
+    offset = 0
+    kinds = ["none", "int", "float", "np_float64", "np_int64", "array"]
+    for rnd in range(rounds):
+        n_layers = int(rng.integers(1, 4))
+        width = int(rng.integers(1, 7))
+        shapes = [tuple(int(v) for v in rng.integers(1, 9, size=int(rng.integers(0, 3)))) + (width,)
+                  for _ in range(n_layers)]
+        container = ["array", "list", "tuple"][rnd % 3] if n_layers == 1 else ["list", "tuple"][rnd % 2]
+        dts = [rng.choice([np.float32, np.float64, np.int64]) for _ in shapes]
+        kind = kinds[rnd % len(kinds)]
+        average = kind != "none" or rnd % 2 == 0
+        payloads, ws = [], []
+        for nm in NAMES:
+            layers = _random_payload(rng, n_layers, shapes, dts)
+            payloads.append(layers)
+            ws.append(_random_weight(rng, kind, (width,)))
+        objs = []
+        for nm, layers in zip(NAMES, payloads):
+            v = layers[0] if container == "array" else (tuple(layers) if container == "tuple" else layers)
+            objs.append(_put(c.pyu(nm), v))
+        if kind == "none":
+            out = agg.average(objs, axis=0) if average else agg.sum(objs, axis=0)
+            wl = None
+        else:
+            wobj = [_put(c.pyu(nm), w) if rnd % 4 == 1 and not np.ndim(w) else w for nm, w in zip(NAMES, ws)]
+            out = agg.average(objs, axis=0, weights=wobj)
+            wl = ws
+        got = fs.reveal(out)
+        masked = [_expected_masked(layers, None if wl is None else wl[i], nm, seeds, offset)
+                  for i, (nm, layers) in enumerate(zip(NAMES, payloads))]
+        recv = [fs.reveal(m) for m in agg.last_masked]
+        for r, m in zip(recv, masked):
+            assert np.array_equal(r.u64, m), (rnd, kind, dts)
+        s = o.server_sum(masked)
+        if not average:
+            div = None
+        elif wl is None:
+            div = len(NAMES)
+        elif np.ndim(wl[0]):
+            div = np.concatenate([np.sum(np.stack([np.broadcast_to(w, sh).astype(np.float64) for w in wl]), axis=0)
+                                  .reshape(-1) for sh in shapes])
+        else:
+            div = sum(wl)
+        exp = o.decode(s, 18, div)
+        flat = got.reshape(-1) if container == "array" else np.concatenate([np.asarray(g).reshape(-1) for g in got])
+        assert np.array_equal(flat, exp), (rnd, kind, dts)
+        if container != "array":
+            assert isinstance(got, list if container == "list" else tuple) and len(got) == n_layers
+            assert [np.shape(g) for g in got] == shapes
+        offset += sum(int(np.prod(sh)) for sh in shapes)
