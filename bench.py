@@ -57,7 +57,7 @@ from benchkit.roofline import (HBM_PEAK_GBPS, PCG_ONE_DRAWS_8WAVE, PCG_PAIR_DRAW
                                PMC_DIRS, PMC_ELEMS, VALU_PEAK_WAVE_INSTR_PER_S, committed_kernel_ms,
                                draw_loop_ceilings, exchange_model, kernel_key, pmc_traffic, pmc_valu,
                                traffic_field)
-from benchkit.standin import HostStandinComm  # noqa: E402,F401
+from benchkit.standin import HostStandinComm, one_gpu_rccl_comm  # noqa: E402,F401
 
 
 # k_clients' variant flags (sfl_amd/csrc/sa_internal.h): the instantiation a
@@ -644,6 +644,10 @@ def main():
                     help="N>1 rehearsal on a one-GPU box: every rank on cuda:0, a gloo process group and the "
                          "collectives through a shared host mapping (RCCL refuses two ranks on one GPU); runs "
                          "every design's code path, its timings are not the product's")
+    ap.add_argument("--rehearse-comm", choices=("rccl", "standin"), default="rccl",
+                    help="--rehearse-one-gpu's data path: the product's RcclComm, the ranks made distinct RCCL "
+                         "'nodes' on the one GPU (NCCL_HOSTID per rank; RCCL's socket transport on lo), or the "
+                         "host stand-in (benchkit/standin.py)")
     ap.add_argument("--watchdog-seconds", type=float, default=480.0,
                     help="a rank still running after this long exits: with the headline done, rank 0 first "
                          "prints the line so far (Watchdog); before it, faulthandler dumps every thread's stack "
@@ -701,7 +705,7 @@ def rank_main(args):
     comm = None
     if multi and rehearse:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        comm = HostStandinComm(rank, world)
+        comm = HostStandinComm(rank, world) if args.rehearse_comm == "standin" else one_gpu_rccl_comm(rank, world)
     elif multi:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         comm = RcclComm(rank, world, local_rank)
@@ -779,9 +783,12 @@ def rank_main(args):
                               "issue": int_ops}},
     }
     if rehearse:
-        out["rehearsal"] = ("--rehearse-one-gpu: every rank on cuda:0, collectives and their barriers through a "
-                            "shared host mapping (benchkit/standin.py); the N > 1 control flow, not the "
-                            "product's rate")
+        out["rehearsal"] = ("--rehearse-one-gpu: every rank on cuda:0; " + (
+            "the product's RcclComm with a distinct NCCL_HOSTID per rank, so RCCL runs its collectives between the "
+            "ranks over its socket transport on lo (benchkit/standin.py one_gpu_rccl_comm)"
+            if args.rehearse_comm == "rccl" else
+            "collectives and their barriers through a shared host mapping (benchkit/standin.py)")
+            + "; the N > 1 control flow, not the product's rate")
     out["cpu_baseline"] = cpu
     check_local = r.pop("check_local")
     out["check"] = {"round": 0, "decoded_digest": None, "note": CHECK_NOTE}

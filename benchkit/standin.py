@@ -1,10 +1,34 @@
-"""The one-GPU rehearsal's stand-in for the RCCL communicator (bench.py
---rehearse-one-gpu; tests/test_gpu_dist_pipeline.py)."""
+"""The one-GPU rehearsal's communicators (bench.py --rehearse-one-gpu;
+tests/test_gpu_dist_pipeline.py): real RCCL between ranks that share the
+GPU (``one_gpu_rccl_comm``, the default) or the host stand-in
+(``HostStandinComm``)."""
 
 from __future__ import annotations
 
 import os
 import time
+
+
+def one_gpu_rccl_env(rank: int) -> dict:
+    """The environment that lets W ranks on ONE GPU form a real RCCL
+    communicator: RCCL refuses two ranks on one device of one host
+    ("Duplicate GPU detected", a (host hash, bus id) check), and NCCL_HOSTID
+    sets the host hash -- a distinct id per rank makes every rank its own
+    "node", so RCCL connects them through its network transport (sockets on
+    the loopback interface) and runs its collectives' own schedules at world
+    W (tools/rccl_hostid_probe.py; profiles/r05/rccl_hostid_w*.log).  Only
+    the wire differs from the node's xGMI."""
+    return {"NCCL_HOSTID": f"sfl-onegpu-rank{rank}", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1"}
+
+
+def one_gpu_rccl_comm(rank: int, world: int, group=None):
+    """The product's ``RcclComm`` for a rank of a one-GPU rehearsal (every
+    rank on device 0), after ``one_gpu_rccl_env``; the unique id travels
+    through the torch.distributed ``group`` (gloo) as on the node."""
+    os.environ.update(one_gpu_rccl_env(rank))
+    from sfl_amd.parallel_sum import RcclComm
+
+    return RcclComm(rank, world, 0, group)
 
 
 class HostStandinComm:

@@ -118,17 +118,23 @@ def check_1m():
     return oracle_check_in_child(8, 1000003)
 
 
+@pytest.mark.parametrize("comm", ["rccl", "standin"])
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_bench_n_ranks_every_design(world, check_1m):
+def test_bench_n_ranks_every_design(world, comm, check_1m):
+    """bench.py --gpus W with every design, W rank processes on this GPU:
+    comm "rccl" runs the product's RcclComm -- real RCCL collectives between
+    the ranks, each its own RCCL node (NCCL_HOSTID) over the socket
+    transport; "standin" the host stand-in."""
     if not has_gpu():
         pytest.skip("no GPU")
     env = rehearsal_env(dict(os.environ))
     t0, before = time.time(), host_counters()
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-one-gpu",
+                        "--rehearse-comm", comm,
                         "--elems", "1000003", "--steps", "3", "--warmup", "1", "--variant-steps", "2",
                         "--host-resident-steps", "3", "--cpu-baseline-seconds", "0", "--watchdog-seconds", "150"],
                        capture_output=True, text=True, timeout=170, env=env, cwd=ROOT)
-    _keep_stderr(f"every_design_w{world}", r, t0, before=before)
+    _keep_stderr(f"every_design_w{world}_{comm}", r, t0, before=before)
     if r.returncode != 0:  # the lines that say why (ranks interleave their output), then the tail
         why = [ln for ln in r.stderr.splitlines()
                if any(k in ln for k in ("Error", "error:", "Traceback", "watchdog", "still running", "exitcode",
@@ -147,6 +153,8 @@ def test_bench_n_ranks_every_design(world, check_1m):
         f"after {time.time() - t0:.0f} s: {line.get('exchange_variants')}\n" + _explain(r))
     # the headline is the reduce-scatter sharded server, measured first
     assert line["n_gpus"] == world and "rehearsal" in line and line["config"]["design"] == "sharded"
+    assert ("RcclComm" in line["rehearsal"]) == (comm == "rccl")
+    assert line["roofline"]["exchange"]["mode"] == "rehearsal" and line["roofline"]["exchange"]["bound"]
     assert "exchange_probe" not in line and line["exchange_variants"][0]["name"] == "sharded"
     # the headline with inputs and results in pinned host memory (H2D / D2H inclusive)
     hr = line["host_resident"]
@@ -310,7 +318,7 @@ def test_full_size_check_n1_vs_oracle(check_100m):
 def test_full_size_check_n8_rehearsal_vs_oracle(check_100m):
     """The N = 8 configuration at the headline size, rehearsed on this GPU (8
     rank processes, <1,7> lean launches, the 8-chunk pipelined sharded server
-    with host stand-ins of the reduce-scatter): the same digest as the
+    over real RCCL reduce-scatters between the ranks): the same digest as the
     oracle's and N = 1's -- the value the driver's SCALE lines must print."""
     line = _full_size_line("--gpus", "8", "--rehearse-one-gpu", "--watchdog-seconds", "140")
     assert line["check"]["decoded_digest"] == check_100m and line["config"]["clients_per_gpu"] == 1

@@ -3,13 +3,14 @@ block of clients through ``PipelinedMaskedSum`` (the bench's chunked fused
 launches, the comm stream and its per-chunk events, the in-place reduce) on
 the one GPU of the test box.
 
-RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so the
-exchange here is bench.py's rehearsal stand-in with RcclComm's contract
-(``benchkit.standin.HostStandinComm``: the ranks' host copies and barriers
-through a shared mapping): on the comm stream, after the chunk's event, the partial
-sum is reduced to the root IN PLACE (recv=None) -- uint64 addition mod
-2^64.  Everything else is the product code path the N > 1 bench
-runs.  The root's buffer must equal the oracle's server sum bit for bit, and
+The exchange is the product's ``RcclComm`` running real RCCL collectives
+between the W ranks (kind "rccl": RCCL refuses two ranks on one GPU of one
+host, so each rank gets its own NCCL_HOSTID and RCCL connects the "nodes"
+through its socket transport on lo -- ``benchkit.standin.one_gpu_rccl_comm``),
+and again through the host stand-in with the same contract (kind
+"standin"): on the comm stream, after the chunk's event, the partial sum
+is reduced to the root IN PLACE (recv=None) -- uint64 addition mod 2^64.
+Everything else is the product code path the N > 1 bench runs.  The root's buffer must equal the oracle's server sum bit for bit, and
 every client's digest the oracle's."""
 import os
 
@@ -70,7 +71,16 @@ def _with_dump(target, *args):
     target(*args)
 
 
-def _worker(rank, world, init, n, chunks, offset, q):
+def _comm(kind, rank, world):
+    """The exchange under test: the product's RcclComm with the ranks made
+    distinct RCCL nodes on the one GPU (real RCCL collectives over its socket
+    transport), or the host stand-in."""
+    from benchkit.standin import HostStandinComm, one_gpu_rccl_comm
+
+    return one_gpu_rccl_comm(rank, world) if kind == "rccl" else HostStandinComm(rank, world)
+
+
+def _worker(rank, world, init, n, chunks, offset, kind, q):
     import torch
     import torch.distributed as dist
 
@@ -87,9 +97,7 @@ def _worker(rank, world, init, n, chunks, offset, q):
         xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
         dev = torch.device("cuda", 0)
         plan = plan_rank(names, world, rank)
-        from bench import HostStandinComm
-
-        pipe = PipelinedMaskedSum(HostStandinComm(rank, world), dev, n, chunks)
+        pipe = PipelinedMaskedSum(_comm(kind, rank, world), dev, n, chunks)
         gens = [plan_generators(plan, seed_of, offset=offset + lo) for lo, _ in pipe.bounds]
         part = torch.empty(n, dtype=torch.int64, device=dev)
         dig = torch.zeros(len(plan.clients), dtype=torch.int64, device=dev)
@@ -108,18 +116,19 @@ def _worker(rank, world, init, n, chunks, offset, q):
         q.put((rank, repr(e), False, -1))
 
 
+@pytest.mark.parametrize("kind", ["rccl", "standin"])
 @pytest.mark.parametrize("world,chunks", [(2, 4), (4, 3), (8, 8)])
-def test_ranks_pipeline_and_in_place_reduce(world, chunks):
+def test_ranks_pipeline_and_in_place_reduce(world, chunks, kind):
     if torch.cuda.device_count() == 0:  # asked without initialising HIP here (conftest: this module runs early)
         pytest.skip("no GPU")
-    res = _run_ranks(_worker, world, (50_003, chunks, 10**9 + 5))
+    res = _run_ranks(_worker, world, (50_003, chunks, 10**9 + 5, kind))
     for rank, dig_ok, sum_ok, fl in res:
         assert dig_ok is True, (rank, dig_ok)
         assert sum_ok, f"rank {rank}: root's in-place reduced sum differs from the oracle"
         assert fl == 0
 
 
-def _worker_sharded(rank, world, init, n, chunks, offset, exchange, q):
+def _worker_sharded(rank, world, init, n, chunks, offset, exchange, kind, q):
     import torch
     import torch.distributed as dist
 
@@ -136,9 +145,7 @@ def _worker_sharded(rank, world, init, n, chunks, offset, exchange, q):
         xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(C)]
         dev = torch.device("cuda", 0)
         plan = plan_rank(names, world, rank)
-        from bench import HostStandinComm
-
-        pipe = PipelinedMaskedSum(HostStandinComm(rank, world), dev, n, chunks, exchange=exchange)
+        pipe = PipelinedMaskedSum(_comm(kind, rank, world), dev, n, chunks, exchange=exchange)
         gens = [plan_generators(plan, seed_of, offset=offset + lo) for lo, _ in pipe.bounds]
         part = torch.zeros(pipe.buffer_len, dtype=torch.int64, device=dev)
         dec = torch.zeros(pipe.buffer_len, dtype=torch.float64, device=dev)
@@ -157,9 +164,10 @@ def _worker_sharded(rank, world, init, n, chunks, offset, exchange, q):
         q.put((rank, repr(e), False))
 
 
+@pytest.mark.parametrize("kind", ["rccl", "standin"])
 @pytest.mark.parametrize("exchange", ["sharded", "direct"])
 @pytest.mark.parametrize("world,chunks", [(2, 3), (4, 2), (8, 8)])
-def test_ranks_sharded_server(world, chunks, exchange):
+def test_ranks_sharded_server(world, chunks, exchange, kind):
     """exchange="sharded" (reduce-scatter) or "direct" (shard transfers +
     a local sum_u64 through the staging buffer) with W real ranks: every
     rank's shard of the masked sum and its float64 decode equal the oracle's
@@ -167,7 +175,7 @@ def test_ranks_sharded_server(world, chunks, exchange):
     decoded sum."""
     if torch.cuda.device_count() == 0:  # asked without initialising HIP here (conftest: this module runs early)
         pytest.skip("no GPU")
-    res = _run_ranks(_worker_sharded, world, (70_001, chunks, 3 * 10**9 + 1, exchange))
+    res = _run_ranks(_worker_sharded, world, (70_001, chunks, 3 * 10**9 + 1, exchange, kind))
     for rank, shard_ok, full_ok in res:
         assert shard_ok is True, (rank, shard_ok)
         assert full_ok, f"rank {rank}: gathered decode differs from the oracle"
