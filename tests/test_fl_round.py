@@ -173,3 +173,27 @@ def test_fl_round_with_gaussian_dp_hip_vs_oracle_aggregator():
     for a, b in zip(ref_rounds, hip_rounds):
         for x, y in zip(a, b):
             assert np.array_equal(x, y)
+
+
+@pytest.mark.gpu
+def test_fl_round_through_the_per_party_drop_in_bit_exact_vs_oracle():
+    """BASELINE config 4 with the secretflow-facing drop-in
+    (sfl_amd.compat.secretflow: every party masks on its own device through
+    party.mask_payload, only masked payloads reach the server) as the FLModel
+    aggregator: init average and every round equal the oracle's bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.compat import secretflow as hip
+    from sfl_amd.device import PYU
+
+    seeds = o.seeds_for(NAMES)
+    pair = {(a, b): seeds[a][b] for a in NAMES for b in NAMES if a != b}
+    pyus = [PYU(n, 0) for n in NAMES]
+    ref_rounds, hip_rounds = [], []
+    _fl(OracleAggregator(NAMES, seeds), pyus, epochs=2, hook=lambda r, p: ref_rounds.append(p))
+    agg = hip.SecureAggregator(PYU("server", 0), pyus, seeds=pair)
+    _fl(agg, pyus, epochs=2, hook=lambda r, p: hip_rounds.append(p))
+    assert len(ref_rounds) == len(hip_rounds) == 1 + 2 * 3
+    for r, (a, b) in enumerate(zip(ref_rounds, hip_rounds)):
+        for li, (x, y) in enumerate(zip(a, b)):
+            assert np.array_equal(x, y), (r, li)
