@@ -852,9 +852,15 @@ __global__ void __launch_bounds__(kBlockThreads, clients_waves(Pairs<L, K>::coun
         // the lane's two elements are Box-Muller pair (i & 2) / 2 of their
         // Philox block: only that pair is formed
         const Normal2 z = gauss2(ka->dp_key, ka->dp_block0 + (i >> 2), (int)((i >> 1) & 1));
+        if (ka->dp_inv != 0.0f) {  // uniform branch: a power-of-two num_updates multiplies
 #pragma unroll
-        for (int k = 0; k < kE; k++)
-          xv[0].v[k] = dp_apply(xv[0].v[k], dp_s, z.z[k], ka->dp_sigma, ka->dp_updates, ka->dp_inv);
+          for (int k = 0; k < kE; k++)
+            xv[0].v[k] = dp_apply_t<true>(xv[0].v[k], dp_s, z.z[k], ka->dp_sigma, ka->dp_updates, ka->dp_inv);
+        } else {
+#pragma unroll
+          for (int k = 0; k < kE; k++)
+            xv[0].v[k] = dp_apply_t<false>(xv[0].v[k], dp_s, z.z[k], ka->dp_sigma, ka->dp_updates, ka->dp_inv);
+        }
       }
     }
     const QScale qs{ka->scale_f, ka->scale_d, ka->fxp_bits};

@@ -90,26 +90,66 @@ struct DpArgs {
   uint64_t key, block0;
 };
 
-// x' = x * scale + N(0, sigma^2) / updates, 4 elements (one Philox block) per lane
-__global__ void __launch_bounds__(256) k_dp_perturb(const DpArgs a) {
+// x' = x * scale + N(0, sigma^2) / updates, 4 elements (one Philox block)
+// per lane and block; kDpUnroll blocks per lane and trip, their 16-byte
+// loads issued before the noise is formed (one block per lane and trip kept
+// only ~8 MB of reads in flight chip-wide: 0.55 of HBM).
+#ifndef SA_DP_UNROLL
+#define SA_DP_UNROLL 2
+#endif
+constexpr int kDpUnroll = SA_DP_UNROLL;
+
+template <bool kPow2>
+__device__ __forceinline__ f32x4 dp_apply4(f32x4 v, float scale, const Normal4& z, const DpArgs& a) {
+  f32x4 o;
+  o.x = dp_apply_t<kPow2>(v.x, scale, z.z[0], a.sigma, a.updates, a.inv);
+  o.y = dp_apply_t<kPow2>(v.y, scale, z.z[1], a.sigma, a.updates, a.inv);
+  o.z = dp_apply_t<kPow2>(v.z, scale, z.z[2], a.sigma, a.updates, a.inv);
+  o.w = dp_apply_t<kPow2>(v.w, scale, z.z[3], a.sigma, a.updates, a.inv);
+  return o;
+}
+
+template <bool kPow2>
+__device__ __forceinline__ void dp_perturb_body(const DpArgs& a) {
   const float scale = dp_scale(a.sumsq, a.sumsq_layer, a.clip);
   const uint64_t nb = (a.n + 3) / 4;
+  const uint64_t full = a.n / 4;  // blocks with 4 elements
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += stride) {
-    const Normal4 z = gauss4(a.key, a.block0 + b);
-    const uint64_t e = b * 4;
-    if (e + 4 <= a.n) {
-      const float4 v = reinterpret_cast<const float4*>(a.x)[b];
-      float4 o;
-      o.x = dp_apply(v.x, scale, z.z[0], a.sigma, a.updates, a.inv);
-      o.y = dp_apply(v.y, scale, z.z[1], a.sigma, a.updates, a.inv);
-      o.z = dp_apply(v.z, scale, z.z[2], a.sigma, a.updates, a.inv);
-      o.w = dp_apply(v.w, scale, z.z[3], a.sigma, a.updates, a.inv);
-      reinterpret_cast<float4*>(a.out)[b] = o;
-    } else {
-      for (int k = 0; e + k < a.n; k++) a.out[e + k] = dp_apply(a.x[e + k], scale, z.z[k], a.sigma, a.updates, a.inv);
+  const f32x4* x4 = reinterpret_cast<const f32x4*>(a.x);
+  f32x4* o4 = reinterpret_cast<f32x4*>(a.out);
+  uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; b + (kDpUnroll - 1) * stride < full; b += kDpUnroll * stride) {
+    f32x4 v[kDpUnroll];
+#pragma unroll
+    for (int u = 0; u < kDpUnroll; u++) v[u] = __builtin_nontemporal_load(x4 + b + u * stride);
+    // keep every load ahead of the noise (the scheduler otherwise sinks the
+    // second load below the first block's Philox rounds)
+#ifndef SA_DP_NO_SCHED_BARRIER
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+    for (int u = 0; u < kDpUnroll; u++) {
+      const Normal4 z = gauss4(a.key, a.block0 + b + u * stride);
+      __builtin_nontemporal_store(dp_apply4<kPow2>(v[u], scale, z, a), o4 + b + u * stride);
     }
   }
+  for (; b < nb; b += stride) {
+    const Normal4 z = gauss4(a.key, a.block0 + b);
+    if (b < full) {
+      o4[b] = dp_apply4<kPow2>(x4[b], scale, z, a);
+    } else {
+      const uint64_t e = b * 4;
+      for (int k = 0; e + k < a.n; k++)
+        a.out[e + k] = dp_apply_t<kPow2>(a.x[e + k], scale, z.z[k], a.sigma, a.updates, a.inv);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_dp_perturb(const DpArgs a) {
+  if (a.inv != 0.0f)  // uniform: num_updates a power of two, multiply by its exact reciprocal
+    dp_perturb_body<true>(a);
+  else
+    dp_perturb_body<false>(a);
 }
 
 }  // namespace sa

@@ -22,12 +22,23 @@ struct Normal4 {
 #define SA_PHX_HD
 #endif
 
+// the round's three-way XORs: one v_bitop3_b32 each on the device (0x96 =
+// a ^ b ^ c), where the compiler emits two v_xor_b32
+SA_PHX_HD inline uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 SA_PHX_HD inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
   for (int r = 0; r < 10; r++) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c[1], k0);
+    const uint32_t n2 = xor3((uint32_t)(p0 >> 32), c[3], k1);
     c[0] = n0;
     c[1] = (uint32_t)p1;
     c[2] = n2;
@@ -42,16 +53,24 @@ struct Normal2 {
   float z[2];
 };
 
-// Box-Muller of one pair of Philox words -> 2 standard normals.
+// Box-Muller of one pair of Philox words -> 2 standard normals, on the
+// hardware transcendental units (8 issue cycles each, MI355X_MICROARCH.md):
+// v_log_f32 (log2), v_sqrt_f32, and v_sin_f32 / v_cos_f32, which take their
+// argument in revolutions -- sin(2*pi*u2) is v_sin_f32(u2) with no range
+// reduction.  The libm forms (logf, sqrtf, sincospif) cost ~60 VALU per pair
+// and made the noise VALU-bound (k_dp_perturb 0.55 of HBM); the noise is
+// this build's own keyed stream (the reference draws unseeded
+// np.random.normal), so its parity is distributional and the oracle's numpy
+// restatement in the tests is matched within the tolerance
+// tests/test_gpu_dp.py states.  u1 >= 2^-24 is a normal float, so v_log_f32
+// needs no denormal path.
 __device__ __forceinline__ Normal2 box_muller(uint32_t w0, uint32_t w1) {
   const float u1 = (float)((w0 >> 8) + 1u) * 0x1p-24f;  // (0, 1]
   const float u2 = (float)(w1 >> 8) * 0x1p-24f;         // [0, 1)
-  const float rad = sqrtf(-2.0f * logf(u1));
-  float s, co;
-  sincospif(2.0f * u2, &s, &co);
+  const float rad = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln 2 log2(u1)
   Normal2 o;
-  o.z[0] = rad * co;
-  o.z[1] = rad * s;
+  o.z[0] = rad * __builtin_amdgcn_cosf(u2);
+  o.z[1] = rad * __builtin_amdgcn_sinf(u2);
   return o;
 }
 
@@ -62,24 +81,26 @@ __device__ __forceinline__ void philox_block(uint64_t key, uint64_t blk, uint32_
   philox4x32_10(c, (uint32_t)key, (uint32_t)(key >> 32));
 }
 
-// The two entry points below are never inlined.  Inlined, the libm code in
-// Box-Muller (logf, sincospif) is contracted together with the caller's
-// arithmetic (rad * co with the noise scaling), and the fused masking kernel
-// and the standalone perturb kernel then differed in the last bit of some
-// normals; returned from a call, every normal is rounded the same way.  Out
-// of line also keeps the Philox rounds' registers out of the masking kernel
-// (sa_mask_dp).  tests/test_gpu_dp.py checks the two paths bit for bit.
+// The two entry points below are inlined (round 5): with the libm forms of
+// Box-Muller they had to stay out of line (the library code was contracted
+// with the caller's arithmetic and the fused and standalone kernels then
+// differed in the last bit of some normals); the hardware forms are single
+// instructions and the build has -ffp-contract=off, so every normal is
+// rounded the same way in both kernels -- tests/test_gpu_dp.py checks the
+// two paths bit for bit.  Inlined, the key schedule stays on the SALU (the
+// key is uniform) and the 10 unrolled rounds cost 2 v_mad_u64_u32 + 2
+// three-way XORs each, where the call's rolled loop took ~9 VALU per round.
 
 // Box-Muller pair j (normals 2j, 2j+1) of counter block `blk` under `key`:
 // the fused masking kernel needs one pair per lane.
-__device__ __noinline__ Normal2 gauss2(uint64_t key, uint64_t blk, int j) {
+__device__ __forceinline__ Normal2 gauss2(uint64_t key, uint64_t blk, int j) {
   uint32_t c[4];
   philox_block(key, blk, c);
   return j ? box_muller(c[2], c[3]) : box_muller(c[0], c[1]);
 }
 
 // All 4 standard normals of counter block `blk` (one Philox block).
-__device__ __noinline__ Normal4 gauss4(uint64_t key, uint64_t blk) {
+__device__ __forceinline__ Normal4 gauss4(uint64_t key, uint64_t blk) {
   uint32_t c[4];
   philox_block(key, blk, c);
   const Normal2 a = box_muller(c[0], c[1]), b = box_muller(c[2], c[3]);
@@ -104,9 +125,17 @@ __host__ __device__ inline float exact_recip_pow2(float u) {
 // x' = x * scale + (z * sigma) / num_updates, float32 in the reference's
 // operation order (mechanism_fl.py:112-127: clip, astype(float32) noise,
 // noise / num_updates, np.add); inv = exact_recip_pow2(updates) or 0.
-__device__ __forceinline__ float dp_apply(float x, float scale, float z, float sigma, float updates, float inv) {
+template <bool kPow2>
+__device__ __forceinline__ float dp_apply_t(float x, float scale, float z, float sigma, float updates, float inv) {
   const float zs = __fmul_rn(z, sigma);
-  return __fadd_rn(__fmul_rn(x, scale), inv != 0.0f ? __fmul_rn(zs, inv) : __fdiv_rn(zs, updates));
+  return __fadd_rn(__fmul_rn(x, scale), kPow2 ? __fmul_rn(zs, inv) : __fdiv_rn(zs, updates));
+}
+
+// callers hoist the (kernel-uniform) choice out of their loops: an inline
+// select computed the IEEE division for every element even when inv != 0
+__device__ __forceinline__ float dp_apply(float x, float scale, float z, float sigma, float updates, float inv) {
+  return inv != 0.0f ? dp_apply_t<true>(x, scale, z, sigma, updates, inv)
+                     : dp_apply_t<false>(x, scale, z, sigma, updates, inv);
 }
 
 // scale = min(1, clip / norm) (mechanism_fl.py:107); with a layer squared
