@@ -92,10 +92,13 @@ struct DpArgs {
 
 // x' = x * scale + N(0, sigma^2) / updates, 4 elements (one Philox block)
 // per lane and block; kDpUnroll blocks per lane and trip, their 16-byte
-// loads issued before the noise is formed (one block per lane and trip kept
-// only ~8 MB of reads in flight chip-wide: 0.55 of HBM).
+// loads issued before the noise is formed.  With the libm Box-Muller, 2
+// blocks in flight won (0.154 vs 0.164 ms at 100M); with the hardware
+// transcendentals and bitop3 Philox, 1 block does (0.173-0.177 vs 0.186 for
+// 2 and 0.197-0.200 for 4 on one box, tools/r05_dpu.sh,
+// profiles/r05/dp_unroll_ab.txt).
 #ifndef SA_DP_UNROLL
-#define SA_DP_UNROLL 2
+#define SA_DP_UNROLL 1
 #endif
 constexpr int kDpUnroll = SA_DP_UNROLL;
 
