@@ -437,3 +437,25 @@ def _payload_fuzz(c, seed, rounds):
             assert isinstance(got, list if container == "list" else tuple) and len(got) == n_layers
             assert [np.shape(g) for g in got] == shapes
         offset += sum(int(np.prod(sh)) for sh in shapes)
+
+
+def test_server_that_is_also_a_participant():
+    """The notebook's own constructor, SecureAggregator(device=alice,
+    participants=[alice, bob]) (secure_aggregation.ipynb:257-258): alice
+    masks as a participant AND sums as the server; bob's values stay private."""
+    from sfl_amd.compat import secretflow as hip
+
+    c = fs.Cluster(NAMES, private=["bob"], init=_oracle_backend_init)
+    try:
+        seeds, pair = _seeds()
+        alice, bob = c.pyu("alice"), c.pyu("bob")
+        agg = hip.SecureAggregator(alice, [alice, bob], reveal=fs.reveal, seeds=pair)
+        case = CONTRACT["sum_single"]
+        xa, xb = _case_inputs(case)
+        out = agg.sum([_put(alice, xa), _put(bob, xb)], axis=0)
+        assert out.device == alice
+        exp, _, _ = o.secure_sum([_cat(xa), _cat(xb)], NAMES, seeds=seeds)
+        assert np.array_equal(fs.reveal(out).reshape(-1), exp)
+        assert [p for p, _ in c.reveals if p == "bob"] == ["bob"]  # bob: his public key only
+    finally:
+        c.close()
