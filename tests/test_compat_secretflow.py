@@ -459,3 +459,37 @@ def test_server_that_is_also_a_participant():
         assert [p for p, _ in c.reveals if p == "bob"] == ["bob"]  # bob: his public key only
     finally:
         c.close()
+
+
+def _notebook_kat(alice, bob, reveal):
+    from sfl_amd.compat import secretflow as hip
+
+    k = json.load(open(os.path.join(HERE, "golden", "notebook_kat.json")))
+    agg = hip.SecureAggregator(device=alice, participants=[alice, bob], reveal=reveal)  # DH seeds
+    a, b = _put(alice, np.array(k["arr0"])), _put(bob, np.array(k["arr1"]))
+    s = reveal(agg.sum([a, b], axis=0))
+    avg = reveal(agg.average([a, b], axis=0))
+    assert s.dtype == np.float64
+    assert np.abs(s - np.array(k["secure_sum"])).max() < 1e-8
+    assert np.abs(avg - np.array(k["secure_average"])).max() < 1e-8
+
+
+def test_notebook_kat_through_the_drop_in():
+    """docs/developer/algorithm/secure_aggregation.ipynb cells 16-18 through
+    the drop-in, parties as spawned processes (alice the server too)."""
+    c = fs.Cluster(NAMES, private=["bob"], init=_oracle_backend_init)
+    try:
+        _notebook_kat(c.pyu("alice"), c.pyu("bob"), fs.reveal)
+    finally:
+        c.close()
+
+
+@pytest.mark.gpu
+def test_gpu_notebook_kat_through_the_drop_in_in_process():
+    """The same with sfl_amd's in-process devices (the drop-in accepts any
+    secretflow-shaped PYU) and the HIP steps."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.device import PYU, reveal
+
+    _notebook_kat(PYU("alice", 0), PYU("bob", 0), reveal)
