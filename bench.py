@@ -57,7 +57,7 @@ from benchkit.roofline import (HBM_PEAK_GBPS, PCG_ONE_DRAWS_8WAVE, PCG_PAIR_DRAW
                                PMC_DIRS, PMC_ELEMS, VALU_PEAK_WAVE_INSTR_PER_S, committed_kernel_ms,
                                draw_loop_ceilings, exchange_model, kernel_key, pmc_traffic, pmc_valu,
                                traffic_field)
-from benchkit.standin import HostStandinComm, one_gpu_rccl_comm  # noqa: E402,F401
+from benchkit.standin import HostStandinComm, one_gpu_rccl_comm, one_gpu_rccl_env  # noqa: E402,F401
 
 
 # k_clients' variant flags (sfl_amd/csrc/sa_internal.h): the instantiation a
@@ -529,7 +529,7 @@ def run_design(ctx, v: Variant, steps: int, warmup: int, keep: bool = False) -> 
     xchg_ms = sum(a.elapsed_time(b) for a, b in xev) / steps  # exchange time per step (comm stream)
     if multi:
         t = torch.tensor([elapsed, kern_ms, xchg_ms], dtype=torch.float64,
-                         device="cpu" if ctx.get("rehearse") else dev)
+                         device="cpu" if ctx.get("pg_gloo") else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms, xchg_ms = float(t[0]), float(t[1]), float(t[2])
     try:  # the check is extra: a failure here must not cost the design's timing
@@ -703,16 +703,23 @@ def rank_main(args):
     dev = torch.device("cuda", gpu)
     _lib.check(_lib.lib().sa_set_masking_reserve(args.masking_reserve), "sa_set_masking_reserve")
     comm = None
-    if multi and rehearse:
+    if multi and rehearse and args.rehearse_comm == "standin":
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        comm = HostStandinComm(rank, world) if args.rehearse_comm == "standin" else one_gpu_rccl_comm(rank, world)
+        comm = HostStandinComm(rank, world)
+    elif multi and rehearse:
+        # the product's process group and communicator, every rank its own
+        # RCCL node on this one GPU (NCCL_HOSTID): torch's NCCL group
+        # carries the barriers and the timing reductions, as on the node
+        os.environ.update(one_gpu_rccl_env(rank))
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        comm = one_gpu_rccl_comm(rank, world)
     elif multi:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         comm = RcclComm(rank, world, local_rank)
 
     C, N = args.clients, args.elems
     ctx = {"args": args, "world": world, "rank": rank, "dev": dev, "comm": comm, "rehearse": rehearse,
-           "names": [f"client{c}" for c in range(C)]}
+           "pg_gloo": multi and dist.get_backend() == "gloo", "names": [f"client{c}" for c in range(C)]}
     head = headline_variant(args, multi)
     wd.enter("headline")
     r = run_design(ctx, head, args.steps, args.warmup, keep=args.extra and world == 1)
@@ -784,8 +791,8 @@ def rank_main(args):
     }
     if rehearse:
         out["rehearsal"] = ("--rehearse-one-gpu: every rank on cuda:0; " + (
-            "the product's RcclComm with a distinct NCCL_HOSTID per rank, so RCCL runs its collectives between the "
-            "ranks over its socket transport on lo (benchkit/standin.py one_gpu_rccl_comm)"
+            "the product's NCCL process group and RcclComm with a distinct NCCL_HOSTID per rank, so RCCL runs its "
+            "collectives between the ranks over its socket transport on lo (benchkit/standin.py one_gpu_rccl_comm)"
             if args.rehearse_comm == "rccl" else
             "collectives and their barriers through a shared host mapping (benchkit/standin.py)")
             + "; the N > 1 control flow, not the product's rate")
