@@ -493,3 +493,42 @@ def test_gpu_notebook_kat_through_the_drop_in_in_process():
     from sfl_amd.device import PYU, reveal
 
     _notebook_kat(PYU("alice", 0), PYU("bob", 0), reveal)
+
+
+def _rejection_rounds(c):
+    """The (alice, bob) pair stream draws a raw 0 at element 1000 of round 0
+    (numpy's Generator.integers rejects it and takes the next draw): every
+    masked vector the server receives and every result, over two rounds,
+    equal numpy's own generators (OracleMaskers) -- the party resolves the
+    rejection before its vector leaves, and its stream position moves one
+    raw draw further."""
+    from sfl_amd.compat import secretflow as hip
+    from test_gpu_rejection import forced_zero_state
+
+    state = {("alice", "bob"): forced_zero_state(1000)}
+    agg = hip.SecureAggregator(c.pyu("carol"), [c.pyu(n) for n in NAMES], reveal=fs.reveal, seeds=state)
+    ora = o.OracleMaskers(NAMES, state)
+    rng = np.random.default_rng(12)
+    n = 3001
+    for rnd in range(2):
+        xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in NAMES]
+        out = agg.sum([_put(c.pyu(nm), x) for nm, x in zip(NAMES, xs)], axis=0)
+        masked, ssum = ora.round(xs)
+        assert np.array_equal(fs.reveal(out), o.decode(ssum)), rnd
+        for r, m in zip([fs.reveal(m) for m in agg.last_masked], masked):
+            assert np.array_equal(r.u64, m), rnd
+        if rnd == 0:  # the round really held a rejection: numpy's stream differs from the plain raw + offset one
+            plain = o.quantize(xs[0]) + (np.array(o.pcg64_raw_py(*state[("alice", "bob")], n), dtype=np.uint64)
+                                         + np.uint64(o.MASK_OFFSET))
+            assert not np.array_equal(masked[0], plain)
+        # positions: round 1 starts one raw draw further for the pair
+        assert [fs.reveal(m).positions for m in agg.last_masked] == [{"bob": rnd * (n + 1)}, {"alice": rnd * (n + 1)}]
+
+
+def test_rejection_resolved_inside_the_party(cpu_cluster):
+    _rejection_rounds(cpu_cluster)
+
+
+@pytest.mark.gpu
+def test_gpu_rejection_resolved_inside_the_party(gpu_cluster):
+    _rejection_rounds(gpu_cluster)
