@@ -28,6 +28,7 @@ spawned process per party.
 
 from __future__ import annotations
 
+import copy
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -70,7 +71,9 @@ def public_key(masker: Masker) -> int:
 
 def agree(masker: Masker, peer_keys: dict, seeds: dict | None = None) -> Masker:
     """Runs on the participant: pairwise seeds from the revealed public keys
-    (``seeds``: explicit ``{peer: seed | (state, inc)}`` for tests)."""
+    (``seeds``: explicit ``{peer: seed | (state, inc)}`` for tests).  Returns
+    the agreed masker (a new object, like ``mask_payload``)."""
+    masker = copy.deepcopy(masker)
     if seeds is None:
         masker.agree({str(k): int(v) for k, v in peer_keys.items()})
     else:
@@ -111,10 +114,14 @@ def mask_payload(masker: Masker, payload, weight=None, gpu: int | None = 0):
     """Runs on the participant: quantize ``payload * weight`` and add the
     pairwise masks (``sa_mask`` on this party's GPU ``gpu``).
 
-    Returns ``(MaskedPayload, masker)``, the masker advanced past this round's
-    draws (numpy's rejections included)."""
+    Returns ``(MaskedPayload, masker)``, a NEW masker advanced past this
+    round's draws (numpy's rejections included); the one passed in is left
+    as it was -- an object store hands the function a copy anyway, and an
+    in-process device must not see a round that failed part-way advance
+    some parties' streams."""
     from .secure_aggregator import _compute_dtype, _np_dtype, _shape
 
+    masker = copy.deepcopy(masker)
     layers, container = _layers(payload)
     weight = _host_weight(weight)
     shapes = [_shape(a) for a in layers]

@@ -532,3 +532,18 @@ def test_rejection_resolved_inside_the_party(cpu_cluster):
 @pytest.mark.gpu
 def test_gpu_rejection_resolved_inside_the_party(gpu_cluster):
     _rejection_rounds(gpu_cluster)
+
+
+def test_party_functions_leave_their_masker_argument_alone(monkeypatch):
+    """mask_payload / agree return a NEW masker: with in-process devices a
+    round that fails part-way must not have advanced the streams the
+    aggregator still holds (an object store passes copies anyway)."""
+    import party_oracle_backend
+    from sfl_amd.security.aggregation import party as P
+
+    monkeypatch.setattr(P, "_mask_vector", party_oracle_backend._mask_vector)
+    m = P.new_masker("alice")
+    m2 = P.agree(m, {"alice": m.public_key, "bob": P.new_masker("bob").public_key})
+    assert m.peers == [] and m2.peers == ["bob"]
+    wire, m3 = P.mask_payload(m2, np.ones(10, np.float32), None, None)
+    assert m2.position("bob") == 0 and m3.position("bob") == 10 and wire.positions == {"bob": 0}
