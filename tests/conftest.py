@@ -21,7 +21,7 @@ def golden_dir():
 # process must not hold a GPU context of its own yet (W + 1 processes at
 # W = 8 is the suspected cause of rehearsals running ~10x slower, DESIGN.md
 # §5); these modules never initialise HIP in the test process themselves.
-_FIRST = ("test_gpu_bench_rehearsal.py", "test_gpu_dist_pipeline.py")
+_FIRST = ("test_gpu_bench_rehearsal.py", "test_gpu_dist_pipeline.py", "test_gpu_rccl_multirank.py")
 
 
 def pytest_collection_modifyitems(session, config, items):
