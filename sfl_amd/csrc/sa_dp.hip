@@ -96,7 +96,10 @@ struct DpArgs {
 // blocks in flight won (0.154 vs 0.164 ms at 100M); with the hardware
 // transcendentals and bitop3 Philox, 1 block does (0.173-0.177 vs 0.186 for
 // 2 and 0.197-0.200 for 4 on one box, tools/r05_dpu.sh,
-// profiles/r05/dp_unroll_ab.txt).
+// profiles/r05/dp_unroll_ab.txt).  Non-temporal accesses beat plain ones
+// (0.165-0.170 vs 0.176-0.178 ms) and a grid of 2x or 4x the occupancy did
+// not help (profiles/r05/dp_forms_ab.txt; SA_DP_PLAIN_MEM, SA_DP_GRID_MULT
+// select those forms for such A/Bs).
 #ifndef SA_DP_UNROLL
 #define SA_DP_UNROLL 1
 #endif
@@ -124,7 +127,13 @@ __device__ __forceinline__ void dp_perturb_body(const DpArgs& a) {
   for (; b + (kDpUnroll - 1) * stride < full; b += kDpUnroll * stride) {
     f32x4 v[kDpUnroll];
 #pragma unroll
-    for (int u = 0; u < kDpUnroll; u++) v[u] = __builtin_nontemporal_load(x4 + b + u * stride);
+    for (int u = 0; u < kDpUnroll; u++) {
+#ifdef SA_DP_PLAIN_MEM
+      v[u] = x4[b + u * stride];
+#else
+      v[u] = __builtin_nontemporal_load(x4 + b + u * stride);
+#endif
+    }
     // keep every load ahead of the noise (the scheduler otherwise sinks the
     // second load below the first block's Philox rounds)
 #ifndef SA_DP_NO_SCHED_BARRIER
@@ -133,7 +142,11 @@ __device__ __forceinline__ void dp_perturb_body(const DpArgs& a) {
 #pragma unroll
     for (int u = 0; u < kDpUnroll; u++) {
       const Normal4 z = gauss4(a.key, a.block0 + b + u * stride);
+#ifdef SA_DP_PLAIN_MEM
+      o4[b + u * stride] = dp_apply4<kPow2>(v[u], scale, z, a);
+#else
       __builtin_nontemporal_store(dp_apply4<kPow2>(v[u], scale, z, a), o4 + b + u * stride);
+#endif
     }
   }
   for (; b < nb; b += stride) {
@@ -195,7 +208,10 @@ extern "C" int sa_dp_perturb_f32(const float* x, uint64_t n, const sa_dp* dp, fl
   if (n == 0) return SA_OK;
   DpArgs a{x,  out, n, dp->sumsq, dp->sumsq_layer, dp->l2_norm_clip, dp->noise_std, dp->num_updates,
            exact_recip_pow2(dp->num_updates), dp->key, dp->counter0 / 4};
-  const int maxb = occupancy_blocks((const void*)&k_dp_perturb);
+#ifndef SA_DP_GRID_MULT
+#define SA_DP_GRID_MULT 1
+#endif
+  const int maxb = occupancy_blocks((const void*)&k_dp_perturb) * SA_DP_GRID_MULT;
   if (maxb <= 0) return SA_ERR_HIP;
   const uint64_t want = ((n + 3) / 4 + 255) / 256;
   const int grid = (int)(want < (uint64_t)maxb ? want : (uint64_t)maxb);
