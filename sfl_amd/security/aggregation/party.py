@@ -199,13 +199,15 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
         raise RuntimeError("the party has no GPU: libsfl_sa masks on the device")
     dev = torch.device("cuda", gpu)
     tdt = {_F32: torch.float32, _F64: torch.float64, _I64: torch.int64}
-    parts = []
-    for a in xs:
-        if isinstance(a, torch.Tensor):
-            parts.append(a.detach().reshape(-1).to(device=dev, dtype=tdt[xt]))
-        else:
-            parts.append(torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=xt).reshape(-1)).to(dev))
-    x = parts[0] if len(parts) == 1 else torch.cat(parts)
+    if not any(isinstance(a, torch.Tensor) for a in xs):
+        # host layers (FedAvgW's get_weights payloads): packed on the host, ONE H2D copy
+        flat = (np.ascontiguousarray(np.asarray(xs[0]), dtype=xt).reshape(-1) if len(xs) == 1 else
+                np.concatenate([np.asarray(a, dtype=xt).reshape(-1) for a in xs]))
+        x = torch.from_numpy(flat).to(dev)
+    else:
+        parts = [a.detach().reshape(-1).to(device=dev, dtype=tdt[xt]) if isinstance(a, torch.Tensor) else
+                 torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=xt).reshape(-1)).to(dev) for a in xs]
+        x = parts[0] if len(parts) == 1 else torch.cat(parts)
     x = x.contiguous()
     if x.data_ptr() % 16:
         x = x.clone()
