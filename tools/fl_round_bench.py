@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """BASELINE config 4: a horizontal-FL round (fed_avg_w, reference MlpNet
 4-50-50-3, 8 clients, synthetic data) with the secure aggregator swapped to
-the HIP path end-to-end, against the same loop on the numpy oracle
-aggregator.  Reports per-round and per-aggregation wall time.
+the HIP path end-to-end -- the in-process simulation (one fused launch) and
+the per-party drop-in (sfl_amd.compat.secretflow) -- against the same loop
+on the numpy oracle aggregator.  Reports per-round and per-aggregation wall
+time.
 
 usage: python tools/fl_round_bench.py [--epochs 2] [--train-device cuda|cpu] [--hidden 50]
 """
@@ -47,7 +49,12 @@ def main():
                    train_device=args.train_device)
     warm.fit({p: x for p, x in zip(pyus, xs)}, {p: y for p, y in zip(pyus, ys)}, batch_size=32, epochs=1,
              aggregate_freq=1, validation_data=(np.concatenate(xs), np.concatenate(ys)))  # first evaluate too
+    from sfl_amd.compat import secretflow as hip_compat
+
     for label, agg in (("hip", SecureAggregator(PYU("server", 0), pyus, seeds=pair)),
+                       # the secretflow-facing drop-in: every party masks by itself (sa_mask on its
+                       # device, masked payload to the server, sa_sum_u64 + sa_decode there)
+                       ("hip_per_party_drop_in", hip_compat.SecureAggregator(PYU("server", 0), pyus, seeds=pair)),
                        ("oracle_numpy", T.OracleAggregator(names, seeds))):
         model = TorchModel(model_fn=T.MlpNet, loss_fn=torch.nn.CrossEntropyLoss,
                            optim_fn=optim_wrapper(torch.optim.Adam, lr=5e-3))
