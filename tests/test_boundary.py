@@ -204,3 +204,44 @@ def test_integration_table_cites_the_header_lines():
     text = " ".join(r.split("|")[1] for r in table)
     missing = [d for d in declared if d not in text and "_" + d.split("_", 2)[-1] not in text]
     assert not missing, f"entry points missing from INTEGRATION.md's table: {missing}"
+
+
+def test_ctypes_structs_match_the_header_layout(tmp_path):
+    """The ctypes mirrors in sfl_amd/_lib.py have the C layout of
+    include/sfl_sa.h (sizes and every field offset), compiled with gcc:
+    ABI 3 changed sa_dp (a double clip), so a stale mirror would pass the
+    wrong bytes silently."""
+    import ctypes as C
+    import shutil
+    import subprocess
+
+    from sfl_amd import _lib as L
+
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    structs = {"sa_dp": (L.DP, ["sumsq", "sumsq_layer", "l2_norm_clip", "noise_std", "num_updates", "key",
+                                "counter0"]),
+               "sa_pcg64": (L.PCG64, ["state", "inc"]),
+               "sa_mask_stream": (L.MaskStream, ["gen", "sign", "peer"]),
+               "sa_local_client": (L.LocalClient, ["x", "weight", "masked_out"])}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{os.path.join(ROOT, "include", "sfl_sa.h")}"',
+             "int main(void) {"]
+    for name, (_, fields) in structs.items():
+        lines.append(f'  printf("{name} size %zu\\n", sizeof({name}));')
+        for f in fields:
+            lines.append(f'  printf("{name} {f} %zu\\n", offsetof({name}, {f}));')
+    lines.append("  return 0;\n}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    r = subprocess.run(["gcc", "-std=c11", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", str(src), "-o", str(exe)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    got = {}
+    for ln in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        a, b, c = ln.split()
+        got[(a, b)] = int(c)
+    for name, (cls, fields) in structs.items():
+        assert got[(name, "size")] == C.sizeof(cls), name
+        for f in fields:
+            assert got[(name, f)] == getattr(cls, f).offset, (name, f)
