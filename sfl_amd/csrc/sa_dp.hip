@@ -161,11 +161,62 @@ __device__ __forceinline__ void dp_perturb_body(const DpArgs& a) {
   }
 }
 
+// Tile form (SA_DP_TILE = T > 0): one launch-wide pass, no grid stride; a
+// workgroup owns T * 256 consecutive Philox blocks, lane t blocks t, t + 256,
+// ...  The grid is ceil(blocks / (256 T)), so every workgroup streams once
+// and retires (the streaming shape that reached 0.77 of HBM for a copy,
+// profiles/r05/stream_rate.jsonl "tile").
+#ifndef SA_DP_TILE
+#define SA_DP_TILE 0
+#endif
+constexpr int kDpTile = SA_DP_TILE;
+
+template <bool kPow2, int T>
+__device__ __forceinline__ void dp_perturb_tile(const DpArgs& a) {
+  const float scale = dp_scale(a.sumsq, a.sumsq_layer, a.clip);
+  const uint64_t nb = (a.n + 3) / 4;
+  const uint64_t full = a.n / 4;
+  const f32x4* x4 = reinterpret_cast<const f32x4*>(a.x);
+  f32x4* o4 = reinterpret_cast<f32x4*>(a.out);
+  const uint64_t b0 = (uint64_t)blockIdx.x * (256 * T) + threadIdx.x;
+  if (b0 + (uint64_t)(T - 1) * 256 < full) {
+    f32x4 v[T];
+#pragma unroll
+    for (int u = 0; u < T; u++) v[u] = __builtin_nontemporal_load(x4 + b0 + u * 256);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < T; u++) {
+      const Normal4 z = gauss4(a.key, a.block0 + b0 + u * 256);
+      __builtin_nontemporal_store(dp_apply4<kPow2>(v[u], scale, z, a), o4 + b0 + u * 256);
+    }
+    return;
+  }
+  for (int u = 0; u < T; u++) {
+    const uint64_t b = b0 + (uint64_t)u * 256;
+    if (b >= nb) break;
+    const Normal4 z = gauss4(a.key, a.block0 + b);
+    if (b < full) {
+      o4[b] = dp_apply4<kPow2>(x4[b], scale, z, a);
+    } else {
+      const uint64_t e = b * 4;
+      for (int k = 0; e + k < a.n; k++)
+        a.out[e + k] = dp_apply_t<kPow2>(a.x[e + k], scale, z.z[k], a.sigma, a.updates, a.inv);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) k_dp_perturb(const DpArgs a) {
-  if (a.inv != 0.0f)  // uniform: num_updates a power of two, multiply by its exact reciprocal
-    dp_perturb_body<true>(a);
-  else
-    dp_perturb_body<false>(a);
+  if constexpr (kDpTile > 0) {
+    if (a.inv != 0.0f)
+      dp_perturb_tile<true, kDpTile>(a);
+    else
+      dp_perturb_tile<false, kDpTile>(a);
+  } else {
+    if (a.inv != 0.0f)  // uniform: num_updates a power of two, multiply by its exact reciprocal
+      dp_perturb_body<true>(a);
+    else
+      dp_perturb_body<false>(a);
+  }
 }
 
 }  // namespace sa
@@ -211,10 +262,20 @@ extern "C" int sa_dp_perturb_f32(const float* x, uint64_t n, const sa_dp* dp, fl
 #ifndef SA_DP_GRID_MULT
 #define SA_DP_GRID_MULT 1
 #endif
-  const int maxb = occupancy_blocks((const void*)&k_dp_perturb) * SA_DP_GRID_MULT;
-  if (maxb <= 0) return SA_ERR_HIP;
-  const uint64_t want = ((n + 3) / 4 + 255) / 256;
-  const int grid = (int)(want < (uint64_t)maxb ? want : (uint64_t)maxb);
+  int grid;
+  if (kDpTile > 0) {
+    const uint64_t want = ((n + 3) / 4 + 256 * kDpTile - 1) / (256 * kDpTile);
+    if (want > 0x7fffffffull) {
+      sa_set_error("sa_dp_perturb_f32: n too large for the tile grid");
+      return SA_ERR_ARG;
+    }
+    grid = (int)want;
+  } else {
+    const int maxb = occupancy_blocks((const void*)&k_dp_perturb) * SA_DP_GRID_MULT;
+    if (maxb <= 0) return SA_ERR_HIP;
+    const uint64_t want = ((n + 3) / 4 + 255) / 256;
+    grid = (int)(want < (uint64_t)maxb ? want : (uint64_t)maxb);
+  }
   hipLaunchKernelGGL(k_dp_perturb, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
   SA_HIP_CHECK(hipGetLastError());
   return SA_OK;
