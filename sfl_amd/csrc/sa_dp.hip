@@ -90,6 +90,7 @@ struct DpArgs {
   uint64_t key, block0;
 };
 
+// Grid-stride form (SA_DP_TILE = 0; the tile form below replaced it):
 // x' = x * scale + N(0, sigma^2) / updates, 4 elements (one Philox block)
 // per lane and block; kDpUnroll blocks per lane and trip, their 16-byte
 // loads issued before the noise is formed.  With the libm Box-Muller, 2
@@ -161,13 +162,16 @@ __device__ __forceinline__ void dp_perturb_body(const DpArgs& a) {
   }
 }
 
-// Tile form (SA_DP_TILE = T > 0): one launch-wide pass, no grid stride; a
-// workgroup owns T * 256 consecutive Philox blocks, lane t blocks t, t + 256,
-// ...  The grid is ceil(blocks / (256 T)), so every workgroup streams once
-// and retires (the streaming shape that reached 0.77 of HBM for a copy,
-// profiles/r05/stream_rate.jsonl "tile").
+// Tile form (SA_DP_TILE = T > 0, the product's with T = 1): no grid stride;
+// a workgroup owns T * 256 consecutive Philox blocks, lane t blocks t,
+// t + 256, ...  The grid is ceil(blocks / (256 T)), so every workgroup
+// streams once and retires (the streaming shape that reached 0.77 of HBM for
+// a copy, profiles/r05/stream_rate.jsonl "tile").  At 100M: 0.142-0.144 ms
+// (0.70 of HBM) for T = 1, 0.148 for 2, 0.157 for 4, against 0.171-0.174 ms
+// for the occupancy-sized grid-stride form (SA_DP_TILE = 0,
+// profiles/r05/dp_tile_ab.txt).
 #ifndef SA_DP_TILE
-#define SA_DP_TILE 0
+#define SA_DP_TILE 1
 #endif
 constexpr int kDpTile = SA_DP_TILE;
 
