@@ -67,6 +67,25 @@ def test_perturb_clip_exact_without_noise(clip):
     assert np.array_equal(y.cpu().numpy(), x.cpu().numpy() * scale)
 
 
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 1023, 1024, 1025, 4095, 4096, 4097, 262_147])
+def test_perturb_tile_edges_and_no_write_past_n(n):
+    """The tile form's whole-tile and partial-tile paths (1,024 elements per
+    workgroup) against the oracle's noise stream; the 16 floats after n keep
+    their sentinel."""
+    K = _K()
+    key, ctr = 0x0123456789ABCDEF, 4 * 7
+    x = torch.randn(n, device=DEV) * 0.2
+    s = _sumsq(x)
+    buf = torch.full((n + 16,), 12345.0, device=DEV)
+    dp = K.make_dp(s, l2_norm_clip=0.5, noise_std=0.3, num_updates=4, key=key, counter0=ctr)
+    K.dp_perturb(x, buf[:n], dp)
+    torch.cuda.synchronize()
+    assert torch.all(buf[n:] == 12345.0)
+    xh = x.cpu().numpy()
+    exp = D.perturb(xh, D.clip_scale(s.item(), 0.5), D.gauss(key, ctr, n), 0.3, 4)
+    assert np.allclose(buf[:n].cpu().numpy(), exp, rtol=2e-5, atol=2e-6)
+
+
 @pytest.mark.parametrize("updates", [4, 3])
 def test_perturb_noise_matches_oracle_stream(updates):
     K = _K()
