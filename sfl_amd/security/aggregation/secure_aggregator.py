@@ -40,6 +40,12 @@ _NP2T = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float6
          np.dtype(np.int64): torch.int64}
 _T2NP = {v: k for k, v in _NP2T.items()}
 MAX_FUSED_CLIENTS = 8
+# per-party bytes up to which a call is latency-bound (tools/config1_bench.py
+# at 9 .. 1M elements): host arrays packed into one pinned copy and host
+# results collected after one synchronisation; above it the driver's pageable
+# copies, which pipeline their staging, are faster than a host memcpy
+# into pinned memory
+SMALL_CALL_BYTES = 1 << 20
 
 
 class _Rejected(Exception):
@@ -220,7 +226,6 @@ class SecureAggregator(Aggregator):
 
         server = self._device
         sdev = server.torch_device
-        flags = torch.zeros(1, dtype=torch.int32, device=sdev)
         masked_keep, digests_keep = [], []
 
         # layers are masked in order with one stream position per (party, peer),
@@ -228,7 +233,8 @@ class SecureAggregator(Aggregator):
         sizes = [int(np.prod(sh)) if sh else 1 for sh in shapes]
         if self._host_fusable(data, layer_lists, as_torch, weights, sum(sizes)):
             return self._aggregate_host_fused(data, layer_lists, sizes, shapes, weights, average, is_list,
-                                              payloads, flags, digests_keep)
+                                              payloads, digests_keep)
+        flags = torch.zeros(1, dtype=torch.int32, device=sdev)
         if (nl > 1 and not as_torch and (weights is None or all(np.ndim(w) == 0 for w in weights))
                 and all(len({np.asarray(a).dtype for a in ll}) == 1 for ll in layer_lists)):
             # host payloads of one dtype: pack on the host, one H2D copy per party
@@ -280,48 +286,83 @@ class SecureAggregator(Aggregator):
         return True
 
     def _staging(self, C: int, n_pad: int, sdev):
-        """Pinned host / device buffers reused across rounds of the same size."""
+        """Pinned host / device buffers reused across rounds of the same size:
+        the input block [C, n_pad] float32 (host and device), the masked-sum
+        buffer, and one float64 block ``io`` of n_pad + 1 + C words on the
+        device with its pinned host mirror -- the decoded result, then a word
+        whose low half is the PRG flag word, then the C digests -- so that ONE
+        zero fill and ONE device-to-host copy serve all three."""
         key = (C, n_pad, str(sdev))
-        if getattr(self, "_stage_key", None) != key:
-            self._stage_in = torch.empty((C, n_pad), dtype=torch.float32, pin_memory=True)
-            self._dev_in = torch.empty((C, n_pad), dtype=torch.float32, device=sdev)
-            self._stage_out = torch.empty(n_pad, dtype=torch.float64, pin_memory=True)
-            self._stage_flags = torch.empty(1, dtype=torch.int32, pin_memory=True)
-            self._stage_key = key
-        return self._stage_in, self._dev_in, self._stage_out
+        st = getattr(self, "_stage", None)
+        if st is None or st["key"] != key:
+            io_dev = torch.empty(n_pad + 1 + C, dtype=torch.float64, device=sdev)
+            io_host = torch.empty(n_pad + 1 + C, dtype=torch.float64, pin_memory=True)
+            meta = io_dev[n_pad:].view(torch.int64)
+            small = 4 * n_pad <= SMALL_CALL_BYTES  # large calls copy from the caller's arrays
+            st = {"key": key,
+                  "in_host": torch.empty((C, n_pad) if small else (0, 0), dtype=torch.float32, pin_memory=True),
+                  "in_dev": torch.empty((C, n_pad), dtype=torch.float32, device=sdev),
+                  "sum": torch.empty(n_pad, dtype=K.U64, device=sdev),
+                  "io_dev": io_dev, "io_host": io_host, "meta": meta,
+                  "flags": meta[:1].view(torch.int32)[:1], "digests": meta[1:],
+                  "io_f64": io_host.numpy(), "io_i64": io_host.numpy().view(np.int64)}
+            st["in_np"] = st["in_host"].numpy()
+            self._stage = st
+        return st
 
     def _aggregate_host_fused(self, data, layer_lists, sizes, shapes, weights, average, is_list, payloads,
-                              flags, digests_keep):
-        """Every party's layers packed into one pinned [C, n] block, ONE H2D
-        copy, the fused masking launch (same kernels and stream positions as
-        the general path: bit-identical), decode, ONE D2H copy of the result
-        (and of the 4-byte PRG flag), one synchronisation."""
+                              digests_keep):
+        """Small calls (up to SMALL_CALL_BYTES a party): every party's layers
+        packed into one pinned [C, n] block, ONE H2D copy, one zero fill (PRG
+        flag + digests), the fused masking launch (same kernels and stream
+        positions as the general path: bit-identical), decode, ONE D2H copy of
+        the result with the flag word and the digests, one synchronisation.
+        Large calls copy each party's array and the result directly."""
         sdev = self._device.torch_device
         C, n = len(data), sum(sizes)
         n_pad = -(-n // 4) * 4  # rows start 16-byte aligned
-        stage_in, dev_in, stage_out = self._staging(C, n_pad, sdev)
-        host = stage_in.numpy()
-        for c, ll in enumerate(layer_lists):
-            np.concatenate([np.asarray(a, dtype=np.float32).reshape(-1) for a in ll], out=host[c, :n])
+        st = self._staging(C, n_pad, sdev)
+        # small calls: one pinned block, one copy; large ones: the driver's
+        # pageable copy per party (its staging pipelines, a host memcpy into
+        # pinned memory first does not)
+        big = 4 * n_pad > SMALL_CALL_BYTES
+        host = st["in_np"]
         with torch.cuda.device(sdev):
-            dev_in.copy_(stage_in, non_blocking=True)
+            dev_in = st["in_dev"]
+            for c, ll in enumerate(layer_lists):
+                if big:
+                    src = (np.asarray(ll[0], dtype=np.float32).reshape(-1) if len(ll) == 1 else
+                           np.concatenate([np.asarray(a, dtype=np.float32).reshape(-1) for a in ll]))
+                    dev_in[c, :n].copy_(torch.from_numpy(np.ascontiguousarray(src)))
+                elif len(ll) == 1:
+                    host[c, :n] = np.asarray(ll[0], dtype=np.float32).reshape(-1)
+                else:
+                    np.concatenate([np.asarray(a, dtype=np.float32).reshape(-1) for a in ll], out=host[c, :n])
+            if not big:
+                dev_in.copy_(st["in_host"], non_blocking=True)
+            st["meta"].zero_()
             xs = [dev_in[c, :n] for c in range(C)]
             ws = [1.0 if weights is None else float(w) for w in (weights or [None] * C)]
-            s = self._masked_sum(data, xs, [np.dtype(np.float32)] * C, ws, [None] * C, n, flags, [],
-                                 digests_keep)
+            s = self._masked_sum(data, xs, [np.dtype(np.float32)] * C, ws, [None] * C, n, st["flags"], [],
+                                 digests_keep, s_out=st["sum"][:n], digests_out=st["digests"])
             divisor = 1.0
             if average:
                 divisor = float(C) if weights is None else float(sum(weights))
-            dec = torch.empty(n, dtype=torch.float64, device=sdev)
-            K.decode(s, dec, fxp_bits=self._fxp_bits, divisor=divisor)
-            stage_out[:n].copy_(dec, non_blocking=True)
-            self._stage_flags.copy_(flags, non_blocking=True)
-            torch.cuda.current_stream(sdev).synchronize()
-        out = stage_out.numpy()[:n].copy()
-        if int(self._stage_flags[0]) & L.SA_FLAG_PRG_REJECT:
+            K.decode(s, st["io_dev"][:n], fxp_bits=self._fxp_bits, divisor=divisor)
+            if big:
+                out = st["io_dev"][:n].cpu().numpy()
+                st["io_host"][n_pad:].copy_(st["io_dev"][n_pad:])
+            else:
+                st["io_host"].copy_(st["io_dev"], non_blocking=True)
+                torch.cuda.current_stream(sdev).synchronize()
+        io64, ioi = st["io_f64"], st["io_i64"]
+        if not big:
+            out = io64[:n].copy()
+        if int(ioi[n_pad]) & L.SA_FLAG_PRG_REJECT:  # the flag word's low half (little-endian)
             raise _Rejected()
-        self.last_digests = digests_keep
-        parts = np.split(out, np.cumsum(sizes)[:-1])
+        self.last_digests = [None if d is None else torch.from_numpy(ioi[n_pad + 1:n_pad + 1 + C].copy())
+                             for d in digests_keep]
+        parts = np.split(out, np.cumsum(sizes)[:-1]) if len(sizes) > 1 else [out]
         result = [p.reshape(sh) for p, sh in zip(parts, shapes)]
         if not is_list:
             return PYUObject(self._device, result[0])
@@ -334,6 +375,7 @@ class SecureAggregator(Aggregator):
         server = self._device
         nl = len(shapes)
         out_layers = [None] * nl
+        host_groups = []
         for lis, sizes, g in groups:
             n = g["n"]
             keep_before = len(masked_keep)
@@ -360,11 +402,30 @@ class SecureAggregator(Aggregator):
                         for w in weights]
                     divisor_vec = K.sum_f64(wb, torch.empty(n, dtype=torch.float64, device=sdev))
             K.decode(s, dec, fxp_bits=self._fxp_bits, divisor=divisor, divisor_vec=divisor_vec)
-            parts = dec.split(sizes) if as_torch else np.split(dec.cpu().numpy(), np.cumsum(sizes)[:-1])
-            for li, part in zip(lis, parts):
-                out_layers[li] = part.reshape(shapes[li])
+            if as_torch:
+                for li, part in zip(lis, dec.split(sizes)):
+                    out_layers[li] = part.reshape(shapes[li])
+            elif 8 * n > SMALL_CALL_BYTES:
+                vals = dec.cpu().numpy()
+                for li, part in zip(lis, np.split(vals, np.cumsum(sizes)[:-1])):
+                    out_layers[li] = part.reshape(shapes[li])
+            else:  # small host results: pinned copies, collected after ONE synchronisation below
+                host = torch.empty(n, dtype=torch.float64, pin_memory=True)
+                host.copy_(dec, non_blocking=True)
+                host_groups.append((lis, sizes, host))
 
-        if int(flags.item()) & L.SA_FLAG_PRG_REJECT:
+        if not host_groups:
+            rejected = int(flags.item()) & L.SA_FLAG_PRG_REJECT
+        else:
+            fl_host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            fl_host.copy_(flags, non_blocking=True)
+            torch.cuda.current_stream(sdev).synchronize()
+            rejected = int(fl_host[0]) & L.SA_FLAG_PRG_REJECT
+            for lis, sizes, host in host_groups:
+                vals = host.numpy().copy()
+                for li, part in zip(lis, np.split(vals, np.cumsum(sizes)[:-1]) if len(lis) > 1 else [vals]):
+                    out_layers[li] = part.reshape(shapes[li])
+        if rejected:
             raise _Rejected()
         if self._keep_masked:
             self.last_masked = masked_keep
@@ -378,6 +439,7 @@ class SecureAggregator(Aggregator):
         """Per-party device vector, arithmetic type and weight of one layer."""
         n = int(np.prod(shape)) if shape else 1
         xs, cts, ws, wvecs = [], [], [], []
+        packed = self._pack_host(data, arrays, n)
         for ci, d in enumerate(data):
             party = d.device
             a = arrays[ci]
@@ -389,7 +451,8 @@ class SecureAggregator(Aggregator):
             xt = ldt if ldt in _NP2T else (np.dtype(np.int64) if ldt.kind in "biu" else np.dtype(np.float64))
             if ldt.kind in "biu" and ldt != np.dtype(np.int64) and ct.kind == "i":
                 raise NotImplementedError(f"integer data of type {ldt} is not supported")
-            x = self._to_device(a, xt, party)
+            x = packed[ci] if packed.get(ci) is not None and packed[ci].dtype == _NP2T[xt] else \
+                self._to_device(a, xt, party)
             wv, wscalar = None, 1.0
             if w is not None:
                 if np.ndim(w) == 0:
@@ -404,6 +467,36 @@ class SecureAggregator(Aggregator):
         return {"n": n, "xs": xs, "cts": cts, "ws": ws, "wvecs": wvecs}
 
     @staticmethod
+    def _pack_host(data, arrays, n) -> dict:
+        """Host (numpy) arrays of parties on one GPU with one element type:
+        packed into one pinned block, ONE host-to-device copy per GPU (the
+        small calls of secondary callers, e.g. HomoBinning's counts, are
+        bound by per-copy latency).  Returns {party index: device row}."""
+        groups = {}
+        for ci, d in enumerate(data):
+            a = arrays[ci]
+            if isinstance(a, torch.Tensor) or n == 0:
+                continue
+            a = np.asarray(a)
+            if a.dtype not in _NP2T or n * a.dtype.itemsize > SMALL_CALL_BYTES:
+                continue
+            groups.setdefault((d.device.torch_device, a.dtype), []).append(ci)
+        rows = {}
+        for (dev, dt), cis in groups.items():
+            if len(cis) < 2:
+                continue
+            per = 16 // dt.itemsize
+            n_pad = -(-n // per) * per  # every row 16-byte aligned
+            host = torch.empty((len(cis), n_pad), dtype=_NP2T[dt], pin_memory=True)
+            hv = host.numpy()
+            for r, ci in enumerate(cis):
+                hv[r, :n] = np.asarray(arrays[ci]).reshape(-1)
+            dv = host.to(dev, non_blocking=True)
+            for r, ci in enumerate(cis):
+                rows[ci] = dv[r, :n]
+        return rows
+
+    @staticmethod
     def _to_device(a, xt: np.dtype, party: PYU) -> torch.Tensor:
         tdt = _NP2T[xt]
         if isinstance(a, torch.Tensor):
@@ -415,19 +508,25 @@ class SecureAggregator(Aggregator):
             t = t.clone()
         return t
 
-    def _masked_sum(self, data, xs, cts, ws, wvecs, n, flags, masked_keep, digests_keep):
+    def _masked_sum(self, data, xs, cts, ws, wvecs, n, flags, masked_keep, digests_keep, *, s_out=None,
+                    digests_out=None):
+        """``s_out`` / ``digests_out``: preallocated sum (n) and zeroed digest
+        (C) buffers on the server GPU (the host latency path's staging)."""
         server = self._device
         sdev = server.torch_device
         parties = [d.device for d in data]
         names = [p.party for p in parties]
         C = len(names)
-        s = torch.empty(n, dtype=K.U64, device=sdev)
+        s = torch.empty(n, dtype=K.U64, device=sdev) if s_out is None else s_out
         # more co-located parties than one launch holds: the pair-shared
         # multi-launch schedule (kernels.fused_many), which forms only the sum
         # (no per-party digests; wire images and the careful replay take the
         # per-party path below)
         many = C > MAX_FUSED_CLIENTS
-        digests = None if many else torch.zeros(C, dtype=K.U64, device=sdev)
+        if many:
+            digests = None
+        else:
+            digests = torch.zeros(C, dtype=K.U64, device=sdev) if digests_out is None else digests_out
         fusable = (self._fused and C >= 2 and (not many or not (self._keep_masked or self._careful))
                    and all(p.gpu == server.gpu for p in parties)
                    and all(ct == np.dtype(np.float32) for ct in cts)
@@ -460,19 +559,22 @@ class SecureAggregator(Aggregator):
                 masked_keep.append(masked)
         else:
             if digests is None:
-                digests = torch.zeros(C, dtype=K.U64, device=sdev)
+                digests = torch.zeros(C, dtype=K.U64, device=sdev) if digests_out is None else digests_out
             masked = []
             for ci, p in enumerate(parties):
-                out = torch.empty(n, dtype=K.U64, device=p.torch_device)
-                dig = torch.zeros(1, dtype=K.U64, device=p.torch_device)
-                fl = flags if p.torch_device == sdev else torch.zeros(1, dtype=torch.int32, device=p.torch_device)
-                with torch.cuda.device(p.torch_device):
+                pdev = p.torch_device
+                local = pdev == sdev
+                out = torch.empty(n, dtype=K.U64, device=pdev)
+                # a party on the server's GPU writes its digest and flag in place
+                dig = digests[ci:ci + 1] if local else torch.zeros(1, dtype=K.U64, device=pdev)
+                fl = flags if local else torch.zeros(1, dtype=torch.int32, device=pdev)
+                with torch.cuda.device(pdev):
                     K.mask(xs[ci], out, client_streams[ci], weight=ws[ci], weight_vec=wvecs[ci],
                            compute_dtype=_NP2T[cts[ci]], fxp_bits=self._fxp_bits, digest=dig, flags=fl)
-                if fl is not flags:
+                if not local:
                     flags |= fl.to(sdev)
-                digests[ci] = dig.to(sdev)[0]
-                masked.append(out.to(sdev))   # the wire: masked vector to the server
+                    digests[ci] = dig.to(sdev)[0]
+                masked.append(out if local else out.to(sdev))   # the wire: masked vector to the server
             with torch.cuda.device(sdev):
                 K.sum_u64(masked, s)
             if self._keep_masked:
