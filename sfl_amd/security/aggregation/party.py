@@ -28,7 +28,6 @@ spawned process per party.
 
 from __future__ import annotations
 
-import copy
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -73,7 +72,7 @@ def agree(masker: Masker, peer_keys: dict, seeds: dict | None = None) -> Masker:
     """Runs on the participant: pairwise seeds from the revealed public keys
     (``seeds``: explicit ``{peer: seed | (state, inc)}`` for tests).  Returns
     the agreed masker (a new object, like ``mask_payload``)."""
-    masker = copy.deepcopy(masker)
+    masker = masker.copy()
     if seeds is None:
         masker.agree({str(k): int(v) for k, v in peer_keys.items()})
     else:
@@ -121,7 +120,7 @@ def mask_payload(masker: Masker, payload, weight=None, gpu: int | None = 0):
     some parties' streams."""
     from .secure_aggregator import _compute_dtype, _np_dtype, _shape
 
-    masker = copy.deepcopy(masker)
+    masker = masker.copy()
     layers, container = _layers(payload)
     weight = _host_weight(weight)
     shapes = [_shape(a) for a in layers]
@@ -189,46 +188,81 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
     """One launch group on the party's GPU: ``sa_mask`` over the packed
     layers ``xs`` from the masker's current stream positions; a flagged raw
     0 is moved onto numpy's stream (``sa_stream_shift``).  Returns the host
-    uint64 vector and ``{peer: extra raw draws}``."""
+    uint64 vector and ``{peer: extra raw draws}``.
+
+    The masked vector and the PRG flag word share one device buffer, so a
+    small call (up to ``SMALL_CALL_BYTES``) brings both back with one copy
+    into pinned memory and one synchronisation."""
     import torch
 
     from ... import _lib as L
     from ... import kernels as K
+    from .secure_aggregator import SMALL_CALL_BYTES
 
     if gpu is None:
         raise RuntimeError("the party has no GPU: libsfl_sa masks on the device")
     dev = torch.device("cuda", gpu)
     tdt = {_F32: torch.float32, _F64: torch.float64, _I64: torch.int64}
-    if not any(isinstance(a, torch.Tensor) for a in xs):
-        # host layers (FedAvgW's get_weights payloads): packed on the host, ONE H2D copy
-        flat = (np.ascontiguousarray(np.asarray(xs[0]), dtype=xt).reshape(-1) if len(xs) == 1 else
-                np.concatenate([np.asarray(a, dtype=xt).reshape(-1) for a in xs]))
-        x = torch.from_numpy(flat).to(dev)
-    else:
-        parts = [a.detach().reshape(-1).to(device=dev, dtype=tdt[xt]) if isinstance(a, torch.Tensor) else
-                 torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=xt).reshape(-1)).to(dev) for a in xs]
-        x = parts[0] if len(parts) == 1 else torch.cat(parts)
-    x = x.contiguous()
-    if x.data_ptr() % 16:
-        x = x.clone()
-    n = x.numel()
-    wv = None if wvec is None else torch.from_numpy(wvec).to(dev)
+    n = int(sum(int(np.prod(_shape_of(a))) for a in xs))
+    small = 8 * n <= SMALL_CALL_BYTES
     with torch.cuda.device(dev):
-        out = torch.empty(n, dtype=K.U64, device=dev)
-        flags = torch.zeros(1, dtype=torch.int32, device=dev)
+        if not any(isinstance(a, torch.Tensor) for a in xs):
+            # host layers (FedAvgW's get_weights payloads): packed on the host, ONE H2D copy
+            if small:
+                pin = torch.empty(n, dtype=tdt[xt], pin_memory=True)
+                pv = pin.numpy()
+                off = 0
+                for a in xs:
+                    a = np.asarray(a).reshape(-1)
+                    pv[off:off + a.size] = a
+                    off += a.size
+                x = pin.to(dev, non_blocking=True)
+            else:
+                flat = (np.ascontiguousarray(np.asarray(xs[0]), dtype=xt).reshape(-1) if len(xs) == 1 else
+                        np.concatenate([np.asarray(a, dtype=xt).reshape(-1) for a in xs]))
+                x = torch.from_numpy(flat).to(dev)
+        else:
+            parts = [a.detach().reshape(-1).to(device=dev, dtype=tdt[xt]) if isinstance(a, torch.Tensor) else
+                     torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=xt).reshape(-1)).to(dev)
+                     for a in xs]
+            x = parts[0] if len(parts) == 1 else torch.cat(parts)
+        x = x.contiguous()
+        if x.data_ptr() % 16:
+            x = x.clone()
+        wv = None if wvec is None else torch.from_numpy(wvec).to(dev)
+        buf = torch.empty(n + 1, dtype=K.U64, device=dev)  # masked vector | flag word
+        out = buf[:n]
+        flags = buf[n:].view(torch.int32)[:1]
+        buf[n:].zero_()
         streams = masker.streams()
         K.mask(x, out, streams, weight=wscalar, weight_vec=wv, compute_dtype=tdt[ct],
                fxp_bits=masker.fxp_bits, flags=flags)
+        if small:
+            pin_out = torch.empty(n + 1, dtype=K.U64, pin_memory=True)
+            pin_out.copy_(buf, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+            hv = pin_out.numpy().view(np.uint64)
+            flag = int(hv[n]) & 0xFFFFFFFF  # the flag word's low half (little-endian)
+        else:
+            flag = int(flags.item())
         extra = {}
-        if int(flags.item()) & L.SA_FLAG_PRG_REJECT:
+        if flag & L.SA_FLAG_PRG_REJECT:
             found = K.rejected_draws_many([g for g, _, _ in streams], n, dev)
             for peer, (gen, sign, _), (pts, total) in zip(masker.peers, streams, found):
                 for k, shift in pts:
                     K.stream_shift(out, gen, sign, k, shift)
                 if total > n:
                     extra[peer] = total - n
-        host = K.as_u64(out)
+            host = K.as_u64(out)
+        elif small:
+            host = hv[:n].copy()
+        else:
+            host = K.as_u64(out)
     return host, extra
+
+
+def _shape_of(a):
+    return tuple(a.shape) if hasattr(a, "shape") else np.shape(a)
 
 
 # ------------------------------------------------------------- server side
@@ -276,30 +310,58 @@ class DigestMismatch(RuntimeError):
 
 
 def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_torch):
+    """The server's device work: the payloads in (one pinned copy for a small
+    call), their XOR digests, the mod-2^64 sum and the decode; the decoded
+    result and the digests share one device buffer, so a small host result
+    comes back with one copy and one synchronisation."""
     import torch
 
     from ... import kernels as K
+    from .secure_aggregator import SMALL_CALL_BYTES
 
     if gpu is None:
         raise RuntimeError("the server has no GPU: libsfl_sa sums on the device")
     dev = torch.device("cuda", gpu)
-    n = int(u64s[0].size)
+    n, C = int(u64s[0].size), len(u64s)
+    small = 8 * n <= SMALL_CALL_BYTES
     with torch.cuda.device(dev):
-        vecs = [torch.from_numpy(np.ascontiguousarray(u).view(np.int64)).to(dev, non_blocking=False) for u in u64s]
-        out = torch.empty(n, dtype=torch.float64, device=dev)
+        if small and n:
+            n_pad = n + (n & 1)  # rows 16-byte aligned
+            pin = torch.empty((C, n_pad), dtype=torch.int64, pin_memory=True)
+            pv = pin.numpy()
+            for i, u in enumerate(u64s):
+                pv[i, :n] = np.asarray(u).view(np.int64)
+            dv = pin.to(dev, non_blocking=True)
+            vecs = [dv[i, :n] for i in range(C)]
+        else:
+            vecs = [torch.from_numpy(np.ascontiguousarray(u).view(np.int64)).to(dev, non_blocking=False)
+                    for u in u64s]
+        io = torch.empty(n + C, dtype=torch.float64, device=dev)  # decoded result | digests
+        out = io[:n]
         if n:
-            dig = torch.zeros(len(vecs), dtype=K.U64, device=dev)
+            dig = io[n:].view(torch.int64)
+            dig.zero_()
             for i, v in enumerate(vecs):
                 K.xor_digest(v, dig[i:i + 1])
             s = torch.empty(n, dtype=K.U64, device=dev)
             K.sum_u64(vecs, s)
-            dv = None
+            dv_ = None
             if divisor_vec is not None:
-                dv = K.sum_f64([torch.from_numpy(w).to(dev) for w in divisor_vec],
-                               torch.empty(n, dtype=torch.float64, device=dev))
-            K.decode(s, out, fxp_bits=fxp_bits, divisor=divisor, divisor_vec=dv)
-            got = K.as_u64(dig).tolist()
+                dv_ = K.sum_f64([torch.from_numpy(w).to(dev) for w in divisor_vec],
+                                torch.empty(n, dtype=torch.float64, device=dev))
+            K.decode(s, out, fxp_bits=fxp_bits, divisor=divisor, divisor_vec=dv_)
+            if small and not as_torch:
+                pin_io = torch.empty(n + C, dtype=torch.float64, pin_memory=True)
+                pin_io.copy_(io, non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
+                hv = pin_io.numpy()
+                got = hv[n:].view(np.uint64).tolist()
+                result = hv[:n].copy()
+            else:
+                got = K.as_u64(dig).tolist()
+                result = out if as_torch else out.cpu().numpy()
             for i, (g, want) in enumerate(zip(got, digests)):
                 if int(g) != int(want) & ((1 << 64) - 1):
                     raise DigestMismatch(f"masked vector {i}: digest {int(g):016x}, sent {int(want):016x}")
+            return result
     return out if as_torch else out.cpu().numpy()

@@ -33,9 +33,13 @@ def main():
     pyus = [PYU(n, 0) for n in names]
     server = PYU("carol", 0)
     rng = np.random.default_rng(1)
-    for dt in (np.float32, np.float64, np.int64):
+    from sfl_amd.compat import secretflow as hip_compat
+
+    cases = [(dt, SecureAggregator) for dt in (np.float32, np.float64, np.int64)]
+    cases.append((np.float32, hip_compat.SecureAggregator))  # the per-party drop-in, in-process devices
+    for dt, cls in cases:
         xs = [(rng.random(args.elems) * 1000).astype(dt) for _ in names]
-        agg = SecureAggregator(server, pyus)
+        agg = cls(server, pyus)
         objs = [PYUObject(p, x) for p, x in zip(pyus, xs)]
         for _ in range(200):
             agg.sum(objs, axis=0)
@@ -51,7 +55,7 @@ def main():
         pr.disable()
         s = io.StringIO()
         pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(args.top)
-        print(f"==== {np.dtype(dt).name}: {per * 1e6:.1f} us per call (unprofiled)")
+        print(f"==== {np.dtype(dt).name} {cls.__module__}: {per * 1e6:.1f} us per call (unprofiled)")
         print(s.getvalue())
 
 
