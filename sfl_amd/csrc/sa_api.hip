@@ -11,6 +11,7 @@
 #include "../../include/sfl_sa.h"
 #include "pcg128.h"
 #include "sa_internal.h"
+#include "sa_tiles.h"
 #include "sa_philox.h"
 
 namespace sa {
@@ -96,7 +97,7 @@ struct SumArgs {
 
 __global__ void __launch_bounds__(256) k_sum_u64(const SumArgs a) {
   const uint64_t n2 = a.n / 2;
-  const uint64_t base = (uint64_t)blockIdx.x * kTileAccesses + threadIdx.x;
+  const uint64_t base = (uint64_t)stream_tile() * kTileAccesses + threadIdx.x;
   u64x2 s[kUnroll];
 #pragma unroll
   for (int u = 0; u < kUnroll; u++)
@@ -129,7 +130,7 @@ __global__ void __launch_bounds__(256) k_decode(const uint64_t* __restrict__ s, 
                                                 double div, const double* __restrict__ divv,
                                                 double* __restrict__ out) {
   const uint64_t n2 = n / 2;
-  const uint64_t base = (uint64_t)blockIdx.x * kTileAccesses + threadIdx.x;
+  const uint64_t base = (uint64_t)stream_tile() * kTileAccesses + threadIdx.x;
   const u64x2* s2 = reinterpret_cast<const u64x2*>(s);
   const f64x2* d2 = reinterpret_cast<const f64x2*>(divv);
   f64x2* o2 = reinterpret_cast<f64x2*>(out);
@@ -170,7 +171,7 @@ struct SumF64Args {
 };
 __global__ void __launch_bounds__(256) k_sum_f64(const SumF64Args a) {
   const uint64_t n2 = a.n / 2;
-  const uint64_t base = (uint64_t)blockIdx.x * kTileAccesses + threadIdx.x;
+  const uint64_t base = (uint64_t)stream_tile() * kTileAccesses + threadIdx.x;
   const int j0 = a.accumulate ? 0 : 1;
   const f64x2* first = reinterpret_cast<const f64x2*>(a.accumulate ? a.out : a.in[0]);
   f64x2 s[kUnroll];

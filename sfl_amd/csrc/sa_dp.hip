@@ -8,6 +8,7 @@
 #include "../../include/sfl_sa.h"
 #include "pcg128.h"
 #include "sa_internal.h"
+#include "sa_tiles.h"
 #include "sa_philox.h"
 
 namespace sa {
@@ -182,7 +183,7 @@ __device__ __forceinline__ void dp_perturb_tile(const DpArgs& a) {
   const uint64_t full = a.n / 4;
   const f32x4* x4 = reinterpret_cast<const f32x4*>(a.x);
   f32x4* o4 = reinterpret_cast<f32x4*>(a.out);
-  const uint64_t b0 = (uint64_t)blockIdx.x * (256 * T) + threadIdx.x;
+  const uint64_t b0 = (uint64_t)stream_tile() * (256 * T) + threadIdx.x;
   if (b0 + (uint64_t)(T - 1) * 256 < full) {
     f32x4 v[T];
 #pragma unroll
