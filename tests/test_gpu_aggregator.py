@@ -357,3 +357,61 @@ def test_many_colocated_parties_pair_shared(as_torch):
         exp = o.secure_average(xs, names, weights=w, seeds=seeds, offset=offset)[0]
         assert np.array_equal(got, exp), rnd
         offset += xs[0].size
+
+
+@pytest.mark.parametrize("dtype,n", [(np.float32, 262_144), (np.float32, 262_148), (np.float64, 131_072),
+                                     (np.float64, 131_073), (np.int64, 131_072), (np.int64, 131_073)])
+def test_small_call_boundary_bit_exact(dtype, n):
+    """Both sides of SMALL_CALL_BYTES (1 MiB a party): the pinned one-copy
+    path and the direct-copy path, 3 parties, sum then weighted average
+    (consecutive stream positions), then a small call again on the same
+    aggregator (staging reused across sizes) -- bit-exact vs the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    names = ["alice", "bob", "carol"]
+    seeds = o.seeds_for(names)
+    pyus = [PYU(nm, 0) for nm in names]
+    agg = SecureAggregator(PYU("server", 0), pyus,
+                           seeds={(a, b): seeds[a][b] for a in names for b in names if a < b})
+    rng = np.random.default_rng(n)
+    mk = (lambda m: (rng.standard_normal(m) * 3).astype(dtype)) if dtype != np.int64 else \
+        (lambda m: rng.integers(-10**6, 10**6, m))
+    xs = [mk(n) for _ in names]
+    ws = [2, 3, 5]
+    objs = [p(lambda x=x: x)() for p, x in zip(pyus, xs)]
+    s = rv(agg.sum(objs, axis=0))
+    assert np.array_equal(s, o.secure_sum(xs, names, seeds=seeds)[0])
+    avg = rv(agg.average(objs, axis=0, weights=ws))
+    assert np.array_equal(avg, o.secure_average(xs, names, weights=ws, seeds=seeds, offset=n)[0])
+    ys = [mk(99) for _ in names]
+    s2 = rv(agg.sum([p(lambda y=y: y)() for p, y in zip(pyus, ys)], axis=0))
+    assert np.array_equal(s2, o.secure_sum(ys, names, seeds=seeds, offset=2 * n)[0])
+
+
+@pytest.mark.parametrize("n", [131_072, 131_073])
+def test_party_functions_small_call_boundary_bit_exact(n):
+    """The per-party drop-in steps on both sides of SMALL_CALL_BYTES:
+    party.mask_payload's masked vector and party.sum_decode's result
+    bit-exact vs the oracle, the masker advanced by n."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.security.aggregation import party as P
+
+    names = ["alice", "bob"]
+    seeds = o.seeds_for(names)
+    ms = [P.agree(P.new_masker(nm), {p: 0 for p in names}, {p: seeds[nm][p] for p in names if p != nm})
+          for nm in names]
+    rng = np.random.default_rng(n)
+    xs = [(rng.standard_normal(n) * 0.1).astype(np.float32) for _ in names]
+    masked = o.secure_masked(xs, names, seeds=seeds)
+    pays = []
+    for i, (m, x) in enumerate(zip(ms, xs)):
+        pay, m2 = P.mask_payload(m, x, None, 0)
+        assert np.array_equal(pay.u64, masked[i])
+        assert m2.position(names[1 - i]) == n and m.position(names[1 - i]) == 0
+        pays.append(pay)
+    got = P.sum_decode(*pays, gpu=0)
+    assert np.array_equal(got, o.secure_sum(xs, names, seeds=seeds)[0])
