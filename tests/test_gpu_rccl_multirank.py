@@ -34,7 +34,11 @@ def test_every_collective_between_real_rccl_ranks(world):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_hostid_probe.py"), "--world", str(world)],
                        capture_output=True, text=True, timeout=200, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
-    res = [json.loads(ln[len("PROBE "):]) for ln in r.stdout.splitlines() if ln.startswith("PROBE ")]
+    dec, res, i = json.JSONDecoder(), [], r.stdout.find("PROBE ")
+    while i >= 0:  # every "PROBE {...}" record, wherever the ranks' lines fell
+        obj, end = dec.raw_decode(r.stdout, i + len("PROBE "))
+        res.append(obj)
+        i = r.stdout.find("PROBE ", end)
     assert sorted(x["rank"] for x in res) == list(range(world)), r.stdout
     for x in res:
         assert "error" not in x, x

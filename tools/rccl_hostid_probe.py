@@ -91,7 +91,9 @@ def rank_main():
         comm.close()
     except Exception as e:  # noqa: BLE001 - the probe reports it
         out["error"] = repr(e)[:600]
-    print("PROBE " + json.dumps(out), flush=True)
+    # one write(2) per line: the ranks share the parent's stdout pipe, and a
+    # print's text and newline can otherwise interleave with another rank's
+    os.write(1, ("PROBE " + json.dumps(out) + "\n").encode())
     dist.destroy_process_group()
 
 
