@@ -159,6 +159,30 @@ int sa_fused_clients(const sa_local_client* clients, int n_clients, int x_type, 
                      const sa_mask_stream* cross, int n_cross, uint64_t* sum_out, int accumulate,
                      uint64_t* digests, uint32_t* flags, void* stream);
 
+/* Host-resident float32 clients, co-located on one GPU, in ONE blocking call:
+ * the small-call path of `SecureAggregator.sum` / `.average` on host arrays
+ * (FL rounds of small models, HomoBinning's
+ * counts), where per-call latency, not bandwidth, decides.  Copies the
+ * n_clients host vectors into `pinned`, ONE host-to-device copy, zeroes the
+ * flag + digest words, sa_fused_clients (masked_out NULL, no cross streams),
+ * sa_decode by `divisor`, ONE device-to-host copy of result + flag word +
+ * digests, synchronises `stream`, then fills the outputs.  With n_pad = n
+ * rounded up to a multiple of 4, the caller owns (nothing is allocated):
+ *   pinned  >= n_clients*n_pad*4 + (n_pad + 1 + n_clients)*8 bytes of
+ *           page-locked host memory, 16-byte aligned;
+ *   dev     >= n_clients*n_pad*4 + n_pad*8 + (n_pad + 1 + n_clients)*8
+ *           bytes of device memory, 16-byte aligned.
+ * Outputs (host): out[n] the decoded float64, digests[n_clients] the masked
+ * vectors' XOR digests, *flags the PRG flag word (SA_FLAG_PRG_REJECT: the
+ * caller replays the round as after sa_fused_clients).  2..8 clients.
+ * Unlike the launch functions this one blocks: it returns once the result
+ * is on the host.  Replaces, for co-located parties, the per-party `mask`
+ * calls plus the server's `_sum` and decode. */
+int sa_fused_clients_host_f32(const float* const* host_x, const double* weights, int n_clients, uint64_t n,
+                              int fxp_bits, const sa_pcg64* pair_gens, const int8_t* pair_sign, double divisor,
+                              void* pinned, void* dev, double* out, uint64_t* digests, uint32_t* flags,
+                              void* stream);
+
 /* One block of the pair-shared schedule for MORE co-located clients than one
  * sa_fused_clients launch holds (more than 8): the 8 slots are two quads of
  * clients, (0-3) and (4-7), and the launch expands only the 16 streams of the

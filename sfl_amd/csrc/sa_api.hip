@@ -696,3 +696,48 @@ extern "C" int sa_sum_f64(const double* const* w, int k, uint64_t n, double* out
   }
   return SA_OK;
 }
+
+extern "C" int sa_fused_clients_host_f32(const float* const* host_x, const double* weights, int n_clients,
+                                         uint64_t n, int fxp_bits, const sa_pcg64* pair_gens,
+                                         const int8_t* pair_sign, double divisor, void* pinned, void* dev,
+                                         double* out, uint64_t* digests, uint32_t* flags, void* stream) {
+  if (!host_x || !weights || n_clients < 2 || n_clients > 8 || n == 0 || !pair_gens || !pair_sign || !pinned ||
+      !dev || !out || !digests || !flags || ((uintptr_t)pinned & 15) || ((uintptr_t)dev & 15)) {
+    sa_set_error("sa_fused_clients_host_f32: bad arguments (2..8 clients, n > 0, 16-byte aligned buffers)");
+    return SA_ERR_ARG;
+  }
+  for (int c = 0; c < n_clients; c++)
+    if (!host_x[c]) {
+      sa_set_error("sa_fused_clients_host_f32: host_x[%d] is NULL", c);
+      return SA_ERR_ARG;
+    }
+  const uint64_t C = (uint64_t)n_clients, n_pad = (n + 3) & ~3ull;
+  float* pin_in = (float*)pinned;
+  double* pin_io = (double*)((char*)pinned + C * n_pad * 4);
+  float* d_in = (float*)dev;
+  uint64_t* d_sum = (uint64_t*)((char*)dev + C * n_pad * 4);
+  double* d_io = (double*)((char*)d_sum + n_pad * 8);  // result | flag word | digests
+  const hipStream_t s = (hipStream_t)stream;
+  for (uint64_t c = 0; c < C; c++) memcpy(pin_in + c * n_pad, host_x[c], n * 4);
+  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * 4, hipMemcpyHostToDevice, s));
+  SA_HIP_CHECK(hipMemsetAsync(d_io + n_pad, 0, (1 + C) * 8, s));
+  sa_local_client cl[8];
+  for (uint64_t c = 0; c < C; c++) {
+    cl[c].x = d_in + c * n_pad;
+    cl[c].weight = weights[c];
+    cl[c].masked_out = nullptr;
+  }
+  int rc = sa_fused_clients(cl, n_clients, SA_F32, n, fxp_bits, pair_gens, pair_sign, nullptr, 0, d_sum, 0,
+                            (uint64_t*)(d_io + n_pad + 1), (uint32_t*)(d_io + n_pad), stream);
+  if (rc) return rc;
+  rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_io, stream);
+  if (rc) return rc;
+  SA_HIP_CHECK(hipMemcpyAsync(pin_io, d_io, (n_pad + 1 + C) * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK(hipStreamSynchronize(s));
+  memcpy(out, pin_io, n * 8);
+  uint64_t word;
+  memcpy(&word, pin_io + n_pad, 8);
+  *flags = (uint32_t)word;  // the flag word's low half (little-endian)
+  memcpy(digests, pin_io + n_pad + 1, C * 8);
+  return SA_OK;
+}

@@ -237,6 +237,47 @@ def decode(s: torch.Tensor, out: torch.Tensor, *, fxp_bits: int = 18, divisor: f
     return out
 
 
+def host_fused_scratch(n_clients: int, n: int) -> tuple[int, int]:
+    """(pinned bytes, device bytes) sa_fused_clients_host_f32 needs."""
+    n_pad = -(-n // 4) * 4
+    io = (n_pad + 1 + n_clients) * 8
+    return n_clients * n_pad * 4 + io, n_clients * n_pad * 4 + n_pad * 8 + io
+
+
+def fused_clients_host_f32(xs: Sequence[np.ndarray], weights: Sequence[float], pair_gens: Sequence,
+                           pair_signs: Sequence[int], pinned: torch.Tensor, dev: torch.Tensor, *,
+                           fxp_bits: int = 18, divisor: float = 1.0):
+    """Host float32 vectors of 2..8 co-located clients -> (decoded float64
+    host array, uint64 digests, flag word) in ONE blocking call (see
+    sa_fused_clients_host_f32 in include/sfl_sa.h).  ``pinned`` / ``dev``:
+    byte tensors of host_fused_scratch's sizes (page-locked / on the GPU).
+    None when the library has no fused kernel for this client count."""
+    _require_gpu(dev)
+    nc, n = len(xs), int(xs[0].size)
+    need_pin, need_dev = host_fused_scratch(nc, n)
+    if not pinned.is_pinned() or pinned.numel() < need_pin or dev.numel() < need_dev:
+        raise ValueError("scratch buffers too small or not page-locked")
+    arrs = [np.ascontiguousarray(x, dtype=np.float32).reshape(-1) for x in xs]
+    if any(a.size != n for a in arrs):
+        raise ValueError("fused clients need equal-size vectors")
+    ptrs = (C.c_void_p * nc)(*[a.ctypes.data for a in arrs])
+    ws = (C.c_double * nc)(*[float(w) for w in weights])
+    npair = nc * (nc - 1) // 2
+    pg = (L.PCG64 * max(1, npair))(*pair_gens)
+    ps = (C.c_int8 * max(1, npair))(*[int(s) for s in pair_signs])
+    out = np.empty(n, dtype=np.float64)
+    digests = np.empty(nc, dtype=np.uint64)
+    flags = C.c_uint32(0)
+    rc = L.lib().sa_fused_clients_host_f32(ptrs, ws, nc, n, int(fxp_bits), pg, ps, float(divisor),
+                                           _ptr(pinned), _ptr(dev), C.c_void_p(out.ctypes.data),
+                                           C.c_void_p(digests.ctypes.data), C.byref(flags),
+                                           C.c_void_p(_stream(dev)))
+    if rc == L.SA_ERR_UNSUPPORTED:
+        return None
+    L.check(rc, "sa_fused_clients_host_f32")
+    return out, digests, int(flags.value)
+
+
 def sum_f64(ins: Sequence[torch.Tensor], out: torch.Tensor) -> torch.Tensor:
     _require_gpu(out, *ins)
     ptrs = (C.c_void_p * len(ins))(*[t.data_ptr() for t in ins])

@@ -312,20 +312,28 @@ class SecureAggregator(Aggregator):
 
     def _aggregate_host_fused(self, data, layer_lists, sizes, shapes, weights, average, is_list, payloads,
                               digests_keep):
-        """Small calls (up to SMALL_CALL_BYTES a party): every party's layers
-        packed into one pinned [C, n] block, ONE H2D copy, one zero fill (PRG
-        flag + digests), the fused masking launch (same kernels and stream
-        positions as the general path: bit-identical), decode, ONE D2H copy of
-        the result with the flag word and the digests, one synchronisation.
-        Large calls copy each party's array and the result directly."""
+        """Small calls (up to SMALL_CALL_BYTES a party): ONE blocking library
+        call (``_host_one_call``: the parties' layers packed into one pinned
+        block, one H2D copy, one zero fill of the PRG flag + digests, the
+        fused masking launch -- same kernels and stream positions as the
+        general path: bit-identical -- decode, one D2H copy of the result
+        with the flag word and the digests, one synchronisation); the same
+        steps from Python when a replay (careful mode) or more than 8 parties
+        need the general machinery.  Large calls copy each party's array and
+        the result directly."""
         sdev = self._device.torch_device
         C, n = len(data), sum(sizes)
         n_pad = -(-n // 4) * 4  # rows start 16-byte aligned
-        st = self._staging(C, n_pad, sdev)
         # small calls: one pinned block, one copy; large ones: the driver's
         # pageable copy per party (its staging pipelines, a host memcpy into
         # pinned memory first does not)
         big = 4 * n_pad > SMALL_CALL_BYTES
+        if not big and not self._careful and C <= MAX_FUSED_CLIENTS:
+            res = self._host_one_call(data, layer_lists, sizes, shapes, weights, average, is_list, payloads,
+                                      digests_keep, C, n, sdev)
+            if res is not None:
+                return res
+        st = self._staging(C, n_pad, sdev)
         host = st["in_np"]
         with torch.cuda.device(sdev):
             dev_in = st["in_dev"]
@@ -362,6 +370,51 @@ class SecureAggregator(Aggregator):
             raise _Rejected()
         self.last_digests = [None if d is None else torch.from_numpy(ioi[n_pad + 1:n_pad + 1 + C].copy())
                              for d in digests_keep]
+        parts = np.split(out, np.cumsum(sizes)[:-1]) if len(sizes) > 1 else [out]
+        result = [p.reshape(sh) for p, sh in zip(parts, shapes)]
+        if not is_list:
+            return PYUObject(self._device, result[0])
+        return PYUObject(self._device, tuple(result) if isinstance(payloads[0], tuple) else result)
+
+    def _host_one_call(self, data, layer_lists, sizes, shapes, weights, average, is_list, payloads, digests_keep,
+                       C, n, sdev):
+        """The small call as ONE blocking library call
+        (``sa_fused_clients_host_f32``: host arrays in, decoded result,
+        digests and PRG flag out; the Python side only positions the pair
+        streams).  None when the library has no fused kernel for C."""
+        names = [d.device.party for d in data]
+        pair_gens, pair_signs = [], []
+        for u in range(C):
+            for v in range(u + 1, C):
+                mu, mv = self._maskers[names[u]], self._maskers[names[v]]
+                assert mu.position(names[v]) == mv.position(names[u]), "pair streams out of step"
+                pair_gens.append(mu.generator(names[v]))
+                pair_signs.append(mu.sign(names[v]))
+        key = (C, n, str(sdev))
+        sc = getattr(self, "_one_call", None)
+        if sc is None or sc[0] != key:
+            pin_b, dev_b = K.host_fused_scratch(C, n)
+            sc = (key, torch.empty(pin_b, dtype=torch.uint8, pin_memory=True),
+                  torch.empty(dev_b, dtype=torch.uint8, device=sdev))
+            self._one_call = sc
+        xs = [ll[0] if len(ll) == 1 else np.concatenate([np.asarray(a, dtype=np.float32).reshape(-1) for a in ll])
+              for ll in layer_lists]
+        ws = [1.0 if weights is None else float(w) for w in (weights or [None] * C)]
+        divisor = 1.0
+        if average:
+            divisor = float(C) if weights is None else float(sum(weights))
+        with torch.cuda.device(sdev):
+            got = K.fused_clients_host_f32(xs, ws, pair_gens, pair_signs, sc[1], sc[2], fxp_bits=self._fxp_bits,
+                                           divisor=divisor)
+        if got is None:
+            return None
+        out, digests, flag = got
+        if flag & L.SA_FLAG_PRG_REJECT:
+            raise _Rejected()
+        for nm in names:
+            self._maskers[nm].consume(n)
+        digests_keep.append(torch.from_numpy(digests.view(np.int64)))
+        self.last_digests = digests_keep
         parts = np.split(out, np.cumsum(sizes)[:-1]) if len(sizes) > 1 else [out]
         result = [p.reshape(sh) for p, sh in zip(parts, shapes)]
         if not is_list:
