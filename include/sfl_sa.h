@@ -183,6 +183,24 @@ int sa_fused_clients_host_f32(const float* const* host_x, const double* weights,
                               void* pinned, void* dev, double* out, uint64_t* digests, uint32_t* flags,
                               void* stream);
 
+/* The same blocking small call for any element type (float64 / int64 data,
+ * or float32 data with a float64 compute type): n_clients host vectors of
+ * x_type, every party masked by sa_mask with its OWN streams (no pair
+ * sharing: the non-float32 kernels hold one client) into a zeroed masked
+ * sum, then sa_decode.  `streams`: n_clients * (n_clients - 1) entries,
+ * client-major (client c's peers in its masker's order); `weights` are the
+ * scalar weights as sa_mask takes them.  With n_pad = n rounded up to a
+ * multiple of 4 and xs the element size of x_type:
+ *   pinned >= n_clients*n_pad*xs + (n_pad + 1 + n_clients)*8 bytes, page-locked;
+ *   dev    >= n_clients*n_pad*(xs + 8) + n_pad*8 + (n_pad + 1 + n_clients)*8 bytes;
+ * both 16-byte aligned.  2..9 clients.  Outputs as for
+ * sa_fused_clients_host_f32.  Replaces, for co-located parties with small
+ * integer / float64 vectors (HomoBinning's counts),
+ * the per-party `mask` calls plus the server's `_sum` and decode. */
+int sa_clients_host(const void* const* host_x, int x_type, int compute_type, const double* weights,
+                    int n_clients, uint64_t n, int fxp_bits, const sa_mask_stream* streams, double divisor,
+                    void* pinned, void* dev, double* out, uint64_t* digests, uint32_t* flags, void* stream);
+
 /* One block of the pair-shared schedule for MORE co-located clients than one
  * sa_fused_clients launch holds (more than 8): the 8 slots are two quads of
  * clients, (0-3) and (4-7), and the launch expands only the 16 streams of the

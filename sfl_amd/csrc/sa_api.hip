@@ -741,3 +741,50 @@ extern "C" int sa_fused_clients_host_f32(const float* const* host_x, const doubl
   memcpy(digests, pin_io + n_pad + 1, C * 8);
   return SA_OK;
 }
+
+extern "C" int sa_clients_host(const void* const* host_x, int x_type, int compute_type, const double* weights,
+                               int n_clients, uint64_t n, int fxp_bits, const sa_mask_stream* streams,
+                               double divisor, void* pinned, void* dev, double* out, uint64_t* digests,
+                               uint32_t* flags, void* stream) {
+  if (check_type(x_type, "sa_clients_host x_type") || check_type(compute_type, "sa_clients_host compute_type"))
+    return SA_ERR_ARG;
+  if (!host_x || !weights || n_clients < 2 || n_clients > 9 || n == 0 || !streams || !pinned || !dev || !out ||
+      !digests || !flags || ((uintptr_t)pinned & 15) || ((uintptr_t)dev & 15)) {
+    sa_set_error("sa_clients_host: bad arguments (2..9 clients, n > 0, 16-byte aligned buffers)");
+    return SA_ERR_ARG;
+  }
+  for (int c = 0; c < n_clients; c++)
+    if (!host_x[c]) {
+      sa_set_error("sa_clients_host: host_x[%d] is NULL", c);
+      return SA_ERR_ARG;
+    }
+  const uint64_t C = (uint64_t)n_clients, n_pad = (n + 3) & ~3ull, xs = x_type == SA_F32 ? 4 : 8;
+  char* pin_in = (char*)pinned;
+  double* pin_io = (double*)(pin_in + C * n_pad * xs);
+  char* d_in = (char*)dev;
+  uint64_t* d_masked = (uint64_t*)(d_in + C * n_pad * xs);
+  uint64_t* d_sum = d_masked + C * n_pad;
+  double* d_io = (double*)(d_sum + n_pad);  // result | flag word | digests, right behind the sum
+  const hipStream_t s = (hipStream_t)stream;
+  for (uint64_t c = 0; c < C; c++) memcpy(pin_in + c * n_pad * xs, host_x[c], n * xs);
+  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * xs, hipMemcpyHostToDevice, s));
+  SA_HIP_CHECK(hipMemsetAsync(d_sum, 0, n_pad * 8 + (n_pad + 1 + C) * 8, s));  // sum, flag word, digests
+  uint32_t* d_flags = (uint32_t*)(d_io + n_pad);
+  uint64_t* d_dig = (uint64_t*)(d_io + n_pad + 1);
+  for (uint64_t c = 0; c < C; c++) {
+    const int rc = sa_mask(d_in + c * n_pad * xs, x_type, compute_type, n, weights[c], nullptr, fxp_bits,
+                           streams + c * (C - 1), n_clients - 1, d_masked + c * n_pad, d_sum, d_dig + c, d_flags,
+                           stream);
+    if (rc) return rc;
+  }
+  const int rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_io, stream);
+  if (rc) return rc;
+  SA_HIP_CHECK(hipMemcpyAsync(pin_io, d_io, (n_pad + 1 + C) * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK(hipStreamSynchronize(s));
+  memcpy(out, pin_io, n * 8);
+  uint64_t word;
+  memcpy(&word, pin_io + n_pad, 8);
+  *flags = (uint32_t)word;
+  memcpy(digests, pin_io + n_pad + 1, C * 8);
+  return SA_OK;
+}

@@ -278,6 +278,48 @@ def fused_clients_host_f32(xs: Sequence[np.ndarray], weights: Sequence[float], p
     return out, digests, int(flags.value)
 
 
+_NP_XTYPE = {np.dtype(np.float32): L.SA_F32, np.dtype(np.float64): L.SA_F64, np.dtype(np.int64): L.SA_I64}
+
+
+def host_clients_scratch(n_clients: int, n: int, itemsize: int) -> tuple[int, int]:
+    """(pinned bytes, device bytes) sa_clients_host needs."""
+    n_pad = -(-n // 4) * 4
+    io = (n_pad + 1 + n_clients) * 8
+    return n_clients * n_pad * itemsize + io, n_clients * n_pad * (itemsize + 8) + n_pad * 8 + io
+
+
+def clients_host(xs: Sequence[np.ndarray], compute_dtype, weights: Sequence[float], streams: Sequence[Sequence],
+                 pinned: torch.Tensor, dev: torch.Tensor, *, fxp_bits: int = 18, divisor: float = 1.0):
+    """Host vectors of one element type (float32 / float64 / int64) of 2..9
+    co-located clients, each masked with its own streams (``streams[c]``:
+    (gen, sign, peer) triples) -> (decoded float64 host array, uint64
+    digests, flag word) in ONE blocking call (sa_clients_host in
+    include/sfl_sa.h)."""
+    _require_gpu(dev)
+    nc, n = len(xs), int(np.asarray(xs[0]).size)
+    dt = np.asarray(xs[0]).dtype
+    arrs = [np.ascontiguousarray(x, dtype=dt).reshape(-1) for x in xs]
+    if dt not in _NP_XTYPE or any(a.size != n for a in arrs):
+        raise ValueError("host clients need equal-size float32 / float64 / int64 vectors of one type")
+    need_pin, need_dev = host_clients_scratch(nc, n, dt.itemsize)
+    if not pinned.is_pinned() or pinned.numel() < need_pin or dev.numel() < need_dev:
+        raise ValueError("scratch buffers too small or not page-locked")
+    if any(len(st) != nc - 1 for st in streams):
+        raise ValueError("every client needs n_clients - 1 streams")
+    ptrs = (C.c_void_p * nc)(*[a.ctypes.data for a in arrs])
+    ws = (C.c_double * nc)(*[float(w) for w in weights])
+    sarr = make_streams([e for st in streams for e in st])
+    out = np.empty(n, dtype=np.float64)
+    digests = np.empty(nc, dtype=np.uint64)
+    flags = C.c_uint32(0)
+    ct = _NP_XTYPE[np.dtype(compute_dtype)]
+    L.check(L.lib().sa_clients_host(ptrs, _NP_XTYPE[dt], ct, ws, nc, n, int(fxp_bits), sarr, float(divisor),
+                                    _ptr(pinned), _ptr(dev), C.c_void_p(out.ctypes.data),
+                                    C.c_void_p(digests.ctypes.data), C.byref(flags), C.c_void_p(_stream(dev))),
+            "sa_clients_host")
+    return out, digests, int(flags.value)
+
+
 def sum_f64(ins: Sequence[torch.Tensor], out: torch.Tensor) -> torch.Tensor:
     _require_gpu(out, *ins)
     ptrs = (C.c_void_p * len(ins))(*[t.data_ptr() for t in ins])

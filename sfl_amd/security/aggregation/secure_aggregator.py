@@ -234,6 +234,11 @@ class SecureAggregator(Aggregator):
         if self._host_fusable(data, layer_lists, as_torch, weights, sum(sizes)):
             return self._aggregate_host_fused(data, layer_lists, sizes, shapes, weights, average, is_list,
                                               payloads, digests_keep)
+        if not as_torch:
+            res = self._host_general_one_call(data, layer_lists, sizes, shapes, weights, average, is_list,
+                                              payloads, digests_keep)
+            if res is not None:
+                return res
         flags = torch.zeros(1, dtype=torch.int32, device=sdev)
         if (nl > 1 and not as_torch and (weights is None or all(np.ndim(w) == 0 for w in weights))
                 and all(len({np.asarray(a).dtype for a in ll}) == 1 for ll in layer_lists)):
@@ -409,6 +414,65 @@ class SecureAggregator(Aggregator):
         if got is None:
             return None
         out, digests, flag = got
+        if flag & L.SA_FLAG_PRG_REJECT:
+            raise _Rejected()
+        for nm in names:
+            self._maskers[nm].consume(n)
+        digests_keep.append(torch.from_numpy(digests.view(np.int64)))
+        self.last_digests = digests_keep
+        parts = np.split(out, np.cumsum(sizes)[:-1]) if len(sizes) > 1 else [out]
+        result = [p.reshape(sh) for p, sh in zip(parts, shapes)]
+        if not is_list:
+            return PYUObject(self._device, result[0])
+        return PYUObject(self._device, tuple(result) if isinstance(payloads[0], tuple) else result)
+
+    def _host_general_one_call(self, data, layer_lists, sizes, shapes, weights, average, is_list, payloads,
+                               digests_keep):
+        """Small host calls of float64 / int64 data (or float32 data with a
+        float64 compute type) of 2..9 parties on the server's GPU as ONE
+        blocking library call (``sa_clients_host``: every party masked with
+        its own streams into the sum, decode, one copy each way).  None when
+        the call is not of that shape (the general path takes it)."""
+        C, n = len(data), sum(sizes)
+        if (self._careful or self._keep_masked or not self._fused or not 2 <= C <= 9 or n == 0
+                or any(d.device.gpu != self._device.gpu for d in data)):
+            return None
+        if weights is not None and any(np.ndim(w) for w in weights):
+            return None
+        try:
+            dts = {np.asarray(a).dtype for ll in layer_lists for a in ll}
+        except Exception:  # noqa: BLE001 - ragged or exotic payloads: the general path decides
+            return None
+        if len(dts) != 1:
+            return None
+        xt = dts.pop()
+        if xt not in _NP2T or n * xt.itemsize > SMALL_CALL_BYTES:
+            return None
+        cts = {_compute_dtype(xt, None if weights is None else weights[i], self._fxp_bits) for i in range(C)}
+        if len(cts) != 1:
+            return None
+        ct = cts.pop()
+        if ct not in _NP2T:
+            return None
+        names = [d.device.party for d in data]
+        ws = [1.0 if weights is None else (float(w) if ct.kind == "f" else int(w)) for w in (weights or [None] * C)]
+        streams = [self._maskers[nm].streams(self._maskers[nm].peers) for nm in names]
+        xs = [np.asarray(ll[0]).reshape(-1) if len(ll) == 1 else
+              np.concatenate([np.asarray(a).reshape(-1) for a in ll]) for ll in layer_lists]
+        sdev = self._device.torch_device
+        key = (C, n, xt.itemsize, str(sdev))
+        sc = getattr(self, "_general_call", None)
+        if sc is None or sc[0] != key:
+            pin_b, dev_b = K.host_clients_scratch(C, n, xt.itemsize)
+            sc = (key, torch.empty(pin_b, dtype=torch.uint8, pin_memory=True),
+                  torch.empty(dev_b, dtype=torch.uint8, device=sdev))
+            self._general_call = sc
+        divisor = 1.0
+        if average:
+            divisor = float(C) if weights is None else float(sum(weights))
+        with torch.cuda.device(sdev):
+            out, digests, flag = K.clients_host(xs, ct, ws, streams, sc[1], sc[2], fxp_bits=self._fxp_bits,
+                                                divisor=divisor)
         if flag & L.SA_FLAG_PRG_REJECT:
             raise _Rejected()
         for nm in names:
