@@ -201,6 +201,32 @@ int sa_clients_host(const void* const* host_x, int x_type, int compute_type, con
                     int n_clients, uint64_t n, int fxp_bits, const sa_mask_stream* streams, double divisor,
                     void* pinned, void* dev, double* out, uint64_t* digests, uint32_t* flags, void* stream);
 
+/* The per-party drop-in's two device steps for small host payloads, each as
+ * ONE blocking call (sfl_amd/security/aggregation/party.py; the reference's
+ * `_Masker.mask` inside the participant and the server's `_sum` + decode,
+ * secure_aggregation.ipynb:227-239, sparse_plain_aggregator.py:86-94).
+ *
+ * sa_mask_host: one party's masked vector.  Copies host_x (n elements of
+ * x_type) into `pinned`, one host-to-device copy, zeroes the flag word,
+ * sa_mask with `streams`, one device-to-host copy of the masked vector and
+ * the flag word, synchronises, fills out[n] (host) and *flags.  n_pad = n
+ * rounded up to a multiple of 4, xs = element size:
+ *   pinned >= n_pad*xs + (n_pad + 2)*8 bytes, page-locked;  dev >= n_pad*xs + (n_pad + 2)*8 bytes. */
+int sa_mask_host(const void* host_x, int x_type, int compute_type, uint64_t n, double weight, int fxp_bits,
+                 const sa_mask_stream* streams, int n_streams, void* pinned, void* dev, uint64_t* out,
+                 uint32_t* flags, void* stream);
+
+/* sa_sum_decode_host: the server's step.  Copies the n_clients host masked
+ * vectors into `pinned`, one host-to-device copy, each vector's XOR digest,
+ * their sum mod 2^64, decode by `divisor`, one device-to-host copy of the
+ * result and the digests, synchronises, fills out[n] and digests[n_clients]
+ * (host; the caller compares them with the digests the parties sent).
+ *   pinned >= n_clients*n_pad*8 + (n_pad + n_clients)*8 bytes, page-locked;
+ *   dev    >= n_clients*n_pad*8 + n_pad*8 + (n_pad + n_clients)*8 bytes;
+ * 1..32 vectors, both buffers 16-byte aligned. */
+int sa_sum_decode_host(const uint64_t* const* host_masked, int n_clients, uint64_t n, int fxp_bits, double divisor,
+                       void* pinned, void* dev, double* out, uint64_t* digests, void* stream);
+
 /* One block of the pair-shared schedule for MORE co-located clients than one
  * sa_fused_clients launch holds (more than 8): the 8 slots are two quads of
  * clients, (0-3) and (4-7), and the launch expands only the 16 streams of the

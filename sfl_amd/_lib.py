@@ -30,7 +30,7 @@ TUNING_ABI_OFFSET = 1000  # sa_abi_version() of an SA_ABLATE / SA_TIMING build
 # every symbol include/sfl_sa.h declares (checked by tests/test_boundary.py)
 EXPORTED = (
     "sa_abi_version", "sa_last_error", "sa_pcg64_from_seed", "sa_pcg64_advance",
-    "sa_pcg64_raw_host", "sa_mask", "sa_fused_clients", "sa_fused_clients_host_f32", "sa_clients_host", "sa_fused_bipartite", "sa_set_masking_reserve", "sa_sum_u64", "sa_decode",
+    "sa_pcg64_raw_host", "sa_mask", "sa_fused_clients", "sa_fused_clients_host_f32", "sa_clients_host", "sa_mask_host", "sa_sum_decode_host", "sa_fused_bipartite", "sa_set_masking_reserve", "sa_sum_u64", "sa_decode",
     "sa_sum_f64", "sa_comm_unique_id", "sa_comm_init", "sa_comm_reduce_u64",
     "sa_comm_allreduce_u64", "sa_comm_reduce_scatter_u64", "sa_comm_alltoall_u64", "sa_comm_gather_f64", "sa_comm_destroy", "sa_sumsq_f32", "sa_dp_perturb_f32", "sa_mask_dp",
     "sa_pcg64_find_zero", "sa_stream_shift", "sa_xor_u64",
@@ -98,6 +98,8 @@ def _declare(lib):
                                               dbl, vp, vp, vp, vp, P(C.c_uint32), vp]
     lib.sa_clients_host.argtypes = [P(C.c_void_p), i32, i32, P(C.c_double), i32, u64, i32, P(MaskStream), dbl,
                                     vp, vp, vp, vp, P(C.c_uint32), vp]
+    lib.sa_mask_host.argtypes = [vp, i32, i32, u64, dbl, i32, P(MaskStream), i32, vp, vp, vp, P(C.c_uint32), vp]
+    lib.sa_sum_decode_host.argtypes = [P(C.c_void_p), i32, u64, i32, dbl, vp, vp, vp, vp, vp]
     lib.sa_fused_bipartite.argtypes = [P(LocalClient), i32, u64, i32, P(PCG64), P(C.c_int8), vp, i32, vp, vp]
     lib.sa_set_masking_reserve.argtypes = [i32]
     lib.sa_sum_u64.argtypes = [P(C.c_void_p), i32, u64, vp, vp]

@@ -788,3 +788,73 @@ extern "C" int sa_clients_host(const void* const* host_x, int x_type, int comput
   memcpy(digests, pin_io + n_pad + 1, C * 8);
   return SA_OK;
 }
+
+extern "C" int sa_mask_host(const void* host_x, int x_type, int compute_type, uint64_t n, double weight,
+                            int fxp_bits, const sa_mask_stream* streams, int n_streams, void* pinned, void* dev,
+                            uint64_t* out, uint32_t* flags, void* stream) {
+  if (check_type(x_type, "sa_mask_host x_type") || check_type(compute_type, "sa_mask_host compute_type"))
+    return SA_ERR_ARG;
+  if (!host_x || n == 0 || n_streams < 0 || (n_streams > 0 && !streams) || !pinned || !dev || !out || !flags ||
+      ((uintptr_t)pinned & 15) || ((uintptr_t)dev & 15)) {
+    sa_set_error("sa_mask_host: bad arguments (n > 0, 16-byte aligned buffers)");
+    return SA_ERR_ARG;
+  }
+  const uint64_t n_pad = (n + 3) & ~3ull, xs = x_type == SA_F32 ? 4 : 8;
+  char* pin_in = (char*)pinned;
+  uint64_t* pin_out = (uint64_t*)(pin_in + n_pad * xs);  // masked vector | flag word
+  char* d_in = (char*)dev;
+  uint64_t* d_out = (uint64_t*)(d_in + n_pad * xs);
+  const hipStream_t s = (hipStream_t)stream;
+  memcpy(pin_in, host_x, n * xs);
+  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, n * xs, hipMemcpyHostToDevice, s));
+  SA_HIP_CHECK(hipMemsetAsync(d_out + n_pad, 0, 8, s));
+  const int rc = sa_mask(d_in, x_type, compute_type, n, weight, nullptr, fxp_bits, streams, n_streams, d_out,
+                         nullptr, nullptr, (uint32_t*)(d_out + n_pad), stream);
+  if (rc) return rc;
+  SA_HIP_CHECK(hipMemcpyAsync(pin_out, d_out, (n_pad + 1) * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK(hipStreamSynchronize(s));
+  memcpy(out, pin_out, n * 8);
+  *flags = (uint32_t)pin_out[n_pad];
+  return SA_OK;
+}
+
+extern "C" int sa_sum_decode_host(const uint64_t* const* host_masked, int n_clients, uint64_t n, int fxp_bits,
+                                  double divisor, void* pinned, void* dev, double* out, uint64_t* digests,
+                                  void* stream) {
+  if (!host_masked || n_clients < 1 || n_clients > kSumMaxIn || n == 0 || !pinned || !dev || !out || !digests ||
+      ((uintptr_t)pinned & 15) || ((uintptr_t)dev & 15)) {
+    sa_set_error("sa_sum_decode_host: bad arguments (1..%d vectors, n > 0, 16-byte aligned buffers)", kSumMaxIn);
+    return SA_ERR_ARG;
+  }
+  for (int c = 0; c < n_clients; c++)
+    if (!host_masked[c]) {
+      sa_set_error("sa_sum_decode_host: host_masked[%d] is NULL", c);
+      return SA_ERR_ARG;
+    }
+  const uint64_t C = (uint64_t)n_clients, n_pad = (n + 3) & ~3ull;
+  uint64_t* pin_in = (uint64_t*)pinned;
+  double* pin_io = (double*)(pin_in + C * n_pad);  // result | digests
+  uint64_t* d_in = (uint64_t*)dev;
+  uint64_t* d_sum = d_in + C * n_pad;
+  double* d_io = (double*)(d_sum + n_pad);
+  uint64_t* d_dig = (uint64_t*)(d_io + n_pad);
+  const hipStream_t s = (hipStream_t)stream;
+  for (uint64_t c = 0; c < C; c++) memcpy(pin_in + c * n_pad, host_masked[c], n * 8);
+  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * 8, hipMemcpyHostToDevice, s));
+  SA_HIP_CHECK(hipMemsetAsync(d_dig, 0, C * 8, s));
+  const uint64_t* ins[kSumMaxIn];
+  for (uint64_t c = 0; c < C; c++) {
+    ins[c] = d_in + c * n_pad;
+    const int rc = sa_xor_u64(ins[c], n, d_dig + c, stream);
+    if (rc) return rc;
+  }
+  int rc = sa_sum_u64(ins, n_clients, n, d_sum, stream);
+  if (rc) return rc;
+  rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_io, stream);
+  if (rc) return rc;
+  SA_HIP_CHECK(hipMemcpyAsync(pin_io, d_io, (n_pad + C) * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK(hipStreamSynchronize(s));
+  memcpy(out, pin_io, n * 8);
+  memcpy(digests, pin_io + n_pad, C * 8);
+  return SA_OK;
+}

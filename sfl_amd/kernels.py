@@ -320,6 +320,62 @@ def clients_host(xs: Sequence[np.ndarray], compute_dtype, weights: Sequence[floa
     return out, digests, int(flags.value)
 
 
+def _scratch(pinned: torch.Tensor, dev: torch.Tensor, need_pin: int, need_dev: int) -> None:
+    _require_gpu(dev)
+    if not pinned.is_pinned() or pinned.numel() < need_pin or dev.numel() < need_dev:
+        raise ValueError("scratch buffers too small or not page-locked")
+
+
+def mask_host_scratch(n: int, itemsize: int) -> tuple[int, int]:
+    """(pinned bytes, device bytes) sa_mask_host needs."""
+    n_pad = -(-n // 4) * 4
+    return n_pad * itemsize + (n_pad + 2) * 8, n_pad * itemsize + (n_pad + 2) * 8
+
+
+def mask_host(x: np.ndarray, compute_dtype, streams: Sequence[tuple], pinned: torch.Tensor, dev: torch.Tensor, *,
+              weight: float = 1.0, fxp_bits: int = 18):
+    """One party's masked vector from a host array in ONE blocking call
+    (sa_mask_host in include/sfl_sa.h) -> (uint64 host array, flag word)."""
+    a = np.ascontiguousarray(x).reshape(-1)
+    if a.dtype not in _NP_XTYPE:
+        raise ValueError("mask_host takes float32 / float64 / int64 host arrays")
+    n = int(a.size)
+    _scratch(pinned, dev, *mask_host_scratch(n, a.dtype.itemsize))
+    sarr = make_streams(streams)
+    out = np.empty(n, dtype=np.uint64)
+    flags = C.c_uint32(0)
+    L.check(L.lib().sa_mask_host(C.c_void_p(a.ctypes.data), _NP_XTYPE[a.dtype], _NP_XTYPE[np.dtype(compute_dtype)],
+                                 n, float(weight), int(fxp_bits), sarr, len(streams), _ptr(pinned), _ptr(dev),
+                                 C.c_void_p(out.ctypes.data), C.byref(flags), C.c_void_p(_stream(dev))),
+            "sa_mask_host")
+    return out, int(flags.value)
+
+
+def sum_decode_host_scratch(n_clients: int, n: int) -> tuple[int, int]:
+    """(pinned bytes, device bytes) sa_sum_decode_host needs."""
+    n_pad = -(-n // 4) * 4
+    return n_clients * n_pad * 8 + (n_pad + n_clients) * 8, (n_clients + 1) * n_pad * 8 + (n_pad + n_clients) * 8
+
+
+def sum_decode_host(masked: Sequence[np.ndarray], pinned: torch.Tensor, dev: torch.Tensor, *, fxp_bits: int = 18,
+                    divisor: float = 1.0):
+    """The server's step on host masked vectors in ONE blocking call
+    (sa_sum_decode_host in include/sfl_sa.h) -> (decoded float64 host array,
+    uint64 digests as received)."""
+    arrs = [np.ascontiguousarray(m).view(np.uint64).reshape(-1) for m in masked]
+    nc, n = len(arrs), int(arrs[0].size)
+    if any(a.size != n for a in arrs):
+        raise ValueError("masked vectors of different sizes")
+    _scratch(pinned, dev, *sum_decode_host_scratch(nc, n))
+    ptrs = (C.c_void_p * nc)(*[a.ctypes.data for a in arrs])
+    out = np.empty(n, dtype=np.float64)
+    digests = np.empty(nc, dtype=np.uint64)
+    L.check(L.lib().sa_sum_decode_host(ptrs, nc, n, int(fxp_bits), float(divisor), _ptr(pinned), _ptr(dev),
+                                       C.c_void_p(out.ctypes.data), C.c_void_p(digests.ctypes.data),
+                                       C.c_void_p(_stream(dev))), "sa_sum_decode_host")
+    return out, digests
+
+
 def sum_f64(ins: Sequence[torch.Tensor], out: torch.Tensor) -> torch.Tensor:
     _require_gpu(out, *ins)
     ptrs = (C.c_void_p * len(ins))(*[t.data_ptr() for t in ins])

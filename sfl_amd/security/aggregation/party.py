@@ -28,6 +28,7 @@ spawned process per party.
 
 from __future__ import annotations
 
+import threading
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -54,6 +55,25 @@ class MaskedPayload:
     digest: int
     fxp_bits: int
     positions: dict = field(default_factory=dict)  # peer -> stream position the round started at
+
+
+# scratch of the blocking small-call library entries (sa_mask_host,
+# sa_sum_decode_host), per GPU of this process, grown to the largest call
+_SCRATCH: dict = {}
+_SCRATCH_LOCK = threading.Lock()
+
+
+def _scratch(gpu: int, pin_bytes: int, dev_bytes: int):
+    import torch
+
+    cur = _SCRATCH.get(gpu)
+    if cur is None or cur[0].numel() < pin_bytes or cur[1].numel() < dev_bytes:
+        pb = max(pin_bytes, cur[0].numel() if cur else 0)
+        db = max(dev_bytes, cur[1].numel() if cur else 0)
+        cur = (torch.empty(pb, dtype=torch.uint8, pin_memory=True),
+               torch.empty(db, dtype=torch.uint8, device=torch.device("cuda", gpu)))
+        _SCRATCH[gpu] = cur
+    return cur
 
 
 # --------------------------------------------------------------- key set-up
@@ -205,6 +225,17 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
     tdt = {_F32: torch.float32, _F64: torch.float64, _I64: torch.int64}
     n = int(sum(int(np.prod(_shape_of(a))) for a in xs))
     small = 8 * n <= SMALL_CALL_BYTES
+    streams = masker.streams()
+    if small and wvec is None and not any(isinstance(a, torch.Tensor) for a in xs):
+        # host layers of a small payload: ONE blocking library call
+        flat = (np.asarray(xs[0], dtype=xt).reshape(-1) if len(xs) == 1 else
+                np.concatenate([np.asarray(a, dtype=xt).reshape(-1) for a in xs]))
+        with _SCRATCH_LOCK, torch.cuda.device(dev):
+            pin, dbuf = _scratch(gpu, *K.mask_host_scratch(n, xt.itemsize))
+            host, flag = K.mask_host(flat, ct, streams, pin, dbuf, weight=wscalar, fxp_bits=masker.fxp_bits)
+        if not flag & L.SA_FLAG_PRG_REJECT:
+            return host, {}
+        # numpy's rejection of a raw 0 (p = 2^-64 a draw): the device path below re-positions the streams
     with torch.cuda.device(dev):
         if not any(isinstance(a, torch.Tensor) for a in xs):
             # host layers (FedAvgW's get_weights payloads): packed on the host, ONE H2D copy
@@ -234,7 +265,6 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
         out = buf[:n]
         flags = buf[n:].view(torch.int32)[:1]
         buf[n:].zero_()
-        streams = masker.streams()
         K.mask(x, out, streams, weight=wscalar, weight_vec=wv, compute_dtype=tdt[ct],
                fxp_bits=masker.fxp_bits, flags=flags)
         if small:
@@ -324,6 +354,15 @@ def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_t
     dev = torch.device("cuda", gpu)
     n, C = int(u64s[0].size), len(u64s)
     small = 8 * n <= SMALL_CALL_BYTES
+    if small and n and not as_torch and divisor_vec is None and C <= 32:
+        # ONE blocking library call: the vectors in, digests, sum, decode, the result out
+        with _SCRATCH_LOCK, torch.cuda.device(dev):
+            pin, dbuf = _scratch(gpu, *K.sum_decode_host_scratch(C, n))
+            result, got = K.sum_decode_host(u64s, pin, dbuf, fxp_bits=fxp_bits, divisor=divisor)
+        for i, (g, want) in enumerate(zip(got.tolist(), digests)):
+            if int(g) != int(want) & ((1 << 64) - 1):
+                raise DigestMismatch(f"masked vector {i}: digest {int(g):016x}, sent {int(want):016x}")
+        return result
     with torch.cuda.device(dev):
         if small and n:
             n_pad = n + (n & 1)  # rows 16-byte aligned

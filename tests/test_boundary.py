@@ -94,6 +94,8 @@ def test_every_entry_point_validates_before_touching_the_gpu():
                                                                            None, None, None, None, None, None),
         "sa_clients_host": lambda: lib.sa_clients_host(None, 2, 2, None, 2, 10, 18, None, 1.0, None, None, None,
                                                        None, None, None),
+        "sa_mask_host": lambda: lib.sa_mask_host(None, 0, 0, 10, 1.0, 18, None, 0, None, None, None, None, None),
+        "sa_sum_decode_host": lambda: lib.sa_sum_decode_host(None, 2, 10, 18, 1.0, None, None, None, None, None),
         "sa_sum_f64": lambda: lib.sa_sum_f64(None, 0, 10, None, None),
         "sa_pcg64_find_zero": lambda: lib.sa_pcg64_find_zero(None, 1, 10, None, None),
         "sa_stream_shift": lambda: lib.sa_stream_shift(None, 10, None, 1, 0, 1, None),
