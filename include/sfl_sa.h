@@ -14,7 +14,9 @@
  *  - device buffers are caller-owned; launches are asynchronous and ordered
  *    on the caller's hipStream_t (passed as void*; NULL = legacy stream).
  *  - the launch functions never allocate, copy or synchronise, so they can be
- *    captured into a hipGraph.  Re-entrant per stream.
+ *    captured into a hipGraph.  Re-entrant per stream.  The four *_host
+ *    entries are the exception: blocking calls on host arrays for small
+ *    payloads (they copy and synchronise, but allocate nothing either).
  *  - n == 0 is a no-op that returns SA_OK; the vector pointers of an empty
  *    call may be NULL (an empty framework tensor has no storage).
  *  - mask-stream generator states are numpy PCG64 states (state, inc) as
@@ -163,15 +165,17 @@ int sa_fused_clients(const sa_local_client* clients, int n_clients, int x_type, 
  * the small-call path of `SecureAggregator.sum` / `.average` on host arrays
  * (FL rounds of small models, HomoBinning's
  * counts), where per-call latency, not bandwidth, decides.  Copies the
- * n_clients host vectors into `pinned`, ONE host-to-device copy, zeroes the
- * flag + digest words, sa_fused_clients (masked_out NULL, no cross streams),
+ * n_clients host vectors into `pinned`, ONE host-to-device copy (inputs and
+ * zeroed flag + digest words), sa_fused_clients (masked_out NULL, no cross streams),
  * sa_decode by `divisor`, ONE device-to-host copy of result + flag word +
- * digests, synchronises `stream`, then fills the outputs.  With n_pad = n
- * rounded up to a multiple of 4, the caller owns (nothing is allocated):
- *   pinned  >= n_clients*n_pad*4 + (n_pad + 1 + n_clients)*8 bytes of
- *           page-locked host memory, 16-byte aligned;
- *   dev     >= n_clients*n_pad*4 + n_pad*8 + (n_pad + 1 + n_clients)*8
- *           bytes of device memory, 16-byte aligned.
+ * digests, synchronises `stream`, then fills the outputs (the zeroed flag
+ * and digest words ride the host-to-device copy: no fill operation).  With
+ * n_pad = n rounded up to a multiple of 4 and M = 1 + n_clients rounded up
+ * to even, the caller owns (nothing is allocated):
+ *   pinned  >= n_clients*n_pad*4 + (M + n_pad)*8 bytes of page-locked host
+ *           memory, 16-byte aligned;
+ *   dev     >= n_clients*n_pad*4 + (M + 2*n_pad)*8 bytes of device memory,
+ *           16-byte aligned.
  * Outputs (host): out[n] the decoded float64, digests[n_clients] the masked
  * vectors' XOR digests, *flags the PRG flag word (SA_FLAG_PRG_REJECT: the
  * caller replays the round as after sa_fused_clients).  2..8 clients.
@@ -190,9 +194,10 @@ int sa_fused_clients_host_f32(const float* const* host_x, const double* weights,
  * sum, then sa_decode.  `streams`: n_clients * (n_clients - 1) entries,
  * client-major (client c's peers in its masker's order); `weights` are the
  * scalar weights as sa_mask takes them.  With n_pad = n rounded up to a
- * multiple of 4 and xs the element size of x_type:
- *   pinned >= n_clients*n_pad*xs + (n_pad + 1 + n_clients)*8 bytes, page-locked;
- *   dev    >= n_clients*n_pad*(xs + 8) + n_pad*8 + (n_pad + 1 + n_clients)*8 bytes;
+ * multiple of 4, xs the element size of x_type and M = 1 + n_clients
+ * rounded up to even:
+ *   pinned >= n_clients*n_pad*xs + (2*n_pad + M)*8 bytes, page-locked;
+ *   dev    >= n_clients*n_pad*(xs + 8) + (2*n_pad + M)*8 bytes;
  * both 16-byte aligned.  2..9 clients.  Outputs as for
  * sa_fused_clients_host_f32.  Replaces, for co-located parties with small
  * integer / float64 vectors (HomoBinning's counts),
@@ -211,7 +216,7 @@ int sa_clients_host(const void* const* host_x, int x_type, int compute_type, con
  * sa_mask with `streams`, one device-to-host copy of the masked vector and
  * the flag word, synchronises, fills out[n] (host) and *flags.  n_pad = n
  * rounded up to a multiple of 4, xs = element size:
- *   pinned >= n_pad*xs + (n_pad + 2)*8 bytes, page-locked;  dev >= n_pad*xs + (n_pad + 2)*8 bytes. */
+ *   pinned >= n_pad*xs + (2 + n_pad)*8 bytes, page-locked;  dev >= the same. */
 int sa_mask_host(const void* host_x, int x_type, int compute_type, uint64_t n, double weight, int fxp_bits,
                  const sa_mask_stream* streams, int n_streams, void* pinned, void* dev, uint64_t* out,
                  uint32_t* flags, void* stream);
@@ -221,8 +226,9 @@ int sa_mask_host(const void* host_x, int x_type, int compute_type, uint64_t n, d
  * their sum mod 2^64, decode by `divisor`, one device-to-host copy of the
  * result and the digests, synchronises, fills out[n] and digests[n_clients]
  * (host; the caller compares them with the digests the parties sent).
- *   pinned >= n_clients*n_pad*8 + (n_pad + n_clients)*8 bytes, page-locked;
- *   dev    >= n_clients*n_pad*8 + n_pad*8 + (n_pad + n_clients)*8 bytes;
+ * With M = n_clients rounded up to even:
+ *   pinned >= (n_clients*n_pad + M + n_pad)*8 bytes, page-locked;
+ *   dev    >= (n_clients*n_pad + M + 2*n_pad)*8 bytes;
  * 1..32 vectors, both buffers 16-byte aligned. */
 int sa_sum_decode_host(const uint64_t* const* host_masked, int n_clients, uint64_t n, int fxp_bits, double divisor,
                        void* pinned, void* dev, double* out, uint64_t* digests, void* stream);

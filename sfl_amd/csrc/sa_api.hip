@@ -697,6 +697,14 @@ extern "C" int sa_sum_f64(const double* const* w, int k, uint64_t n, double* out
   return SA_OK;
 }
 
+// The blocking small-call entries below lay their buffers out so that the
+// words the kernels accumulate into (PRG flag, digests, and for
+// sa_clients_host the masked sum) ride the one host-to-device copy as zeros
+// -- no separate fill -- and the words read back sit right before the
+// result, so one device-to-host copy brings everything (a small call is
+// bound by its number of device operations).
+static inline uint64_t even_words(uint64_t w) { return (w + 1) & ~1ull; }
+
 extern "C" int sa_fused_clients_host_f32(const float* const* host_x, const double* weights, int n_clients,
                                          uint64_t n, int fxp_bits, const sa_pcg64* pair_gens,
                                          const int8_t* pair_sign, double divisor, void* pinned, void* dev,
@@ -711,16 +719,19 @@ extern "C" int sa_fused_clients_host_f32(const float* const* host_x, const doubl
       sa_set_error("sa_fused_clients_host_f32: host_x[%d] is NULL", c);
       return SA_ERR_ARG;
     }
-  const uint64_t C = (uint64_t)n_clients, n_pad = (n + 3) & ~3ull;
+  const uint64_t C = (uint64_t)n_clients, n_pad = (n + 3) & ~3ull, M = even_words(1 + C);
+  // host and device: [inputs C x n_pad f32 | meta M words: flag, digests | result n_pad f64] (+ device: sum)
   float* pin_in = (float*)pinned;
-  double* pin_io = (double*)((char*)pinned + C * n_pad * 4);
+  uint64_t* pin_meta = (uint64_t*)(pin_in + C * n_pad);
+  double* pin_res = (double*)(pin_meta + M);
   float* d_in = (float*)dev;
-  uint64_t* d_sum = (uint64_t*)((char*)dev + C * n_pad * 4);
-  double* d_io = (double*)((char*)d_sum + n_pad * 8);  // result | flag word | digests
+  uint64_t* d_meta = (uint64_t*)(d_in + C * n_pad);
+  double* d_res = (double*)(d_meta + M);
+  uint64_t* d_sum = (uint64_t*)(d_res + n_pad);
   const hipStream_t s = (hipStream_t)stream;
   for (uint64_t c = 0; c < C; c++) memcpy(pin_in + c * n_pad, host_x[c], n * 4);
-  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * 4, hipMemcpyHostToDevice, s));
-  SA_HIP_CHECK(hipMemsetAsync(d_io + n_pad, 0, (1 + C) * 8, s));
+  memset(pin_meta, 0, M * 8);
+  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * 4 + M * 8, hipMemcpyHostToDevice, s));
   sa_local_client cl[8];
   for (uint64_t c = 0; c < C; c++) {
     cl[c].x = d_in + c * n_pad;
@@ -728,17 +739,15 @@ extern "C" int sa_fused_clients_host_f32(const float* const* host_x, const doubl
     cl[c].masked_out = nullptr;
   }
   int rc = sa_fused_clients(cl, n_clients, SA_F32, n, fxp_bits, pair_gens, pair_sign, nullptr, 0, d_sum, 0,
-                            (uint64_t*)(d_io + n_pad + 1), (uint32_t*)(d_io + n_pad), stream);
+                            d_meta + 1, (uint32_t*)d_meta, stream);
   if (rc) return rc;
-  rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_io, stream);
+  rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_res, stream);
   if (rc) return rc;
-  SA_HIP_CHECK(hipMemcpyAsync(pin_io, d_io, (n_pad + 1 + C) * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK(hipMemcpyAsync(pin_meta, d_meta, (M + n_pad) * 8, hipMemcpyDeviceToHost, s));
   SA_HIP_CHECK(hipStreamSynchronize(s));
-  memcpy(out, pin_io, n * 8);
-  uint64_t word;
-  memcpy(&word, pin_io + n_pad, 8);
-  *flags = (uint32_t)word;  // the flag word's low half (little-endian)
-  memcpy(digests, pin_io + n_pad + 1, C * 8);
+  memcpy(out, pin_res, n * 8);
+  *flags = (uint32_t)pin_meta[0];  // the flag word's low half (little-endian)
+  memcpy(digests, pin_meta + 1, C * 8);
   return SA_OK;
 }
 
@@ -759,33 +768,41 @@ extern "C" int sa_clients_host(const void* const* host_x, int x_type, int comput
       return SA_ERR_ARG;
     }
   const uint64_t C = (uint64_t)n_clients, n_pad = (n + 3) & ~3ull, xs = x_type == SA_F32 ? 4 : 8;
+  const uint64_t M = even_words(1 + C);
+  // host and device: [inputs | sum n_pad u64 | meta M words: flag, digests | result n_pad f64] (+ device:
+  // the masked vectors); a sum of up to 16 KiB rides the copy as zeros, a larger one is filled on the device
+  const bool zero_by_copy = n_pad * 8 <= (16u << 10);
   char* pin_in = (char*)pinned;
-  double* pin_io = (double*)(pin_in + C * n_pad * xs);
+  uint64_t* pin_sum = (uint64_t*)(pin_in + C * n_pad * xs);
+  uint64_t* pin_meta = pin_sum + n_pad;
+  double* pin_res = (double*)(pin_meta + M);
   char* d_in = (char*)dev;
-  uint64_t* d_masked = (uint64_t*)(d_in + C * n_pad * xs);
-  uint64_t* d_sum = d_masked + C * n_pad;
-  double* d_io = (double*)(d_sum + n_pad);  // result | flag word | digests, right behind the sum
+  uint64_t* d_sum = (uint64_t*)(d_in + C * n_pad * xs);
+  uint64_t* d_meta = d_sum + n_pad;
+  double* d_res = (double*)(d_meta + M);
+  uint64_t* d_masked = (uint64_t*)(d_res + n_pad);
   const hipStream_t s = (hipStream_t)stream;
   for (uint64_t c = 0; c < C; c++) memcpy(pin_in + c * n_pad * xs, host_x[c], n * xs);
-  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * xs, hipMemcpyHostToDevice, s));
-  SA_HIP_CHECK(hipMemsetAsync(d_sum, 0, n_pad * 8 + (n_pad + 1 + C) * 8, s));  // sum, flag word, digests
-  uint32_t* d_flags = (uint32_t*)(d_io + n_pad);
-  uint64_t* d_dig = (uint64_t*)(d_io + n_pad + 1);
+  if (zero_by_copy) {
+    memset(pin_sum, 0, (n_pad + M) * 8);
+    SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * xs + (n_pad + M) * 8, hipMemcpyHostToDevice, s));
+  } else {
+    SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * xs, hipMemcpyHostToDevice, s));
+    SA_HIP_CHECK(hipMemsetAsync(d_sum, 0, (n_pad + M) * 8, s));
+  }
   for (uint64_t c = 0; c < C; c++) {
     const int rc = sa_mask(d_in + c * n_pad * xs, x_type, compute_type, n, weights[c], nullptr, fxp_bits,
-                           streams + c * (C - 1), n_clients - 1, d_masked + c * n_pad, d_sum, d_dig + c, d_flags,
-                           stream);
+                           streams + c * (C - 1), n_clients - 1, d_masked + c * n_pad, d_sum, d_meta + 1 + c,
+                           (uint32_t*)d_meta, stream);
     if (rc) return rc;
   }
-  const int rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_io, stream);
+  const int rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_res, stream);
   if (rc) return rc;
-  SA_HIP_CHECK(hipMemcpyAsync(pin_io, d_io, (n_pad + 1 + C) * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK(hipMemcpyAsync(pin_meta, d_meta, (M + n_pad) * 8, hipMemcpyDeviceToHost, s));
   SA_HIP_CHECK(hipStreamSynchronize(s));
-  memcpy(out, pin_io, n * 8);
-  uint64_t word;
-  memcpy(&word, pin_io + n_pad, 8);
-  *flags = (uint32_t)word;
-  memcpy(digests, pin_io + n_pad + 1, C * 8);
+  memcpy(out, pin_res, n * 8);
+  *flags = (uint32_t)pin_meta[0];
+  memcpy(digests, pin_meta + 1, C * 8);
   return SA_OK;
 }
 
@@ -800,21 +817,23 @@ extern "C" int sa_mask_host(const void* host_x, int x_type, int compute_type, ui
     return SA_ERR_ARG;
   }
   const uint64_t n_pad = (n + 3) & ~3ull, xs = x_type == SA_F32 ? 4 : 8;
+  // host and device: [input n_pad | flag word + pad (2 words) | masked vector n_pad u64]
   char* pin_in = (char*)pinned;
-  uint64_t* pin_out = (uint64_t*)(pin_in + n_pad * xs);  // masked vector | flag word
+  uint64_t* pin_flag = (uint64_t*)(pin_in + n_pad * xs);
   char* d_in = (char*)dev;
-  uint64_t* d_out = (uint64_t*)(d_in + n_pad * xs);
+  uint64_t* d_flag = (uint64_t*)(d_in + n_pad * xs);
+  uint64_t* d_out = d_flag + 2;
   const hipStream_t s = (hipStream_t)stream;
   memcpy(pin_in, host_x, n * xs);
-  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, n * xs, hipMemcpyHostToDevice, s));
-  SA_HIP_CHECK(hipMemsetAsync(d_out + n_pad, 0, 8, s));
+  pin_flag[0] = pin_flag[1] = 0;
+  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, n_pad * xs + 16, hipMemcpyHostToDevice, s));
   const int rc = sa_mask(d_in, x_type, compute_type, n, weight, nullptr, fxp_bits, streams, n_streams, d_out,
-                         nullptr, nullptr, (uint32_t*)(d_out + n_pad), stream);
+                         nullptr, nullptr, (uint32_t*)d_flag, stream);
   if (rc) return rc;
-  SA_HIP_CHECK(hipMemcpyAsync(pin_out, d_out, (n_pad + 1) * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK(hipMemcpyAsync(pin_flag, d_flag, 16 + n * 8, hipMemcpyDeviceToHost, s));
   SA_HIP_CHECK(hipStreamSynchronize(s));
-  memcpy(out, pin_out, n * 8);
-  *flags = (uint32_t)pin_out[n_pad];
+  memcpy(out, pin_flag + 2, n * 8);
+  *flags = (uint32_t)pin_flag[0];
   return SA_OK;
 }
 
@@ -831,17 +850,19 @@ extern "C" int sa_sum_decode_host(const uint64_t* const* host_masked, int n_clie
       sa_set_error("sa_sum_decode_host: host_masked[%d] is NULL", c);
       return SA_ERR_ARG;
     }
-  const uint64_t C = (uint64_t)n_clients, n_pad = (n + 3) & ~3ull;
+  const uint64_t C = (uint64_t)n_clients, n_pad = (n + 3) & ~3ull, M = even_words(C);
+  // host and device: [masked vectors C x n_pad | digests M words | result n_pad f64] (+ device: sum)
   uint64_t* pin_in = (uint64_t*)pinned;
-  double* pin_io = (double*)(pin_in + C * n_pad);  // result | digests
+  uint64_t* pin_dig = pin_in + C * n_pad;
+  double* pin_res = (double*)(pin_dig + M);
   uint64_t* d_in = (uint64_t*)dev;
-  uint64_t* d_sum = d_in + C * n_pad;
-  double* d_io = (double*)(d_sum + n_pad);
-  uint64_t* d_dig = (uint64_t*)(d_io + n_pad);
+  uint64_t* d_dig = d_in + C * n_pad;
+  double* d_res = (double*)(d_dig + M);
+  uint64_t* d_sum = (uint64_t*)(d_res + n_pad);
   const hipStream_t s = (hipStream_t)stream;
   for (uint64_t c = 0; c < C; c++) memcpy(pin_in + c * n_pad, host_masked[c], n * 8);
-  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * 8, hipMemcpyHostToDevice, s));
-  SA_HIP_CHECK(hipMemsetAsync(d_dig, 0, C * 8, s));
+  memset(pin_dig, 0, M * 8);
+  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, (C * n_pad + M) * 8, hipMemcpyHostToDevice, s));
   const uint64_t* ins[kSumMaxIn];
   for (uint64_t c = 0; c < C; c++) {
     ins[c] = d_in + c * n_pad;
@@ -850,11 +871,11 @@ extern "C" int sa_sum_decode_host(const uint64_t* const* host_masked, int n_clie
   }
   int rc = sa_sum_u64(ins, n_clients, n, d_sum, stream);
   if (rc) return rc;
-  rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_io, stream);
+  rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_res, stream);
   if (rc) return rc;
-  SA_HIP_CHECK(hipMemcpyAsync(pin_io, d_io, (n_pad + C) * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK(hipMemcpyAsync(pin_dig, d_dig, (M + n) * 8, hipMemcpyDeviceToHost, s));
   SA_HIP_CHECK(hipStreamSynchronize(s));
-  memcpy(out, pin_io, n * 8);
-  memcpy(digests, pin_io + n_pad, C * 8);
+  memcpy(out, pin_res, n * 8);
+  memcpy(digests, pin_dig, C * 8);
   return SA_OK;
 }

@@ -239,9 +239,9 @@ def decode(s: torch.Tensor, out: torch.Tensor, *, fxp_bits: int = 18, divisor: f
 
 def host_fused_scratch(n_clients: int, n: int) -> tuple[int, int]:
     """(pinned bytes, device bytes) sa_fused_clients_host_f32 needs."""
-    n_pad = -(-n // 4) * 4
-    io = (n_pad + 1 + n_clients) * 8
-    return n_clients * n_pad * 4 + io, n_clients * n_pad * 4 + n_pad * 8 + io
+    n_pad, meta = -(-n // 4) * 4, (n_clients + 2) // 2 * 2  # flag + digests, an even word count
+    pin = n_clients * n_pad * 4 + (meta + n_pad) * 8
+    return pin, pin + n_pad * 8
 
 
 def fused_clients_host_f32(xs: Sequence[np.ndarray], weights: Sequence[float], pair_gens: Sequence,
@@ -283,9 +283,9 @@ _NP_XTYPE = {np.dtype(np.float32): L.SA_F32, np.dtype(np.float64): L.SA_F64, np.
 
 def host_clients_scratch(n_clients: int, n: int, itemsize: int) -> tuple[int, int]:
     """(pinned bytes, device bytes) sa_clients_host needs."""
-    n_pad = -(-n // 4) * 4
-    io = (n_pad + 1 + n_clients) * 8
-    return n_clients * n_pad * itemsize + io, n_clients * n_pad * (itemsize + 8) + n_pad * 8 + io
+    n_pad, meta = -(-n // 4) * 4, (n_clients + 2) // 2 * 2
+    pin = n_clients * n_pad * itemsize + (2 * n_pad + meta) * 8
+    return pin, pin + n_clients * n_pad * 8
 
 
 def clients_host(xs: Sequence[np.ndarray], compute_dtype, weights: Sequence[float], streams: Sequence[Sequence],
@@ -329,7 +329,7 @@ def _scratch(pinned: torch.Tensor, dev: torch.Tensor, need_pin: int, need_dev: i
 def mask_host_scratch(n: int, itemsize: int) -> tuple[int, int]:
     """(pinned bytes, device bytes) sa_mask_host needs."""
     n_pad = -(-n // 4) * 4
-    return n_pad * itemsize + (n_pad + 2) * 8, n_pad * itemsize + (n_pad + 2) * 8
+    return n_pad * itemsize + (2 + n_pad) * 8, n_pad * itemsize + (2 + n_pad) * 8
 
 
 def mask_host(x: np.ndarray, compute_dtype, streams: Sequence[tuple], pinned: torch.Tensor, dev: torch.Tensor, *,
@@ -353,8 +353,9 @@ def mask_host(x: np.ndarray, compute_dtype, streams: Sequence[tuple], pinned: to
 
 def sum_decode_host_scratch(n_clients: int, n: int) -> tuple[int, int]:
     """(pinned bytes, device bytes) sa_sum_decode_host needs."""
-    n_pad = -(-n // 4) * 4
-    return n_clients * n_pad * 8 + (n_pad + n_clients) * 8, (n_clients + 1) * n_pad * 8 + (n_pad + n_clients) * 8
+    n_pad, meta = -(-n // 4) * 4, (n_clients + 1) // 2 * 2
+    pin = (n_clients * n_pad + meta + n_pad) * 8
+    return pin, pin + n_pad * 8
 
 
 def sum_decode_host(masked: Sequence[np.ndarray], pinned: torch.Tensor, dev: torch.Tensor, *, fxp_bits: int = 18,
