@@ -4,9 +4,12 @@
  * parties, one secure-aggregation round on the GPU:
  *   sa_pcg64_from_seed -> sa_pcg64_advance -> sa_mask (x3) -> sa_sum_u64
  *   -> sa_decode,
- * with device memory and the stream managed through the HIP C API.  Writes
- * the masked vectors, the masked sum and the decoded float64 result to a
- * binary file; tests/test_gpu_c_abi.py compares them with the numpy oracle.
+ * with device memory and the stream managed through the HIP C API; then the
+ * same round through the blocking host-array entries: sa_mask_host per
+ * party -> sa_sum_decode_host, and sa_fused_clients_host_f32 (all parties,
+ * pair-shared).  Writes the masked vectors, the masked sum, the decoded
+ * float64 result and the host entries' outputs to a binary file;
+ * tests/test_gpu_c_abi.py compares them with the numpy oracle.
  *
  * Inputs are integer-generated so the test recomputes them exactly:
  *   x_c[i] = (float)((int32_t)((i * 2654435761u + 97u * c) % 20001u) - 10000) / 1e6f
@@ -101,13 +104,73 @@ int main(int argc, char** argv) {
   HIPC(hipMemcpyAsync(hd, dd, n * 8, hipMemcpyDeviceToHost, st));
   HIPC(hipStreamSynchronize(st));
 
+  /* the same round through the blocking host-array entries */
+  const uint64_t n_pad = (n + 3) & ~3ull, M = (P + 2) / 2 * 2;
+  const uint64_t pin_bytes = P * n_pad * 8 + (M + 2 * n_pad) * 8 + 64, dev_bytes = pin_bytes + 2 * n_pad * 8;
+  void *pin, *scratch;
+  HIPC(hipHostMalloc(&pin, pin_bytes, 0));
+  HIPC(hipMalloc(&scratch, dev_bytes));
+  uint64_t* hmh = (uint64_t*)malloc(n * 8 * P);
+  double* hdh = (double*)malloc(n * 8);
+  double* hdf = (double*)malloc(n * 8);
+  uint64_t dig_h[P], dig_f[P], fl[2] = {0, 0};
+  sa_pcg64 pg[P * (P - 1) / 2];
+  int8_t ps[P * (P - 1) / 2];
+  if (!hmh || !hdh || !hdf) return 1;
+  for (int c = 0, q = 0; c < P; c++) {
+    sa_mask_stream ms[P - 1];
+    int k = 0;
+    for (int v = 0; v < P; v++) {
+      if (v == c) continue;
+      const uint64_t seed = (0x5ECA66ull << 32) | ((uint64_t)(c < v ? c : v) << 16) | (uint64_t)(c < v ? v : c);
+      const uint32_t words[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+      SA(sa_pcg64_from_seed(words, 2, &ms[k].gen));
+      const sa_u128 d = {offset, 0};
+      SA(sa_pcg64_advance(&ms[k].gen, d));
+      ms[k].sign = v > c ? 1 : -1;
+      ms[k].peer = v;
+      if (v > c) { /* the pair (c, v) for the fused call, in u-major order */
+        pg[q] = ms[k].gen;
+        ps[q++] = 1;
+      }
+      k++;
+    }
+    uint32_t f32 = 0;
+    SA(sa_mask_host(hx + c * n, SA_F32, SA_F32, n, 1.0, 18, ms, P - 1, pin, scratch, hmh + c * n, &f32,
+                    (void*)st));
+    fl[0] |= f32;
+  }
+  const uint64_t* hin[P];
+  for (int c = 0; c < P; c++) hin[c] = hmh + c * n;
+  SA(sa_sum_decode_host(hin, P, n, 18, 1.0, pin, scratch, hdh, dig_h, (void*)st));
+  const float* hxs[P];
+  double w[P];
+  for (int c = 0; c < P; c++) {
+    hxs[c] = hx + c * n;
+    w[c] = 1.0;
+  }
+  uint32_t f32 = 0;
+  SA(sa_fused_clients_host_f32(hxs, w, P, n, 18, pg, ps, 1.0, pin, scratch, hdf, dig_f, &f32, (void*)st));
+  fl[1] = f32;
+
   FILE* f = fopen(argv[1], "wb");
   if (!f) return 1;
   fwrite(&n, 8, 1, f);
   fwrite(hm, 8, n * P, f);
   fwrite(hs, 8, n, f);
   fwrite(hd, 8, n, f);
+  fwrite(hmh, 8, n * P, f);
+  fwrite(hdh, 8, n, f);
+  fwrite(dig_h, 8, P, f);
+  fwrite(hdf, 8, n, f);
+  fwrite(dig_f, 8, P, f);
+  fwrite(fl, 8, 2, f);
   fclose(f);
+  hipHostFree(pin);
+  hipFree(scratch);
+  free(hmh);
+  free(hdh);
+  free(hdf);
   for (int c = 0; c < P; c++) {
     hipFree(dx[c]);
     hipFree(dm[c]);

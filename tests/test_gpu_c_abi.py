@@ -1,8 +1,11 @@
 """The C-ABI used from plain C (tests/c_abi/abi_roundtrip.c: what a cgo /
 JNI / N-API binding would do -- no Python or torch in the process): three
 parties, sa_pcg64_from_seed -> sa_pcg64_advance -> sa_mask -> sa_sum_u64 ->
-sa_decode on the GPU.  Its masked vectors and masked sum equal the numpy
-oracle bit for bit, its decode equals the oracle's float64."""
+sa_decode on the GPU, then the same round through the blocking host-array
+entries (sa_mask_host -> sa_sum_decode_host, sa_fused_clients_host_f32).
+Its masked vectors and masked sum equal the numpy oracle bit for bit, its
+decodes equal the oracle's float64, its digests the XOR of the oracle's
+masked vectors."""
 import os
 import subprocess
 
@@ -48,3 +51,17 @@ def test_plain_c_client_matches_oracle(tmp_path, n):
     s_exp = o.server_sum(exp)
     assert np.array_equal(s, s_exp)
     assert np.array_equal(dec, o.decode(s_exp))
+    # the blocking host-array entries on the same round
+    k = 1 + 5 * n
+    masked_h = raw[k:k + 3 * n].reshape(3, n)
+    dec_h = raw[k + 3 * n:k + 4 * n].view(np.float64)
+    dig_h = raw[k + 4 * n:k + 4 * n + 3]
+    dec_f = raw[k + 4 * n + 3:k + 5 * n + 3].view(np.float64)
+    dig_f = raw[k + 5 * n + 3:k + 5 * n + 6]
+    flags = raw[k + 5 * n + 6:k + 5 * n + 8]
+    want_dig = [int(np.bitwise_xor.reduce(e)) for e in exp]
+    for c in range(3):
+        assert np.array_equal(masked_h[c], exp[c]), c
+    assert np.array_equal(dec_h, o.decode(s_exp)) and np.array_equal(dec_f, o.decode(s_exp))
+    assert [int(v) for v in dig_h] == want_dig and [int(v) for v in dig_f] == want_dig
+    assert raw.size == k + 5 * n + 8 and not flags.any()
