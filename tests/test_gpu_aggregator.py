@@ -415,3 +415,41 @@ def test_party_functions_small_call_boundary_bit_exact(n):
         pays.append(pay)
     got = P.sum_decode(*pays, gpu=0)
     assert np.array_equal(got, o.secure_sum(xs, names, seeds=seeds)[0])
+
+
+@pytest.mark.parametrize("parties,dtype", [(9, np.float64), (9, np.int64), (10, np.int64), (9, np.float32),
+                                           (2, np.float32)])
+def test_small_call_party_counts_containers_and_weights(parties, dtype):
+    """The blocking small-call entries at their party limits (float32 fused:
+    2..8, other types: 2..9; beyond them the general path), a tuple of
+    layers, numpy-scalar weights for the average: bit-exact vs the oracle,
+    round after round."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    names = [f"p{i:02d}" for i in range(parties)]
+    seeds = o.seeds_for(names)
+    pyus = [PYU(nm, 0) for nm in names]
+    agg = SecureAggregator(PYU("server", 0), pyus,
+                           seeds={(a, b): seeds[a][b] for a in names for b in names if a < b})
+    rng = np.random.default_rng(parties)
+    shapes = [(3, 5), (7,)]
+    mk = (lambda sh: rng.integers(-500, 500, sh)) if dtype == np.int64 else \
+        (lambda sh: rng.standard_normal(sh).astype(dtype))
+    off = 0
+    for rnd in range(2):
+        layers = [tuple(mk(sh) for sh in shapes) for _ in names]
+        objs = [p(lambda t=t: t)() for p, t in zip(pyus, layers)]
+        got = rv(agg.sum(objs, axis=0))
+        assert isinstance(got, tuple) and [g.shape for g in got] == shapes
+        flat = [np.concatenate([a.reshape(-1) for a in t]) for t in layers]
+        exp = o.secure_sum(flat, names, seeds=seeds, offset=off)[0]
+        assert np.array_equal(np.concatenate([g.reshape(-1) for g in got]), exp), rnd
+        off += 22
+        ws = [np.int64(i + 1) if dtype == np.int64 else np.float32(0.5 * (i + 1)) for i in range(parties)]
+        got = rv(agg.average(objs, axis=0, weights=ws))
+        exp = o.secure_average(flat, names, weights=ws, seeds=seeds, offset=off)[0]
+        assert np.array_equal(np.concatenate([g.reshape(-1) for g in got]), exp), rnd
+        off += 22
