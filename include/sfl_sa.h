@@ -100,6 +100,11 @@ int sa_pcg64_from_seed(const uint32_t* words, int n_words, sa_pcg64* out);
 /* == numpy PCG64.advance(delta): jump the generator by delta draws. */
 int sa_pcg64_advance(sa_pcg64* g, sa_u128 delta);
 
+/* out[i] = in[i] advanced by delta[i] draws, for count generators in one
+ * call (the per-round positioning of a party's pair streams: one call per
+ * round instead of one per stream; out may alias in). */
+int sa_pcg64_advance_many(const sa_pcg64* in, const uint64_t* delta, int count, sa_pcg64* out);
+
 /* Host-side reference draws, for validating the seeding/jump math only
  * (tests).  Not used by any hot-path entry point. */
 int sa_pcg64_raw_host(sa_pcg64* g, uint64_t* out, uint64_t n);

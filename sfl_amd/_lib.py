@@ -29,7 +29,7 @@ TUNING_ABI_OFFSET = 1000  # sa_abi_version() of an SA_ABLATE / SA_TIMING build
 
 # every symbol include/sfl_sa.h declares (checked by tests/test_boundary.py)
 EXPORTED = (
-    "sa_abi_version", "sa_last_error", "sa_pcg64_from_seed", "sa_pcg64_advance",
+    "sa_abi_version", "sa_last_error", "sa_pcg64_from_seed", "sa_pcg64_advance", "sa_pcg64_advance_many",
     "sa_pcg64_raw_host", "sa_mask", "sa_fused_clients", "sa_fused_clients_host_f32", "sa_clients_host", "sa_mask_host", "sa_sum_decode_host", "sa_fused_bipartite", "sa_set_masking_reserve", "sa_sum_u64", "sa_decode",
     "sa_sum_f64", "sa_comm_unique_id", "sa_comm_init", "sa_comm_reduce_u64",
     "sa_comm_allreduce_u64", "sa_comm_reduce_scatter_u64", "sa_comm_alltoall_u64", "sa_comm_gather_f64", "sa_comm_destroy", "sa_sumsq_f32", "sa_dp_perturb_f32", "sa_mask_dp",
@@ -90,6 +90,7 @@ def _declare(lib):
     lib.sa_last_error.restype = C.c_char_p
     lib.sa_pcg64_from_seed.argtypes = [P(C.c_uint32), i32, P(PCG64)]
     lib.sa_pcg64_advance.argtypes = [P(PCG64), U128]
+    lib.sa_pcg64_advance_many.argtypes = [P(PCG64), P(C.c_uint64), i32, P(PCG64)]
     lib.sa_pcg64_raw_host.argtypes = [P(PCG64), P(C.c_uint64), u64]
     lib.sa_mask.argtypes = [vp, i32, i32, u64, dbl, vp, i32, P(MaskStream), i32, vp, vp, vp, vp, vp]
     lib.sa_fused_clients.argtypes = [P(LocalClient), i32, i32, u64, i32, P(PCG64), P(C.c_int8),
@@ -194,6 +195,18 @@ def pcg64_advance(g: PCG64, delta: int) -> PCG64:
     out = PCG64(g.state, g.inc)
     check(lib().sa_pcg64_advance(C.byref(out), U128.of(int(delta))), "sa_pcg64_advance")
     return out
+
+
+def pcg64_advance_many(gens, deltas) -> list:
+    """[pcg64_advance(g, d) for g, d in zip(gens, deltas)] in one library call
+    (deltas below 2^64)."""
+    k = len(gens)
+    if k == 0:
+        return []
+    arr = (PCG64 * k)(*gens)
+    ds = (C.c_uint64 * k)(*[int(d) for d in deltas])
+    check(lib().sa_pcg64_advance_many(arr, ds, k, arr), "sa_pcg64_advance_many")
+    return list(arr)
 
 
 def pcg64_raw_host(g: PCG64, n: int):

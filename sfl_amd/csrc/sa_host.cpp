@@ -119,6 +119,19 @@ extern "C" int sa_pcg64_advance(sa_pcg64* g, sa_u128 delta) {
   return SA_OK;
 }
 
+extern "C" int sa_pcg64_advance_many(const sa_pcg64* in, const uint64_t* delta, int count, sa_pcg64* out) {
+  if (count < 0 || (count > 0 && (!in || !delta || !out))) {
+    sa_set_error("sa_pcg64_advance_many: bad arguments");
+    return SA_ERR_ARG;
+  }
+  for (int i = 0; i < count; i++) {
+    const sa::Jump j = sa::jump_of(delta[i], 0);
+    out[i].inc = in[i].inc;
+    out[i].state = from128(sa::apply(j, to128(in[i].state), to128(in[i].inc)));
+  }
+  return SA_OK;
+}
+
 extern "C" int sa_pcg64_raw_host(sa_pcg64* g, uint64_t* out, uint64_t n) {
   if (!g || (n && !out)) {
     sa_set_error("sa_pcg64_raw_host: bad arguments");

@@ -81,7 +81,17 @@ class Masker:
     def streams(self, peers=None, offset: int = 0) -> list[tuple]:
         """(generator, sign, peer-index) triples for sa_mask."""
         peers = self.peers if peers is None else peers
-        return [(self.generator(p, offset), self.sign(p), i) for i, p in enumerate(peers)]
+        deltas = [self._pos[p] + offset for p in peers]
+        if any(d >> 64 for d in deltas):
+            gens = [self.generator(p, offset) for p in peers]
+        else:  # one library call for every stream of the round
+            gens = L.pcg64_advance_many([self._gens[p] for p in peers], deltas)
+        return [(g, self.sign(p), i) for i, (g, p) in enumerate(zip(gens, peers))]
+
+    def generators_at(self, peers) -> list:
+        """The generators of ``peers`` at their next unused draws (one
+        library call)."""
+        return [g for g, _, _ in self.streams(peers)]
 
     def consume(self, n: int, peers=None) -> None:
         for p in (self.peers if peers is None else peers):

@@ -381,6 +381,22 @@ class SecureAggregator(Aggregator):
             return PYUObject(self._device, result[0])
         return PYUObject(self._device, tuple(result) if isinstance(payloads[0], tuple) else result)
 
+    def _pair_streams(self, names, want: bool = True):
+        """Every internal pair (u < v) of ``names``: its generator at the next
+        unused draw (u's view, one library call per party) and u's sign,
+        u-major -- the order sa_fused_clients takes."""
+        C = len(names)
+        gens, signs = [], []
+        for u in range(C):
+            mu = self._maskers[names[u]]
+            later = names[u + 1:]
+            for v in later:
+                assert mu.position(v) == self._maskers[v].position(names[u]), "pair streams out of step"
+            if want and later:
+                gens += mu.generators_at(later)
+                signs += [mu.sign(v) for v in later]
+        return gens, signs
+
     def _host_one_call(self, data, layer_lists, sizes, shapes, weights, average, is_list, payloads, digests_keep,
                        C, n, sdev):
         """The small call as ONE blocking library call
@@ -388,13 +404,7 @@ class SecureAggregator(Aggregator):
         digests and PRG flag out; the Python side only positions the pair
         streams).  None when the library has no fused kernel for C."""
         names = [d.device.party for d in data]
-        pair_gens, pair_signs = [], []
-        for u in range(C):
-            for v in range(u + 1, C):
-                mu, mv = self._maskers[names[u]], self._maskers[names[v]]
-                assert mu.position(names[v]) == mv.position(names[u]), "pair streams out of step"
-                pair_gens.append(mu.generator(names[v]))
-                pair_signs.append(mu.sign(names[v]))
+        pair_gens, pair_signs = self._pair_streams(names)
         key = (C, n, str(sdev))
         sc = getattr(self, "_one_call", None)
         if sc is None or sc[0] != key:
@@ -653,14 +663,7 @@ class SecureAggregator(Aggregator):
         # the pair streams (one host jump-ahead each) only where a path uses
         # them: the fused launch and the careful replay's rejection search
         want_pairs = fusable or self._careful
-        pair_gens, pair_signs = [], []
-        for u in range(C):
-            for v in range(u + 1, C):
-                mu, mv = self._maskers[names[u]], self._maskers[names[v]]
-                assert mu.position(names[v]) == mv.position(names[u]), "pair streams out of step"
-                if want_pairs:
-                    pair_gens.append(mu.generator(names[v]))
-                    pair_signs.append(mu.sign(names[v]))
+        pair_gens, pair_signs = self._pair_streams(names, want_pairs)
         # per-party (generator, sign, peer) lists: the wire path's launches and the
         # careful-mode rejection fix-up need them (built lazily: 7 jump-aheads a party)
         client_streams = (None if fusable and not self._careful else

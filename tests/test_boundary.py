@@ -60,6 +60,24 @@ def test_advance_and_host_draws_match_numpy(delta):
     assert np.array_equal(L.pcg64_raw_host(g, 6), bg.random_raw(6))
 
 
+def test_advance_many_equals_one_by_one():
+    """sa_pcg64_advance_many (one call for a round's streams) == per-stream
+    sa_pcg64_advance == numpy's PCG64.advance, including delta 0 and in-place
+    output."""
+    from sfl_amd import _lib as L
+
+    gens = [L.pcg64_from_seed(7 + i) for i in range(6)]
+    deltas = [0, 1, 2, 1000003, 2**40 + 7, 2**64 - 1]
+    many = [g.pair() for g in L.pcg64_advance_many(gens, deltas)]
+    assert many == [L.pcg64_advance(g, d).pair() for g, d in zip(gens, deltas)]
+    bg = np.random.PCG64(9)
+    st = bg.state["state"]
+    bg.advance(12345)
+    g = L.pcg64_advance_many([L.PCG64.of(st["state"], st["inc"])], [12345])[0]
+    assert g.pair() == (bg.state["state"]["state"], bg.state["state"]["inc"])
+    assert L.pcg64_advance_many([], []) == []
+
+
 def test_errors_cross_the_abi_as_codes():
     import ctypes as C
 
@@ -111,6 +129,7 @@ def test_every_entry_point_validates_before_touching_the_gpu():
         "sa_comm_reduce_scatter_u64": lambda: lib.sa_comm_reduce_scatter_u64(None, None, None, 10, None),
         "sa_comm_gather_f64": lambda: lib.sa_comm_gather_f64(None, None, None, 10, 0, None),
         "sa_pcg64_raw_host": lambda: lib.sa_pcg64_raw_host(None, None, 5),
+        "sa_pcg64_advance_many": lambda: lib.sa_pcg64_advance_many(None, None, 3, None),
     }
     for name, call in calls.items():
         assert call() == L.SA_ERR_ARG, name
