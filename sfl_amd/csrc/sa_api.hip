@@ -702,7 +702,14 @@ extern "C" int sa_sum_f64(const double* const* w, int k, uint64_t n, double* out
 // sa_clients_host the masked sum) ride the one host-to-device copy as zeros
 // -- no separate fill -- and the words read back sit right before the
 // result, so one device-to-host copy brings everything (a small call is
-// bound by its number of device operations).
+// bound by its number of device operations).  An error after
+// the first copy was enqueued drains the stream before returning, so the
+// caller may reuse or free the scratch at once.
+static int drain(hipStream_t s, int rc) {
+  (void)hipStreamSynchronize(s);
+  return rc;
+}
+
 static inline uint64_t even_words(uint64_t w) { return (w + 1) & ~1ull; }
 
 extern "C" int sa_fused_clients_host_f32(const float* const* host_x, const double* weights, int n_clients,
@@ -740,9 +747,9 @@ extern "C" int sa_fused_clients_host_f32(const float* const* host_x, const doubl
   }
   int rc = sa_fused_clients(cl, n_clients, SA_F32, n, fxp_bits, pair_gens, pair_sign, nullptr, 0, d_sum, 0,
                             d_meta + 1, (uint32_t*)d_meta, stream);
-  if (rc) return rc;
+  if (rc) return drain(s, rc);
   rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_res, stream);
-  if (rc) return rc;
+  if (rc) return drain(s, rc);
   SA_HIP_CHECK(hipMemcpyAsync(pin_meta, d_meta, (M + n_pad) * 8, hipMemcpyDeviceToHost, s));
   SA_HIP_CHECK(hipStreamSynchronize(s));
   memcpy(out, pin_res, n * 8);
@@ -794,10 +801,10 @@ extern "C" int sa_clients_host(const void* const* host_x, int x_type, int comput
     const int rc = sa_mask(d_in + c * n_pad * xs, x_type, compute_type, n, weights[c], nullptr, fxp_bits,
                            streams + c * (C - 1), n_clients - 1, d_masked + c * n_pad, d_sum, d_meta + 1 + c,
                            (uint32_t*)d_meta, stream);
-    if (rc) return rc;
+    if (rc) return drain(s, rc);
   }
   const int rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_res, stream);
-  if (rc) return rc;
+  if (rc) return drain(s, rc);
   SA_HIP_CHECK(hipMemcpyAsync(pin_meta, d_meta, (M + n_pad) * 8, hipMemcpyDeviceToHost, s));
   SA_HIP_CHECK(hipStreamSynchronize(s));
   memcpy(out, pin_res, n * 8);
@@ -829,7 +836,7 @@ extern "C" int sa_mask_host(const void* host_x, int x_type, int compute_type, ui
   SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, n_pad * xs + 16, hipMemcpyHostToDevice, s));
   const int rc = sa_mask(d_in, x_type, compute_type, n, weight, nullptr, fxp_bits, streams, n_streams, d_out,
                          nullptr, nullptr, (uint32_t*)d_flag, stream);
-  if (rc) return rc;
+  if (rc) return drain(s, rc);
   SA_HIP_CHECK(hipMemcpyAsync(pin_flag, d_flag, 16 + n * 8, hipMemcpyDeviceToHost, s));
   SA_HIP_CHECK(hipStreamSynchronize(s));
   memcpy(out, pin_flag + 2, n * 8);
@@ -867,12 +874,12 @@ extern "C" int sa_sum_decode_host(const uint64_t* const* host_masked, int n_clie
   for (uint64_t c = 0; c < C; c++) {
     ins[c] = d_in + c * n_pad;
     const int rc = sa_xor_u64(ins[c], n, d_dig + c, stream);
-    if (rc) return rc;
+    if (rc) return drain(s, rc);
   }
   int rc = sa_sum_u64(ins, n_clients, n, d_sum, stream);
-  if (rc) return rc;
+  if (rc) return drain(s, rc);
   rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_res, stream);
-  if (rc) return rc;
+  if (rc) return drain(s, rc);
   SA_HIP_CHECK(hipMemcpyAsync(pin_dig, d_dig, (M + n) * 8, hipMemcpyDeviceToHost, s));
   SA_HIP_CHECK(hipStreamSynchronize(s));
   memcpy(out, pin_res, n * 8);
