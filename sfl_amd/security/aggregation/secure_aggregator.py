@@ -21,6 +21,13 @@ pair stream once and applies it to both clients; otherwise each party masks
 on its own GPU (``sa_mask``), the masked vectors move to the server
 (``.to(server)``, the wire) and are summed there (``sa_sum_u64``).  Both give
 bit-identical sums.
+
+Small host calls (up to ``SMALL_CALL_BYTES`` a party, co-located parties)
+are latency-bound, so each is ONE blocking library call
+(``sa_fused_clients_host_f32`` for float32, ``sa_clients_host`` for the
+other types: host arrays in, decoded result out); a replay after a flagged
+raw 0, wire images, per-element weights or more parties than those calls
+take go through the general path above.
 """
 
 from __future__ import annotations
