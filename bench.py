@@ -53,6 +53,7 @@ from benchkit.baseline import cpu_baseline, pair_seed, rank_cpu_baseline, rank_c
 from benchkit.containment import (Watchdog, control_group, inject_in_design, injected, publish_error,  # noqa: E402,F401
                                   published_errors, run_contained, run_variants, variant_summary)
 from benchkit.launcher import failing_ranks_report, launch_ranks  # noqa: E402,F401
+from benchkit import rccl_log  # noqa: E402
 from benchkit.roofline import (HBM_PEAK_GBPS, PCG_ONE_DRAWS_8WAVE, PCG_PAIR_DRAWS_2WAVE,  # noqa: E402,F401
                                PMC_DIRS, PMC_ELEMS, VALU_PEAK_WAVE_INSTR_PER_S, committed_kernel_ms,
                                draw_loop_ceilings, exchange_model, kernel_key, pmc_traffic, pmc_valu,
@@ -164,8 +165,12 @@ def dry_run(args, world: int, rank: int, cpu, wd: Watchdog) -> None:
     import torch.distributed as dist
 
     multi = world > 1 or args.dist
+    # what a GPU rank would add to its environment before its communicators
+    # (rank_comm_env), and the rehearsal-only RCCL variables it inherited
+    comm_env = rank_comm_env(args, rank, multi, "/nonexistent")
     ranks = [{"rank": rank, "pid": os.getpid(), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
-              "master_port": os.environ.get("MASTER_PORT")}]
+              "master_port": os.environ.get("MASTER_PORT"), "comm_env": sorted(comm_env),
+              "inherited_rehearsal_env": sorted(k for k in rccl_log.REHEARSAL_ONLY_ENV if k in os.environ)}]
     if multi:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         allr = [None] * world
@@ -669,6 +674,21 @@ def main():
     record(rank_main)(args)
 
 
+def rank_comm_env(args, rank: int, multi: bool, log_dir: str) -> dict:
+    """What a rank adds to its environment before its first communicator:
+    RCCL's per-rank init log (benchkit/rccl_log.py) on every RCCL path, and
+    ONLY under --rehearse-one-gpu (RCCL between ranks that share one GPU) the
+    NCCL_HOSTID / NCCL_SOCKET_IFNAME / NCCL_IB_DISABLE that make each rank
+    its own RCCL node over sockets -- never on the product path, where they
+    would push the exchange off xGMI (tests/test_bench_launcher.py)."""
+    if not multi or (args.rehearse_one_gpu and args.rehearse_comm == "standin"):
+        return {}
+    env = dict(rccl_log.debug_env(rank, log_dir))
+    if args.rehearse_one_gpu:
+        env.update(one_gpu_rccl_env(rank))
+    return env
+
+
 def rank_main(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -703,14 +723,31 @@ def rank_main(args):
     dev = torch.device("cuda", gpu)
     _lib.check(_lib.lib().sa_set_masking_reserve(args.masking_reserve), "sa_set_masking_reserve")
     comm = None
+    rccl_dir = None
+    if multi and not (rehearse and args.rehearse_comm == "standin"):
+        # RCCL's init log, one file per rank (before the first communicator:
+        # RCCL reads its debug settings once per process) -> the line's
+        # "rccl" record, which transport carried the exchange
+        import tempfile
+
+        rccl_dir = tempfile.mkdtemp(prefix=f"sfl_rccl_rank{rank}_")
+        env = rank_comm_env(args, rank, multi, rccl_dir)
+        if "NCCL_DEBUG_FILE" not in env:
+            os.rmdir(rccl_dir)
+            rccl_dir = None
+        leaked = [k for k in rccl_log.REHEARSAL_ONLY_ENV if k in os.environ and k not in env]
+        if leaked:  # the record names them too (rccl.rehearsal_env)
+            print(f"warning: rank {rank}: {', '.join(leaked)} set in the environment: RCCL may not use "
+                  "xGMI", file=sys.stderr)
+        os.environ.update(env)
     if multi and rehearse and args.rehearse_comm == "standin":
         dist.init_process_group("gloo", rank=rank, world_size=world)
         comm = HostStandinComm(rank, world)
     elif multi and rehearse:
         # the product's process group and communicator, every rank its own
-        # RCCL node on this one GPU (NCCL_HOSTID): torch's NCCL group
-        # carries the barriers and the timing reductions, as on the node
-        os.environ.update(one_gpu_rccl_env(rank))
+        # RCCL node on this one GPU (NCCL_HOSTID, set by rank_comm_env):
+        # torch's NCCL group carries the barriers and the timing reductions,
+        # as on the node
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         comm = one_gpu_rccl_comm(rank, world)
     elif multi:
@@ -807,6 +844,8 @@ def rank_main(args):
         # the exchange against the links: says by itself whether N is link- or kernel-bound
         out["roofline"]["exchange"] = r["exchange"].get("model")
         out["exchange_variants"] = [variant_summary(r)]
+        if hasattr(comm, "info"):  # an RcclComm: what RCCL made of the run (every rank takes part)
+            out["rccl"] = rccl_record(comm, rank, world, rccl_dir)
         out["variant_timeout_seconds"] = args.variant_timeout
         with wd.lock:
             wd.line = out if rank == 0 else {}
@@ -834,6 +873,26 @@ def rank_main(args):
     if comm is not None:
         comm.close()
         dist.destroy_process_group()
+
+
+def rccl_record(comm, rank: int, world: int, log_dir) -> dict:
+    """The line's ``rccl`` record (benchkit/rccl_log.py): this rank's RCCL
+    init log and ``sa_comm_info``, gathered to every rank after the
+    headline (its connections are set up by then)."""
+    import shutil
+
+    import torch.distributed as dist
+
+    try:
+        info = comm.info()
+    except Exception as e:  # noqa: BLE001 - recorded, never costs the headline
+        info = {"error": str(e)[:200]}
+    mine = rccl_log.rank_summary(rank, log_dir, info)
+    if log_dir:
+        shutil.rmtree(log_dir, ignore_errors=True)
+    box = [None] * world
+    dist.all_gather_object(box, mine)
+    return rccl_log.combine(box, world)
 
 
 def run_host_resident(ctx, steps: int, warmup: int) -> dict:
@@ -974,9 +1033,14 @@ def extra_measurements(args, xs, plan, gens, K, torch, dev) -> dict:
                 "fused_wire_images_algorithmic_GBps": (12 * C * N + 8 * N) / t / 1e9})
 
     # ---- host-resident, overlapped
-    host_x = torch.stack([x.cpu() for x in xs]).pin_memory()        # [C, N] fp32
+    host_x = torch.empty((C, N), dtype=torch.float32, pin_memory=True)  # [C, N] fp32, pinned once
+    for c in range(C):
+        host_x[c].copy_(xs[c])
     host_dec = torch.empty(N, dtype=torch.float64).pin_memory()
-    host_m = torch.empty((C, N), dtype=torch.int64).pin_memory()
+    # every client's masked vector back too: up to 16 GiB of pinned host
+    # memory (config 3: 6.4 GB); config 5's 64 GB of wire images are left out
+    images = 8 * C * N <= (16 << 30)
+    host_m = torch.empty((C, N), dtype=torch.int64).pin_memory() if images else None
     dev_x = torch.empty((C, N), dtype=torch.float32, device=dev)
     dec = torch.empty(N, dtype=torch.float64, device=dev)
     s_h2d, s_cmp, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
@@ -1004,7 +1068,7 @@ def extra_measurements(args, xs, plan, gens, K, torch, dev) -> dict:
                     for c in range(C):
                         host_m[c, lo:hi].copy_(outs[c][lo:hi], non_blocking=True)
 
-    for with_images in (False, True):
+    for with_images in ((False, True) if images else (False,)):
         t = timeit(lambda: host_round(with_images), reps=2)
         key = "host_resident_with_wire_images" if with_images else "host_resident"
         h2d, d2h = 4 * C * N, 8 * N + (8 * C * N if with_images else 0)
@@ -1012,7 +1076,21 @@ def extra_measurements(args, xs, plan, gens, K, torch, dev) -> dict:
                     f"{key}_pcie_bytes": {"h2d": h2d, "d2h": d2h}})
     res["host_resident_note"] = ("pinned host fp32 inputs -> H2D -> fused quantize+mask+sum -> decode -> D2H of the "
                                  "float64 aggregate (and of every client's masked u64 vector), 16 chunks, H2D / "
-                                 "compute / D2H on three streams")
+                                 "compute / D2H on three streams" + ("" if images else
+                                 "; no wire-image variant: 8*C*N bytes of pinned host memory exceed 16 GiB"))
+    # the copy floor of the same bytes: the H2D of every client's input alone,
+    # pinned, in the same chunks (the host-resident round cannot beat it)
+    def h2d_only():
+        with torch.cuda.stream(s_h2d):
+            for lo, hi in bounds:
+                for c in range(C):
+                    dev_x[c, lo:hi].copy_(host_x[c, lo:hi], non_blocking=True)
+
+    t = timeit(h2d_only, reps=2)
+    res.update({"h2d_floor_ms": t * 1e3, "h2d_floor_GBps": 4 * C * N / t / 1e9,
+                "host_resident_vs_h2d_floor": t / (res["host_resident_ms"] / 1e3)})
+    if not images:
+        return res
 
     # ---- round-1 serial variant
     host_m1 = [host_m[c] for c in range(C)]

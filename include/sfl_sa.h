@@ -393,6 +393,10 @@ int sa_comm_alltoall_u64(void* comm, const uint64_t* send, uint64_t* recv, uint6
  * = rank r's send (grouped ncclSend/ncclRecv); recv may be NULL off root. */
 int sa_comm_gather_f64(void* comm, const double* send, double* recv, uint64_t count, int root,
                        void* stream);
+/* What RCCL made of the communicator (ncclCommCount, ncclCommUserRank,
+ * ncclCommCuDevice): the bench line's `rccl` record, so a scaling run shows
+ * by itself that RCCL saw N ranks on N devices.  Any pointer may be NULL. */
+int sa_comm_info(void* comm, int* nranks, int* rank, int* device);
 int sa_comm_destroy(void* comm);
 
 #ifdef __cplusplus

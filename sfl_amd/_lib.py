@@ -32,7 +32,7 @@ EXPORTED = (
     "sa_abi_version", "sa_last_error", "sa_pcg64_from_seed", "sa_pcg64_advance", "sa_pcg64_advance_many",
     "sa_pcg64_raw_host", "sa_mask", "sa_fused_clients", "sa_fused_clients_host_f32", "sa_clients_host", "sa_mask_host", "sa_sum_decode_host", "sa_fused_bipartite", "sa_set_masking_reserve", "sa_sum_u64", "sa_decode",
     "sa_sum_f64", "sa_comm_unique_id", "sa_comm_init", "sa_comm_reduce_u64",
-    "sa_comm_allreduce_u64", "sa_comm_reduce_scatter_u64", "sa_comm_alltoall_u64", "sa_comm_gather_f64", "sa_comm_destroy", "sa_sumsq_f32", "sa_dp_perturb_f32", "sa_mask_dp",
+    "sa_comm_allreduce_u64", "sa_comm_reduce_scatter_u64", "sa_comm_alltoall_u64", "sa_comm_gather_f64", "sa_comm_info", "sa_comm_destroy", "sa_sumsq_f32", "sa_dp_perturb_f32", "sa_mask_dp",
     "sa_pcg64_find_zero", "sa_stream_shift", "sa_xor_u64",
 )
 
@@ -113,6 +113,7 @@ def _declare(lib):
     lib.sa_comm_reduce_scatter_u64.argtypes = [vp, vp, vp, u64, vp]
     lib.sa_comm_gather_f64.argtypes = [vp, vp, vp, u64, i32, vp]
     lib.sa_comm_alltoall_u64.argtypes = [vp, vp, vp, u64, vp]
+    lib.sa_comm_info.argtypes = [vp, P(C.c_int), P(C.c_int), P(C.c_int)]
     lib.sa_comm_destroy.argtypes = [vp]
     lib.sa_sumsq_f32.argtypes = [vp, u64, vp, vp, i32, vp]
     lib.sa_dp_perturb_f32.argtypes = [vp, u64, P(DP), vp, vp]

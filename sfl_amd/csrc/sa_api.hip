@@ -738,7 +738,7 @@ extern "C" int sa_fused_clients_host_f32(const float* const* host_x, const doubl
   const hipStream_t s = (hipStream_t)stream;
   for (uint64_t c = 0; c < C; c++) memcpy(pin_in + c * n_pad, host_x[c], n * 4);
   memset(pin_meta, 0, M * 8);
-  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * 4 + M * 8, hipMemcpyHostToDevice, s));
+  SA_HIP_CHECK_DRAIN(s, hipMemcpyAsync(d_in, pin_in, C * n_pad * 4 + M * 8, hipMemcpyHostToDevice, s));
   sa_local_client cl[8];
   for (uint64_t c = 0; c < C; c++) {
     cl[c].x = d_in + c * n_pad;
@@ -750,8 +750,8 @@ extern "C" int sa_fused_clients_host_f32(const float* const* host_x, const doubl
   if (rc) return drain(s, rc);
   rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_res, stream);
   if (rc) return drain(s, rc);
-  SA_HIP_CHECK(hipMemcpyAsync(pin_meta, d_meta, (M + n_pad) * 8, hipMemcpyDeviceToHost, s));
-  SA_HIP_CHECK(hipStreamSynchronize(s));
+  SA_HIP_CHECK_DRAIN(s, hipMemcpyAsync(pin_meta, d_meta, (M + n_pad) * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK_DRAIN(s, hipStreamSynchronize(s));
   memcpy(out, pin_res, n * 8);
   *flags = (uint32_t)pin_meta[0];  // the flag word's low half (little-endian)
   memcpy(digests, pin_meta + 1, C * 8);
@@ -792,10 +792,10 @@ extern "C" int sa_clients_host(const void* const* host_x, int x_type, int comput
   for (uint64_t c = 0; c < C; c++) memcpy(pin_in + c * n_pad * xs, host_x[c], n * xs);
   if (zero_by_copy) {
     memset(pin_sum, 0, (n_pad + M) * 8);
-    SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * xs + (n_pad + M) * 8, hipMemcpyHostToDevice, s));
+    SA_HIP_CHECK_DRAIN(s, hipMemcpyAsync(d_in, pin_in, C * n_pad * xs + (n_pad + M) * 8, hipMemcpyHostToDevice, s));
   } else {
-    SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, C * n_pad * xs, hipMemcpyHostToDevice, s));
-    SA_HIP_CHECK(hipMemsetAsync(d_sum, 0, (n_pad + M) * 8, s));
+    SA_HIP_CHECK_DRAIN(s, hipMemcpyAsync(d_in, pin_in, C * n_pad * xs, hipMemcpyHostToDevice, s));
+    SA_HIP_CHECK_DRAIN(s, hipMemsetAsync(d_sum, 0, (n_pad + M) * 8, s));
   }
   for (uint64_t c = 0; c < C; c++) {
     const int rc = sa_mask(d_in + c * n_pad * xs, x_type, compute_type, n, weights[c], nullptr, fxp_bits,
@@ -805,8 +805,8 @@ extern "C" int sa_clients_host(const void* const* host_x, int x_type, int comput
   }
   const int rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_res, stream);
   if (rc) return drain(s, rc);
-  SA_HIP_CHECK(hipMemcpyAsync(pin_meta, d_meta, (M + n_pad) * 8, hipMemcpyDeviceToHost, s));
-  SA_HIP_CHECK(hipStreamSynchronize(s));
+  SA_HIP_CHECK_DRAIN(s, hipMemcpyAsync(pin_meta, d_meta, (M + n_pad) * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK_DRAIN(s, hipStreamSynchronize(s));
   memcpy(out, pin_res, n * 8);
   *flags = (uint32_t)pin_meta[0];
   memcpy(digests, pin_meta + 1, C * 8);
@@ -833,12 +833,12 @@ extern "C" int sa_mask_host(const void* host_x, int x_type, int compute_type, ui
   const hipStream_t s = (hipStream_t)stream;
   memcpy(pin_in, host_x, n * xs);
   pin_flag[0] = pin_flag[1] = 0;
-  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, n_pad * xs + 16, hipMemcpyHostToDevice, s));
+  SA_HIP_CHECK_DRAIN(s, hipMemcpyAsync(d_in, pin_in, n_pad * xs + 16, hipMemcpyHostToDevice, s));
   const int rc = sa_mask(d_in, x_type, compute_type, n, weight, nullptr, fxp_bits, streams, n_streams, d_out,
                          nullptr, nullptr, (uint32_t*)d_flag, stream);
   if (rc) return drain(s, rc);
-  SA_HIP_CHECK(hipMemcpyAsync(pin_flag, d_flag, 16 + n * 8, hipMemcpyDeviceToHost, s));
-  SA_HIP_CHECK(hipStreamSynchronize(s));
+  SA_HIP_CHECK_DRAIN(s, hipMemcpyAsync(pin_flag, d_flag, 16 + n * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK_DRAIN(s, hipStreamSynchronize(s));
   memcpy(out, pin_flag + 2, n * 8);
   *flags = (uint32_t)pin_flag[0];
   return SA_OK;
@@ -869,7 +869,7 @@ extern "C" int sa_sum_decode_host(const uint64_t* const* host_masked, int n_clie
   const hipStream_t s = (hipStream_t)stream;
   for (uint64_t c = 0; c < C; c++) memcpy(pin_in + c * n_pad, host_masked[c], n * 8);
   memset(pin_dig, 0, M * 8);
-  SA_HIP_CHECK(hipMemcpyAsync(d_in, pin_in, (C * n_pad + M) * 8, hipMemcpyHostToDevice, s));
+  SA_HIP_CHECK_DRAIN(s, hipMemcpyAsync(d_in, pin_in, (C * n_pad + M) * 8, hipMemcpyHostToDevice, s));
   const uint64_t* ins[kSumMaxIn];
   for (uint64_t c = 0; c < C; c++) {
     ins[c] = d_in + c * n_pad;
@@ -880,8 +880,8 @@ extern "C" int sa_sum_decode_host(const uint64_t* const* host_masked, int n_clie
   if (rc) return drain(s, rc);
   rc = sa_decode(d_sum, n, fxp_bits, divisor, nullptr, d_res, stream);
   if (rc) return drain(s, rc);
-  SA_HIP_CHECK(hipMemcpyAsync(pin_dig, d_dig, (M + n) * 8, hipMemcpyDeviceToHost, s));
-  SA_HIP_CHECK(hipStreamSynchronize(s));
+  SA_HIP_CHECK_DRAIN(s, hipMemcpyAsync(pin_dig, d_dig, (M + n) * 8, hipMemcpyDeviceToHost, s));
+  SA_HIP_CHECK_DRAIN(s, hipStreamSynchronize(s));
   memcpy(out, pin_res, n * 8);
   memcpy(digests, pin_dig, C * 8);
   return SA_OK;

@@ -20,6 +20,20 @@ int sa_mask_impl(const void* x, int x_type, int compute_type, uint64_t n, double
     }                                                                                   \
   } while (0)
 
+// SA_HIP_CHECK for calls made after a blocking entry has enqueued work that
+// reads the caller's scratch: on failure it drains the stream first
+// (hipStreamSynchronize, its own result ignored), so the caller may reuse or
+// free the scratch as soon as the entry returns.
+#define SA_HIP_CHECK_DRAIN(s_, expr)                                                     \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      sa_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+      (void)hipStreamSynchronize(s_);                                                   \
+      return SA_ERR_HIP;                                                                \
+    }                                                                                   \
+  } while (0)
+
 namespace sa {
 
 constexpr int kMaxLocal = 8;     // co-located clients per fused launch

@@ -167,3 +167,24 @@ extern "C" int sa_comm_destroy(void* comm) {
   SA_NCCL_CHECK(ncclCommDestroy((ncclComm_t)comm));
   return SA_OK;
 }
+
+extern "C" int sa_comm_info(void* comm, int* nranks, int* rank, int* device) {
+  if (!comm) {
+    sa_set_error("sa_comm_info: bad arguments (comm is NULL)");
+    return SA_ERR_ARG;
+  }
+  int v = 0;
+  if (nranks) {
+    SA_NCCL_CHECK(ncclCommCount((ncclComm_t)comm, &v));
+    *nranks = v;
+  }
+  if (rank) {
+    SA_NCCL_CHECK(ncclCommUserRank((ncclComm_t)comm, &v));
+    *rank = v;
+  }
+  if (device) {
+    SA_NCCL_CHECK(ncclCommCuDevice((ncclComm_t)comm, &v));
+    *device = v;
+  }
+  return SA_OK;
+}

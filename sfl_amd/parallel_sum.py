@@ -149,6 +149,13 @@ class RcclComm:
                                            send.numel(), root, C.c_void_p(stream)), "sa_comm_gather_f64")
         return recv
 
+    def info(self) -> dict:
+        """What RCCL made of this communicator: {"nranks", "rank", "device"}
+        (ncclCommCount / ncclCommUserRank / ncclCommCuDevice)."""
+        n, r, d = C.c_int(-1), C.c_int(-1), C.c_int(-1)
+        L.check(L.lib().sa_comm_info(self._h, C.byref(n), C.byref(r), C.byref(d)), "sa_comm_info")
+        return {"nranks": n.value, "rank": r.value, "device": d.value}
+
     def close(self):
         if self._h:
             L.check(L.lib().sa_comm_destroy(self._h), "sa_comm_destroy")

@@ -164,6 +164,10 @@ ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
   *count = reinterpret_cast<Comm*>(comm)->w->n;
   return ncclSuccess;
 }
+ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* device) {
+  *device = reinterpret_cast<Comm*>(comm)->rank;  // one device per rank thread
+  return ncclSuccess;
+}
 const char* ncclGetErrorString(ncclResult_t) { return "rccl double"; }
 // collectives and set-up sa_rccl.cpp references but this test does not call
 ncclResult_t ncclGetUniqueId(ncclUniqueId*) { return ncclInternalError; }
@@ -217,6 +221,9 @@ int main(int argc, char** argv) {
       for (int p = 0; p < W; ++p)
         for (uint64_t i = 0; i < count; ++i) send[p * count + i] = tag(r, p, i);
       if (sa_comm_alltoall_u64(&comms[r], send.data(), recv.data(), count, nullptr) != SA_OK) bad[r] |= 1;
+      int nr = -1, rk = -1, dv = -1;  // sa_comm_info: what the communicator says of itself
+      if (sa_comm_info(&comms[r], &nr, &rk, &dv) != SA_OK || nr != W || rk != r || dv != r) bad[r] |= 8;
+      if (sa_comm_info(&comms[r], nullptr, nullptr, nullptr) != SA_OK) bad[r] |= 8;
       for (int p = 0; p < W; ++p)
         for (uint64_t i = 0; i < count; ++i) {
           uint64_t want = p == r ? ~0ull : tag(p, r, i);

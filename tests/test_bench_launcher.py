@@ -428,3 +428,93 @@ def test_dry_run_n8_line_carries_the_exchange_model():
     assert R.exchange_model("sharded", 1, 10, 1.0, 1.0, 8) is None
     mm = R.exchange_model("direct", 4, 10**8, 0.9, 3.0, 8, "rehearsal")
     assert mm["link_frac"] == pytest.approx(2e8 / 3e-3 / 1e9 / R.XGMI_LINK_GBPS_PER_DIRECTION)
+
+
+def _dry_ranks(extra):
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--cpu-baseline-seconds", "0",
+                        "--variants", "none", "--steps", "2", "--warmup", "1", *extra],
+                       capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    return line["ranks"]
+
+
+def test_product_ranks_never_set_the_rehearsal_rccl_env():
+    """only --rehearse-one-gpu may set NCCL_HOSTID /
+    NCCL_SOCKET_IFNAME / NCCL_IB_DISABLE (each rank its own RCCL node over
+    sockets); the product's N > 1 ranks -- self-launched here -- set none of
+    them and inherit none from the launcher, but do route RCCL's init log to
+    a per-rank file (the line's rccl record)."""
+    from benchkit.rccl_log import REHEARSAL_ONLY_ENV
+
+    env = _env()
+    leaked = [k for k in REHEARSAL_ONLY_ENV if k in env]
+    if leaked:
+        pytest.skip(f"the test environment itself sets {leaked}")
+    for r in _dry_ranks([]):
+        assert not set(r["comm_env"]) & set(REHEARSAL_ONLY_ENV), r
+        assert r["inherited_rehearsal_env"] == [], r
+        assert {"NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "NCCL_DEBUG_FILE"} <= set(r["comm_env"]), r
+    for r in _dry_ranks(["--rehearse-one-gpu"]):
+        assert set(REHEARSAL_ONLY_ENV) <= set(r["comm_env"]), r
+    for r in _dry_ranks(["--rehearse-one-gpu", "--rehearse-comm", "standin"]):
+        assert r["comm_env"] == [], r
+
+
+def test_rank_comm_env_table():
+    import argparse
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    a = argparse.Namespace(rehearse_one_gpu=False, rehearse_comm="rccl")
+    assert bench.rank_comm_env(a, 0, False, "/x") == {}
+    env = bench.rank_comm_env(a, 3, True, "/x")
+    assert env["NCCL_DEBUG_FILE"] == "/x/rank3.%p.log" and "NCCL_HOSTID" not in env
+    a.rehearse_one_gpu = True
+    assert bench.rank_comm_env(a, 1, True, "/x")["NCCL_HOSTID"] == "sfl-onegpu-rank1"
+    a.rehearse_comm = "standin"
+    assert bench.rank_comm_env(a, 1, True, "/x") == {}
+
+
+# RCCL init-log lines in the formats RCCL/NCCL 2.x print (transport/p2p.cc,
+# net.cc, shm.cc, init.cc); the one-GPU rehearsal's real log is checked on
+# the GPU (tests/test_gpu_bench_rehearsal.py)
+_LOG = """\
+box:123:123 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC/read
+box:123:123 [0] NCCL INFO Channel 01/0 : 0[0] -> 1[1] via P2P/IPC/read comm 0x55d0 nRanks 02
+box:123:123 [0] NCCL INFO Channel 02/0 : 0[0] -> 1[1] via P2P/direct pointer/read
+box:123:123 [0] NCCL INFO Channel 00/0 : 1[1] -> 0[0] [send] via NET/Socket/0
+box:123:123 [0] NCCL INFO Channel 00/0 : 1[1] -> 0[0] [receive] via NET/Socket/0
+box:123:123 [0] NCCL INFO Channel 00 : 0[0] -> 1[1] via SHM/direct/direct
+box:123:123 [0] NCCL INFO comm 0x55d0 rank 0 nRanks 8 nNodes 1 localRanks 8 localRank 0 MNNVL 0
+box:123:123 [0] NCCL INFO ncclCommInitRank comm 0x55d0 rank 0 nranks 8 cudaDev 0 busId 5000 - Init COMPLETE
+box:123:123 [0] NCCL INFO Connected all rings
+unrelated line via P2P/IPC, no info tag
+"""
+
+
+def test_rccl_log_parse_and_combine():
+    from benchkit import rccl_log as R
+
+    s = R.summarise(_LOG)
+    assert s["transports"] == {"P2P/IPC": 2, "P2P/direct pointer": 1, "NET/Socket": 2, "SHM/direct": 1}
+    assert s["nranks"] == [2, 8] and s["nnodes"] == [1] and s["lines"] == 9
+    xgmi_only = {"transports": {"P2P/IPC": 24}, "nranks": [8], "nnodes": [1], "lines": 40}
+    per = [{"rank": r, "comm": {"nranks": 8, "rank": r, "device": r}, "log": xgmi_only} for r in range(8)]
+    c = R.combine(per, 8)
+    assert c["xgmi"] is True and c["nranks"] == 8 and c["transports"] == {"P2P/IPC": 192}
+    assert c["devices"] == list(range(8)) and c["nnodes_logged"] == [1]
+    per[3]["log"] = s
+    assert R.combine(per, 8)["xgmi"] is False
+    none = [{"rank": 0, "comm": None, "log": None}]
+    assert R.combine(none, 1)["xgmi"] is None
+
+
+def test_rccl_debug_env_respects_a_caller_log(monkeypatch):
+    from benchkit import rccl_log as R
+
+    monkeypatch.setenv("NCCL_DEBUG_FILE", "/somewhere/else.log")
+    assert R.debug_env(0, "/x") == {}
+    rec = R.rank_summary(0, None, {"nranks": 2})
+    assert rec["log"] is None and "NCCL_DEBUG_FILE" in rec["note"]

@@ -128,6 +128,7 @@ def test_every_entry_point_validates_before_touching_the_gpu():
         "sa_comm_allreduce_u64": lambda: lib.sa_comm_allreduce_u64(None, None, None, 10, None),
         "sa_comm_reduce_scatter_u64": lambda: lib.sa_comm_reduce_scatter_u64(None, None, None, 10, None),
         "sa_comm_gather_f64": lambda: lib.sa_comm_gather_f64(None, None, None, 10, 0, None),
+        "sa_comm_info": lambda: lib.sa_comm_info(None, None, None, None),
         "sa_pcg64_raw_host": lambda: lib.sa_pcg64_raw_host(None, None, 5),
         "sa_pcg64_advance_many": lambda: lib.sa_pcg64_advance_many(None, None, 3, None),
     }

@@ -156,6 +156,17 @@ def test_bench_n_ranks_every_design(world, comm, check_1m):
     assert ("RcclComm" in line["rehearsal"]) == (comm == "rccl")
     assert line["roofline"]["exchange"]["mode"] == "rehearsal" and line["roofline"]["exchange"]["bound"]
     assert "exchange_probe" not in line and line["exchange_variants"][0]["name"] == "sharded"
+    # RCCL's own account (benchkit/rccl_log.py): W ranks, and the socket
+    # transport the NCCL_HOSTID rehearsal forces -- so the node's first
+    # record will show P2P/IPC (xGMI) by itself
+    if comm == "rccl":
+        rc = line["rccl"]
+        assert rc["world"] == world and rc["nranks"] == world and rc["nranks_logged"] == [world], rc
+        assert rc["transports"].get("NET/Socket", 0) > 0 and rc["xgmi"] is False, rc
+        assert not any(k.startswith("P2P") for k in rc["transports"]), rc
+        assert sorted(rc["rehearsal_env"]) == ["NCCL_HOSTID", "NCCL_IB_DISABLE", "NCCL_SOCKET_IFNAME"], rc
+    else:
+        assert "rccl" not in line
     # the headline with inputs and results in pinned host memory (H2D / D2H inclusive)
     hr = line["host_resident"]
     assert "error" not in hr, hr

@@ -8,7 +8,8 @@ RCCL's point-to-point subset (tests/c_abi/rccl_p2p_double.cpp: ranks are
 threads, groups matched per (source, destination) at ncclGroupEnd, an
 unmatched or mis-sized send/recv fails).  Each rank's receive slot p must hold
 rank p's shard of this rank, its own slot untouched; every root's gather
-holds the ranks' shards in rank order.  What this cannot show is RCCL's own
+holds the ranks' shards in rank order; ``sa_comm_info`` reports W ranks and the
+rank's own index and device.  What this cannot show is RCCL's own
 behaviour on xGMI (the driver's 8-GPU run); it pins this file's indexing."""
 import os
 import shutil
