@@ -102,6 +102,19 @@ class SecureAggregator:
     def average(self, data: List, axis=None, weights=None):
         return self._aggregate(data, axis, weights, average=True)
 
+    def rollback(self) -> None:
+        """Undo the latest round's stream advance in every party: for lazy
+        runtimes, where a party's failure inside ``sum`` / ``average`` shows
+        only when the returned object is resolved (``reveal`` or a later
+        use).  Call it after such a failure, before the next round; every
+        party then masks the next round from the positions the failed round
+        started at, so the masks cancel again.  A no-op before any round or
+        when called twice."""
+        start = getattr(self, "_round_start", None)
+        if start is not None:
+            self._maskers = dict(start)
+            self._round_start = None
+
     # ------------------------------------------------------------ internals
     def _aggregate(self, data, axis, weights, average: bool):
         assert data, "Data to aggregate should not be None or empty!"
@@ -132,12 +145,18 @@ class SecureAggregator:
                     assert _party(w.device) == owners[i], (
                         "Device of weight does not match the corresponding data device.")
         masked, advanced = [], {}
+        self._round_start = None  # an eager failure below advances nothing: rollback() is then a no-op
         for d, w, owner in zip(data, ws, owners):
             m, nxt = d.device(P.mask_payload, num_returns=2)(self._maskers[owner], d, w, self._gpu_of(owner))
             advanced[owner] = nxt
             masked.append(m.to(self._device))
         # the streams moved on in every party (a round that failed part-way in
-        # an eager runtime raised above and leaves the old maskers in place)
+        # an eager runtime raised above and leaves the old maskers in place).
+        # A lazy runtime (Ray, real secretflow) reports a party's failure only
+        # when the round's result is resolved -- by then ``advanced`` holds
+        # failed futures; the maskers this round started from stay here so
+        # ``rollback()`` can put every party back at the same positions.
+        self._round_start = dict(self._maskers)
         self._maskers.update(advanced)
         self.last_masked = masked  # server-owned: what the server received
         server_ws = None

@@ -75,10 +75,22 @@ def _local(x, dev: PYU):
             raise ValueError(f"{x.device} object used on {dev}; move it with .to() first")
         return x.data
     if isinstance(x, (list, tuple)):
-        return type(x)(_local(v, dev) for v in x)
+        return _rebuild(x, [_local(v, dev) for v in x])
     if isinstance(x, dict):
         return {k: _local(v, dev) for k, v in x.items()}
     return x
+
+
+def _rebuild(x, items: list):
+    """``x`` (a list or tuple, possibly a subclass) with its elements replaced
+    by ``items``: ``x`` itself when nothing changed (so any subclass passes
+    through as before), a namedtuple from positional fields, otherwise
+    ``type(x)(items)``."""
+    if all(a is b for a, b in zip(x, items)):
+        return x
+    if hasattr(x, "_fields"):  # namedtuple: fields are positional arguments
+        return type(x)(*items)
+    return type(x)(items)
 
 
 def _move(data, dev: PYU):
@@ -87,7 +99,7 @@ def _move(data, dev: PYU):
     except ImportError:  # pragma: no cover
         torch = None
     if isinstance(data, (list, tuple)):
-        return type(data)(_move(d, dev) for d in data)
+        return _rebuild(data, [_move(d, dev) for d in data])
     if isinstance(data, dict):
         return {k: _move(v, dev) for k, v in data.items()}
     if torch is not None and isinstance(data, torch.Tensor):

@@ -16,6 +16,9 @@ there, and the driver only ever holds opaque handles.  Like secretflow:
   passing through it proves no client datum, masked vector or generator
   state reached the driver.
 
+``Cluster(..., lazy=True)`` defers a failing call's error to where its
+results are used (``reveal``, an argument of a later call), as Ray does.
+
 ``make_package(cluster)`` builds fake ``secretflow``, ``secretflow.security``
 and ``secretflow.security.aggregation`` modules whose ``SecureAggregator`` is
 a placeholder, for ``install()`` tests.
@@ -45,11 +48,29 @@ class Handle:
     oid: int
 
 
+@dataclass(frozen=True)
+class _Failed:
+    """A lazy cluster's result of a call that raised: stored in place of the
+    results, raised again wherever it is used (Ray's error propagation)."""
+    name: str
+    tb: str
+
+
+class UpstreamError(RuntimeError):
+    """A lazy cluster's object whose producing call failed."""
+
+
+def _check(v):
+    if isinstance(v, _Failed):
+        raise UpstreamError(f"{v.name} upstream:\n{v.tb}")
+    return v
+
+
 def _resolve(x, party, store):
     if isinstance(x, Handle):
         if x.party != party:
             raise ValueError(f"object of {x.party} used on {party}; move it with .to() first")
-        return store[x.oid]
+        return _check(store[x.oid])
     if isinstance(x, (list, tuple)):
         return type(x)(_resolve(v, party, store) for v in x)
     if isinstance(x, dict):
@@ -57,7 +78,7 @@ def _resolve(x, party, store):
     return x
 
 
-def _worker_main(party, conn, init, private):
+def _worker_main(party, conn, init, private, lazy=False):
     import cloudpickle
 
     if init is not None:
@@ -72,11 +93,19 @@ def _worker_main(party, conn, init, private):
             if op == "run":
                 fn_b, call_b, num_returns = args
                 fn = cloudpickle.loads(fn_b)
-                a, k = _resolve(cloudpickle.loads(call_b), party, store)
-                out = fn(*a, **k)
-                outs = list(out) if num_returns and num_returns > 1 else [out]
-                if num_returns and num_returns > 1 and len(outs) != num_returns:
-                    raise ValueError(f"{fn} returned {len(outs)} values, num_returns={num_returns}")
+                try:
+                    a, k = _resolve(cloudpickle.loads(call_b), party, store)
+                    out = fn(*a, **k)
+                    outs = list(out) if num_returns and num_returns > 1 else [out]
+                    if num_returns and num_returns > 1 and len(outs) != num_returns:
+                        raise ValueError(f"{fn} returned {len(outs)} values, num_returns={num_returns}")
+                except Exception as e:  # noqa: BLE001
+                    if not lazy:
+                        raise
+                    # lazy: the call "succeeds" with failed results; the error
+                    # surfaces where they are used
+                    f = _Failed(type(e).__name__, "".join(traceback.format_exception(e)))
+                    outs = [f] * (num_returns if num_returns and num_returns > 1 else 1)
                 oids = []
                 for o in outs:
                     oid = next(ids)
@@ -90,7 +119,7 @@ def _worker_main(party, conn, init, private):
                 store[oid] = pickle.loads(args[0])
                 res = oid
             elif op == "reveal":
-                v = store[args[0]]
+                v = _check(store[args[0]])
                 if private and not (isinstance(v, int) and not isinstance(v, bool)):
                     raise RevealRefused(f"reveal of a {type(v).__name__} owned by client {party}")
                 res = pickle.dumps(v)
@@ -108,7 +137,7 @@ class Cluster:
     values ``reveal`` refuses (all but public ints).  ``init``: a callable
     each process runs first (cloudpickled)."""
 
-    def __init__(self, parties, private=(), init=None):
+    def __init__(self, parties, private=(), init=None, lazy=False):
         import cloudpickle
 
         ctx = mp.get_context("spawn")
@@ -116,7 +145,7 @@ class Cluster:
         ib = cloudpickle.dumps(init) if init is not None else None
         for p in parties:
             parent, child = ctx.Pipe()
-            proc = ctx.Process(target=_worker_main, args=(p, child, ib, p in set(private)), daemon=True)
+            proc = ctx.Process(target=_worker_main, args=(p, child, ib, p in set(private), lazy), daemon=True)
             proc.start()
             self.workers[p] = (proc, parent)
         self.reveals = []  # (party, type) of every successful reveal

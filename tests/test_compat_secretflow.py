@@ -547,3 +547,46 @@ def test_party_functions_leave_their_masker_argument_alone(monkeypatch):
     assert m.peers == [] and m2.peers == ["bob"]
     wire, m3 = P.mask_payload(m2, np.ones(10, np.float32), None, None)
     assert m2.position("bob") == 0 and m3.position("bob") == 10 and wire.positions == {"bob": 0}
+
+
+def test_lazy_runtime_failed_round_rolls_back():
+    """under a lazy runtime (Ray, real secretflow) a party's
+    failure inside ``average`` shows only when the result is resolved; the
+    stored maskers are then failed futures and every later round fails.
+    ``rollback()`` restores the maskers the failed round started from in
+    every party, and the next round is bit-exact against the oracle at the
+    positions after the last good round."""
+    from sfl_amd.compat import secretflow as hip
+
+    c = fs.Cluster(NAMES + ["carol"], private=NAMES, init=_oracle_backend_init, lazy=True)
+    try:
+        seeds, pair = _seeds()
+        n = 37
+        rng = np.random.default_rng(7)
+        good = [[rng.standard_normal(n).astype(np.float32) for _ in NAMES] for _ in range(3)]
+
+        def run(agg, xs):
+            objs = [_put(c.pyu(nm), x) for nm, x in zip(NAMES, xs)]
+            return agg.average(objs)
+
+        def expect(xs, offset):
+            return o.secure_average(xs, NAMES, seeds=seeds, offset=offset)[0]
+
+        for use_rollback in (True, False):
+            agg = hip.SecureAggregator(c.pyu("carol"), [c.pyu(nm) for nm in NAMES], reveal=fs.reveal, seeds=pair)
+            assert np.array_equal(fs.reveal(run(agg, good[0])), expect(good[0], 0))
+            # alice's payload has a type the masker refuses: under the lazy
+            # runtime the call returns, the error surfaces at reveal
+            bad = [np.ones(n, dtype=np.complex64), good[1][1]]
+            res = run(agg, bad)
+            with pytest.raises(fs.RemoteError, match="UpstreamError"):
+                fs.reveal(res)
+            if use_rollback:
+                agg.rollback()
+                agg.rollback()  # twice: a no-op
+                assert np.array_equal(fs.reveal(run(agg, good[2])), expect(good[2], n))
+            else:  # the failed futures poison every later round
+                with pytest.raises(fs.RemoteError):
+                    fs.reveal(run(agg, good[2]))
+    finally:
+        c.close()
