@@ -730,7 +730,12 @@ def rank_main(args):
         # "rccl" record, which transport carried the exchange
         import tempfile
 
-        rccl_dir = tempfile.mkdtemp(prefix=f"sfl_rccl_rank{rank}_")
+        keep = os.environ.get("SFL_BENCH_RCCL_LOG_DIR")  # keep the logs there (else a temp dir, removed)
+        if keep:
+            rccl_dir = os.path.join(keep, f"rank{rank}")
+            os.makedirs(rccl_dir, exist_ok=True)
+        else:
+            rccl_dir = tempfile.mkdtemp(prefix=f"sfl_rccl_rank{rank}_")
         env = rank_comm_env(args, rank, multi, rccl_dir)
         if "NCCL_DEBUG_FILE" not in env:
             os.rmdir(rccl_dir)
@@ -888,7 +893,7 @@ def rccl_record(comm, rank: int, world: int, log_dir) -> dict:
     except Exception as e:  # noqa: BLE001 - recorded, never costs the headline
         info = {"error": str(e)[:200]}
     mine = rccl_log.rank_summary(rank, log_dir, info)
-    if log_dir:
+    if log_dir and not os.environ.get("SFL_BENCH_RCCL_LOG_DIR"):
         shutil.rmtree(log_dir, ignore_errors=True)
     box = [None] * world
     dist.all_gather_object(box, mine)

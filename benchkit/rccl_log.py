@@ -34,7 +34,10 @@ def debug_env(rank: int, log_dir: str) -> dict:
     it over, and the record then says so."""
     if os.environ.get("NCCL_DEBUG_FILE"):
         return {}
-    return {"NCCL_DEBUG": os.environ.get("NCCL_DEBUG", "INFO") or "INFO",
+    # INFO at least (the GPU box exports NCCL_DEBUG=VERSION, which logs no
+    # connection); it goes to the file, so the console stays as it was
+    level = os.environ.get("NCCL_DEBUG", "").upper()
+    return {"NCCL_DEBUG": level if level in ("INFO", "TRACE") else "INFO",
             "NCCL_DEBUG_SUBSYS": "INIT,P2P,SHM,NET",
             "NCCL_DEBUG_FILE": os.path.join(log_dir, f"rank{rank}.%p.log")}
 
@@ -112,10 +115,7 @@ def combine(per_rank: list, world: int) -> dict:
         nranks.update(log.get("nranks", []))
         nnodes.update(log.get("nnodes", []))
         lines += log.get("lines", 0)
-        c = r.get("comm") or {}
-        if c.get("nranks") is not None:
-            nranks.add(c["nranks"])
-        devices.append(c.get("device"))
+        devices.append((r.get("comm") or {}).get("device"))
     xgmi = None
     if transports:
         xgmi = all(k.startswith("P2P") for k in transports)

@@ -57,6 +57,10 @@ class MaskedPayload:
     positions: dict = field(default_factory=dict)  # peer -> stream position the round started at
 
 
+# large host payloads run chunked through three streams (_mask_vector_pipelined,
+# _sum_decode_pipelined); False restores the one-shot copies (tools/party_bench.py A/B)
+LARGE_PIPELINE = True
+
 # scratch of the blocking small-call library entries (sa_mask_host,
 # sa_sum_decode_host), per GPU of this process, grown to the largest call
 _SCRATCH: dict = {}
@@ -173,9 +177,8 @@ def mask_payload(masker: Masker, payload, weight=None, gpu: int | None = 0):
             groups.append(cur)
 
     start = {p: masker.position(p) for p in masker.peers}
-    out = np.empty(sum(sizes), dtype=np.uint64)
     bounds = np.cumsum([0] + sizes)
-    digest = 0
+    out, digest = None, 0
     for (xt, ct), lis, wvec in groups:
         lo, hi = int(bounds[lis[0]]), int(bounds[lis[-1] + 1])
         if hi == lo:
@@ -184,13 +187,20 @@ def mask_payload(masker: Masker, payload, weight=None, gpu: int | None = 0):
         wscalar = 1.0
         if weight is not None and not np.ndim(weight):
             wscalar = float(weight) if ct.kind == "f" else int(weight)
-        vec, extra = _mask_vector(masker, xs, xt, ct, wscalar, wvec, gpu)
-        out[lo:hi] = vec
+        vec, extra, dig = _mask_vector(masker, xs, xt, ct, wscalar, wvec, gpu)
+        if out is None and lo == 0 and hi == bounds[-1]:
+            out = vec  # one group: its (fresh) vector is the payload, no copy
+        else:
+            if out is None:
+                out = np.empty(int(bounds[-1]), dtype=np.uint64)
+            out[lo:hi] = vec
+        # the XOR digest of the whole payload is the XOR of the groups' digests
+        digest ^= dig if dig is not None else (int(np.bitwise_xor.reduce(vec)) if vec.size else 0)
         masker.consume(hi - lo)
         for peer, k in extra.items():
             masker.skip(peer, k)
-    if out.size:
-        digest = int(np.bitwise_xor.reduce(out))
+    if out is None:
+        out = np.zeros(int(bounds[-1]), dtype=np.uint64)
     return (MaskedPayload(masker.party, out, sizes, shapes, container, as_torch, digest, masker.fxp_bits, start),
             masker)
 
@@ -208,7 +218,9 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
     """One launch group on the party's GPU: ``sa_mask`` over the packed
     layers ``xs`` from the masker's current stream positions; a flagged raw
     0 is moved onto numpy's stream (``sa_stream_shift``).  Returns the host
-    uint64 vector and ``{peer: extra raw draws}``.
+    uint64 vector, ``{peer: extra raw draws}`` and its XOR digest when the
+    device formed it (None: the caller XORs the host vector).  Large host
+    layers take ``_mask_vector_pipelined``.
 
     The masked vector and the PRG flag word share one device buffer, so a
     small call (up to ``SMALL_CALL_BYTES``) brings both back with one copy
@@ -226,7 +238,14 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
     n = int(sum(int(np.prod(_shape_of(a))) for a in xs))
     small = 8 * n <= SMALL_CALL_BYTES
     streams = masker.streams()
-    if small and wvec is None and not any(isinstance(a, torch.Tensor) for a in xs):
+    host_layers = not any(isinstance(a, torch.Tensor) for a in xs)
+    if not small and wvec is None and host_layers and LARGE_PIPELINE:
+        # host layers of a large payload: chunked H2D / mask / D2H overlap
+        got = _mask_vector_pipelined(masker, xs, xt, ct, wscalar, gpu)
+        if got is not None:
+            return got
+        # numpy's rejection of a raw 0: the device path below re-positions the streams
+    if small and wvec is None and host_layers:
         # host layers of a small payload: ONE blocking library call
         flat = (np.asarray(xs[0], dtype=xt).reshape(-1) if len(xs) == 1 else
                 np.concatenate([np.asarray(a, dtype=xt).reshape(-1) for a in xs]))
@@ -234,7 +253,7 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
             pin, dbuf = _scratch(gpu, *K.mask_host_scratch(n, xt.itemsize))
             host, flag = K.mask_host(flat, ct, streams, pin, dbuf, weight=wscalar, fxp_bits=masker.fxp_bits)
         if not flag & L.SA_FLAG_PRG_REJECT:
-            return host, {}
+            return host, {}, None
         # numpy's rejection of a raw 0 (p = 2^-64 a draw): the device path below re-positions the streams
     with torch.cuda.device(dev):
         if not any(isinstance(a, torch.Tensor) for a in xs):
@@ -288,7 +307,82 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
             host = hv[:n].copy()
         else:
             host = K.as_u64(out)
-    return host, extra
+    return host, extra, None
+
+
+def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, gpu):
+    """A large launch group from host layers, chunked through three streams
+    (``sfl_amd/hostpipe.py``): chunk j's H2D straight from the caller's
+    registered layers, its ``sa_mask`` at stream offset ``lo`` (the XOR
+    digest accumulated on the device), its D2H straight into the fresh
+    result as soon as that chunk's pages are faulted in and registered --
+    the copies of different chunks overlap each other and the page faulting.
+    Bit-identical to one launch over the whole group (chunk j draws
+    positions [lo, hi) of every stream).  Returns (host uint64 vector, {},
+    digest), or None when the round drew a raw 0 (numpy's rejection: the
+    caller's device path replays it from the same positions)."""
+    import torch
+
+    from ... import _lib as L
+    from ... import hostpipe as H
+    from ... import kernels as K
+
+    dev = torch.device("cuda", gpu)
+    tdt = {_F32: torch.float32, _F64: torch.float64, _I64: torch.int64}
+    ph = H.Phases("mask_payload")
+    layers = H.host_layers(xs, xt)
+    n = int(sum(a.size for a in layers))
+    bounds = H.chunk_bounds(n)
+    out = H.FreshOutput(n, np.uint64, bounds)  # its pages start faulting in now
+    s_in, s_k, s_out = H.streams(dev)
+    try:
+        with torch.cuda.device(dev), H.Registered(layers) as reg:
+            ph.mark("register in")
+            cur = torch.cuda.current_stream(dev)
+            x = torch.empty(n, dtype=tdt[xt], device=dev)
+            buf = torch.empty(n + 2, dtype=K.U64, device=dev)  # masked vector | digest | flag word
+            res, dig, flags = buf[:n], buf[n:n + 1], buf[n + 1:].view(torch.int32)[:1]
+            buf[n:].zero_()
+            ready = torch.cuda.Event()
+            ready.record(cur)
+            s_in.wait_event(ready)
+            s_k.wait_event(ready)
+            done = []
+            for lo, hi in bounds:
+                e_in, e_k = torch.cuda.Event(), torch.cuda.Event()
+                with torch.cuda.stream(s_in):
+                    H.copy_pieces(x, reg.usable, lo, hi)
+                    e_in.record(s_in)
+                with torch.cuda.stream(s_k):
+                    s_k.wait_event(e_in)
+                    K.mask(x[lo:hi], res[lo:hi], masker.streams(offset=lo), weight=wscalar,
+                           compute_dtype=tdt[ct], fxp_bits=masker.fxp_bits, digest=dig, flags=flags)
+                    e_k.record(s_k)
+                done.append(e_k)
+            meta = torch.empty(2, dtype=K.U64, pin_memory=True)
+            with torch.cuda.stream(s_k):
+                meta.copy_(buf[n:], non_blocking=True)
+            ph.mark("enqueue")
+            for j, (lo, hi) in enumerate(bounds):
+                dst = torch.from_numpy(out.ready(j).view(np.int64))
+                with torch.cuda.stream(s_out):
+                    s_out.wait_event(done[j])
+                    dst.copy_(res[lo:hi], non_blocking=True)
+            ph.mark("d2h enqueue")
+            s_k.synchronize()
+            s_out.synchronize()
+            s_in.synchronize()
+            cur.wait_stream(s_k)  # x / buf were allocated on the current stream
+            ph.mark("wait")
+    finally:
+        out.close()
+    ph.mark("unregister")
+    ph.note(**out.stats)
+    ph.done()
+    digest, flag = int(meta[0]) & ((1 << 64) - 1), int(meta[1]) & 0xFFFFFFFF
+    if flag & L.SA_FLAG_PRG_REJECT:
+        return None
+    return out.array, {}, digest
 
 
 def _shape_of(a):
@@ -363,6 +457,8 @@ def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_t
             if int(g) != int(want) & ((1 << 64) - 1):
                 raise DigestMismatch(f"masked vector {i}: digest {int(g):016x}, sent {int(want):016x}")
         return result
+    if not small and not as_torch and divisor_vec is None and LARGE_PIPELINE:
+        return _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev)
     with torch.cuda.device(dev):
         if small and n:
             n_pad = n + (n & 1)  # rows 16-byte aligned
@@ -404,3 +500,77 @@ def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_t
                     raise DigestMismatch(f"masked vector {i}: digest {int(g):016x}, sent {int(want):016x}")
             return result
     return out if as_torch else out.cpu().numpy()
+
+
+def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
+    """The server's large host call, chunked through three streams
+    (``sfl_amd/hostpipe.py``): chunk j of every masked vector H2D straight
+    from the registered payloads, then on the device the per-vector XOR
+    digests (accumulated over chunks), the mod-2^64 sum and the decode of
+    chunk j, then its D2H straight into the fresh result as soon as that
+    chunk's pages are faulted in and registered -- overlapped with chunk
+    j+1's copies.  Same kernels and result as the one-shot path."""
+    import torch
+
+    from ... import hostpipe as H
+    from ... import kernels as K
+
+    C, n = len(u64s), int(u64s[0].size)
+    ph = H.Phases("sum_decode")
+    ins = [np.ascontiguousarray(u).reshape(-1).view(np.int64) for u in u64s]
+    bounds = H.chunk_bounds(n)
+    out = H.FreshOutput(n, np.float64, bounds)
+    s_in, s_k, s_out = H.streams(dev)
+    try:
+        with torch.cuda.device(dev), H.Registered(ins) as reg:
+            ph.mark("register in")
+            host_in = [torch.from_numpy(a) for a in reg.usable]
+            cur = torch.cuda.current_stream(dev)
+            vecs = [torch.empty(n, dtype=K.U64, device=dev) for _ in range(C)]
+            s = torch.empty(n, dtype=K.U64, device=dev)
+            dec = torch.empty(n, dtype=torch.float64, device=dev)
+            dig = torch.zeros(C, dtype=K.U64, device=dev)
+            ready = torch.cuda.Event()
+            ready.record(cur)
+            s_in.wait_event(ready)
+            s_k.wait_event(ready)
+            done = []
+            for lo, hi in bounds:
+                e_in, e_k = torch.cuda.Event(), torch.cuda.Event()
+                with torch.cuda.stream(s_in):
+                    for v, h in zip(vecs, host_in):
+                        v[lo:hi].copy_(h[lo:hi], non_blocking=True)
+                    e_in.record(s_in)
+                with torch.cuda.stream(s_k):
+                    s_k.wait_event(e_in)
+                    part = [v[lo:hi] for v in vecs]
+                    for i, v in enumerate(part):
+                        K.xor_digest(v, dig[i:i + 1])
+                    K.sum_u64(part, s[lo:hi])
+                    K.decode(s[lo:hi], dec[lo:hi], fxp_bits=fxp_bits, divisor=divisor)
+                    e_k.record(s_k)
+                done.append(e_k)
+            got_h = torch.empty(C, dtype=K.U64, pin_memory=True)
+            with torch.cuda.stream(s_k):
+                got_h.copy_(dig, non_blocking=True)
+            ph.mark("enqueue")
+            for j, (lo, hi) in enumerate(bounds):
+                dst = torch.from_numpy(out.ready(j))
+                with torch.cuda.stream(s_out):
+                    s_out.wait_event(done[j])
+                    dst.copy_(dec[lo:hi], non_blocking=True)
+            ph.mark("d2h enqueue")
+            s_k.synchronize()
+            s_out.synchronize()
+            s_in.synchronize()
+            cur.wait_stream(s_k)
+            ph.mark("wait")
+    finally:
+        out.close()
+    ph.mark("unregister")
+    ph.note(**out.stats)
+    ph.done()
+    for i, (g, want) in enumerate(zip(got_h.numpy().view(np.uint64).tolist(), digests)):
+        if int(g) != int(want) & ((1 << 64) - 1):
+            raise DigestMismatch(f"masked vector {i}: digest {int(g):016x}, sent {int(want):016x}")
+    return out.array

@@ -48,7 +48,7 @@ def _mask_vector(masker, xs, xt, ct, wscalar, wvec, gpu):
             assert k < 64, "stream position lost"
         if k:
             extra[peer] = k
-    return out, extra
+    return out, extra, None  # no device digest: mask_payload XORs the host vector
 
 
 def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_torch):

@@ -514,7 +514,27 @@ def test_rccl_log_parse_and_combine():
 def test_rccl_debug_env_respects_a_caller_log(monkeypatch):
     from benchkit import rccl_log as R
 
+    monkeypatch.setenv("NCCL_DEBUG", "VERSION")  # what the GPU box exports: too quiet for the record
+    assert R.debug_env(0, "/x")["NCCL_DEBUG"] == "INFO"
+    monkeypatch.setenv("NCCL_DEBUG", "trace")
+    assert R.debug_env(0, "/x")["NCCL_DEBUG"] == "TRACE"
+
     monkeypatch.setenv("NCCL_DEBUG_FILE", "/somewhere/else.log")
     assert R.debug_env(0, "/x") == {}
     rec = R.rank_summary(0, None, {"nranks": 2})
     assert rec["log"] is None and "NCCL_DEBUG_FILE" in rec["note"]
+
+
+def test_rccl_log_parse_real_rehearsal_log():
+    """A real RCCL init log (rank 0 of `bench.py --gpus 2 --rehearse-one-gpu`
+    on the MI355X box, NCCL_DEBUG=INFO via benchkit/rccl_log.py): torch's
+    process group and our RcclComm, two ranks, each its own RCCL node over
+    sockets (NCCL_HOSTID) -- the parser sees only NET/Socket connections."""
+    from benchkit import rccl_log as R
+
+    text = open(os.path.join(ROOT, "tests", "golden", "rccl_init_rehearsal_w2_rank0.log")).read()
+    s = R.summarise(text)
+    assert set(s["transports"]) == {"NET/Socket"} and s["transports"]["NET/Socket"] >= 8
+    assert s["nranks"] == [2] and s["nnodes"] == [2]
+    c = R.combine([{"rank": 0, "comm": {"nranks": 2, "rank": 0, "device": 0}, "log": s}], 2)
+    assert c["xgmi"] is False and c["nranks"] == 2

@@ -453,3 +453,67 @@ def test_small_call_party_counts_containers_and_weights(parties, dtype):
         exp = o.secure_average(flat, names, weights=ws, seeds=seeds, offset=off)[0]
         assert np.array_equal(np.concatenate([g.reshape(-1) for g in got]), exp), rnd
         off += 22
+
+
+@pytest.mark.parametrize("dtype", [np.int64, np.float64])
+def test_general_one_call_matches_general_path(dtype, monkeypatch):
+    """small float64 / int64 host calls of 2..9 parties take ONE
+    blocking library call (``_host_general_one_call`` -> sa_clients_host).
+    The same two rounds with that path forced off (the general per-launch
+    path) give identical results, identical per-party digests and identical
+    masker positions afterwards; both equal the oracle (digests of the
+    oracle's masked vectors, decoded averages)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    names = ["alice", "bob", "carol", "dave"]
+    seeds = o.seeds_for(names)
+    pair = {(a, b): seeds[a][b] for a in names for b in names if a != b}
+    pyus = [PYU(nm, 0) for nm in names]
+    rng = np.random.default_rng(11)
+
+    def layers():
+        if dtype == np.int64:
+            return [rng.integers(-1000, 1000, (3, 5)).astype(np.int64), rng.integers(-9, 9, 7).astype(np.int64)]
+        return [rng.standard_normal((3, 5)), rng.standard_normal(7)]
+
+    rounds = [[layers() for _ in names] for _ in range(2)]
+    weights = [3, 1, 4, 2] if dtype == np.int64 else [0.5, 1.25, 2.0, 0.75]
+
+    def run(one_call: bool):
+        agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
+        calls = []
+        orig = agg._host_general_one_call
+
+        def spy(*a, **k):
+            r = orig(*a, **k) if one_call else None
+            calls.append(r is not None)
+            return r
+
+        monkeypatch.setattr(agg, "_host_general_one_call", spy)
+        outs = []
+        for data in rounds:
+            got = rv(agg.average([p(lambda d=d: d)() for p, d in zip(pyus, data)], axis=0, weights=weights))
+            digs = [np.asarray(d.cpu() if hasattr(d, "cpu") else d).view(np.uint64).copy()
+                    for d in agg.last_digests if d is not None]
+            outs.append((got, digs))
+        pos = {nm: {p: agg._maskers[nm].position(p) for p in names if p != nm} for nm in names}
+        return outs, pos, calls
+
+    a, pos_a, calls_a = run(True)
+    b, pos_b, calls_b = run(False)
+    assert calls_a == [True, True] and calls_b == [False, False]
+    assert pos_a == pos_b
+    n = 22
+    assert all(v == 2 * n for d in pos_a.values() for v in d.values())
+    for r, ((ga, da), (gb, db)) in enumerate(zip(a, b)):
+        for la, lb in zip(ga, gb):
+            assert la.dtype == lb.dtype and np.array_equal(la, lb), r
+        flat = [np.concatenate([x.reshape(-1) for x in d]) for d in rounds[r]]
+        exp_avg, _, masked = o.secure_average(flat, names, weights=weights, seeds=seeds, offset=r * n)
+        assert np.array_equal(np.concatenate([x.reshape(-1) for x in ga]), exp_avg), r
+        want = [o.digest(m) for m in masked]
+        assert [int(x) for x in np.concatenate(da)] == want, r
+        assert [int(x) for x in np.concatenate(db)] == want, r

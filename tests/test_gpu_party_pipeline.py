@@ -1,0 +1,163 @@
+"""The drop-in's large-payload path: party.mask_payload
+and party.sum_decode on host payloads above SMALL_CALL_BYTES run chunked
+through three streams (sfl_amd/hostpipe.py: the caller's arrays registered
+in place, chunk j's H2D / kernels / D2H overlapping chunk j+1's).  Checked
+in-process, as a secretflow PYU would run the functions, against the numpy
+oracle: every party's masked vector and XOR digest bit-exact, the stream
+positions, the decoded result bit-exact -- over several rounds, layer lists
+that straddle chunk joins, every compute type, a non-contiguous and a
+read-only input (the registration fallback), a forced raw-0 rejection, and
+the per-element-weight / torch payloads that keep the one-shot path."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import secagg as o  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+NAMES = ["alice", "bob", "carol"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sfl_amd import _lib as L
+
+    L.lib()
+
+
+def _maskers(seeds):
+    from sfl_amd.security.aggregation import party as P
+
+    out = {}
+    for nm in NAMES:
+        m = P.new_masker(nm)
+        out[nm] = P.agree(m, {p: 0 for p in NAMES}, {p: seeds[nm][p] for p in NAMES if p != nm})
+    return out
+
+
+def _expected(layers, w, name, seeds, offset):
+    q = np.concatenate([o.quantize(a, None if w is None else (np.broadcast_to(w, np.shape(a)) if np.ndim(w) else w))
+                        .reshape(-1) for a in layers])
+    return o.mask_client(q, name, seeds[name], offset)
+
+
+def _payloads(kind, rng):
+    """One party's layers for a round kind (sizes well above 1 MiB)."""
+    if kind == "f32":
+        return [(rng.standard_normal(2_500_003) * 1e-2).astype(np.float32)]
+    if kind == "f32_layers":  # several layers, joins inside chunks
+        return [(rng.standard_normal((1000, 1500)) * 0.1).astype(np.float32),
+                (rng.standard_normal(700_003) * 0.1).astype(np.float32), np.zeros(0, np.float32),
+                (rng.standard_normal(1_100_001) * 0.1).astype(np.float32)]
+    if kind == "f64":
+        return [rng.standard_normal(1_200_007)]
+    if kind == "i64":
+        return [rng.integers(-1000, 1000, 600_001).astype(np.int64), rng.integers(-9, 9, 700_000).astype(np.int64)]
+    if kind == "mixed":  # two launch groups, both large
+        return [(rng.standard_normal(1_500_000) * 0.1).astype(np.float32), rng.standard_normal(300_001)]
+    if kind == "noncontig":
+        return [(rng.standard_normal((2000, 1501)) * 0.1).astype(np.float32).T]
+    if kind == "readonly":
+        a = (rng.standard_normal(1_300_000) * 0.1).astype(np.float32)
+        ro = np.frombuffer(a.tobytes(), dtype=np.float32)
+        assert not ro.flags.writeable
+        return [ro]
+    raise ValueError(kind)
+
+
+WEIGHTS = {"f32": None, "f32_layers": 0.75, "f64": np.float64(1.5), "i64": 3, "mixed": 2.0,
+           "noncontig": None, "readonly": 1.25}
+
+
+def test_large_payload_rounds_bit_exact():
+    from sfl_amd.security.aggregation import party as P
+
+    seeds = o.seeds_for(NAMES)
+    maskers = _maskers(seeds)
+    rng = np.random.default_rng(5)
+    offset = 0
+    for kind in ["f32", "f32_layers", "f64", "i64", "mixed", "noncontig", "readonly", "f32"]:
+        w = WEIGHTS[kind]
+        layers = {nm: _payloads(kind, rng) for nm in NAMES}
+        wires = []
+        for nm in NAMES:
+            payload = layers[nm] if len(layers[nm]) > 1 else layers[nm][0]
+            wire, maskers[nm] = P.mask_payload(maskers[nm], payload, w, gpu=0)
+            exp = _expected(layers[nm], w, nm, seeds, offset)
+            assert wire.u64.dtype == np.uint64 and np.array_equal(wire.u64, exp), (kind, nm)
+            assert wire.digest == o.digest(exp), (kind, nm)
+            assert wire.positions == {p: offset for p in NAMES if p != nm}
+            wires.append(wire)
+        n = sum(int(np.prod(np.shape(a))) for a in layers["alice"])
+        for average in (False, True):
+            got = P.sum_decode(*wires, weights=None if w is None else [w] * 3, average=average, gpu=0)
+            flat = np.concatenate([np.asarray(g).reshape(-1) for g in (got if isinstance(got, list) else [got])])
+            div = None if not average else (3 if w is None else float(sum([w] * 3)))
+            assert np.array_equal(flat, o.decode(o.server_sum([x.u64 for x in wires]), 18, div)), (kind, average)
+        offset += n
+
+
+def test_server_detects_a_changed_large_vector():
+    from sfl_amd.security.aggregation import party as P
+
+    seeds = o.seeds_for(NAMES)
+    maskers = _maskers(seeds)
+    x = (np.random.default_rng(1).standard_normal(1_000_000) * 0.1).astype(np.float32)
+    wires = [P.mask_payload(maskers[nm], x, None, gpu=0)[0] for nm in NAMES]
+    wires[1].u64[777_777] ^= np.uint64(1)
+    with pytest.raises(P.DigestMismatch, match="masked vector 1"):
+        P.sum_decode(*wires, gpu=0)
+
+
+def test_large_payload_rejection_replays_on_numpys_stream():
+    """A raw 0 on the (alice, bob) stream at element 1_500_000 of a 2M round:
+    the pipelined launch flags it, the device path replays the round from
+    the same positions and moves the stream one raw draw further -- numpy's
+    Generator.integers rejection (OracleMaskers)."""
+    from test_gpu_rejection import forced_zero_state
+
+    from sfl_amd.security.aggregation import party as P
+
+    state = {("alice", "bob"): forced_zero_state(1_500_000)}
+    ora = o.OracleMaskers(NAMES[:2], state)
+    ms = {}
+    for nm in NAMES[:2]:
+        m = P.new_masker(nm)
+        peer = [p for p in NAMES[:2] if p != nm][0]
+        ms[nm] = P.agree(m, {p: 0 for p in NAMES[:2]}, {peer: state[("alice", "bob")]})
+    rng = np.random.default_rng(3)
+    n = 2_000_000
+    for rnd in range(2):
+        xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in NAMES[:2]]
+        wires = []
+        for nm, x in zip(NAMES[:2], xs):
+            wire, ms[nm] = P.mask_payload(ms[nm], x, None, gpu=0)
+            wires.append(wire)
+        masked, ssum = ora.round(xs)
+        for wire, m in zip(wires, masked):
+            assert np.array_equal(wire.u64, m) and wire.digest == o.digest(m), rnd
+        assert np.array_equal(P.sum_decode(*wires, gpu=0), o.decode(ssum)), rnd
+        assert wires[0].positions == {"bob": rnd * (n + 1)}
+
+
+def test_per_element_weights_and_torch_payloads_keep_the_one_shot_path(monkeypatch):
+    from sfl_amd.security.aggregation import party as P
+
+    calls = []
+    orig = P._mask_vector_pipelined
+    monkeypatch.setattr(P, "_mask_vector_pipelined", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    seeds = o.seeds_for(NAMES)
+    maskers = _maskers(seeds)
+    n = 400_000
+    rng = np.random.default_rng(9)
+    w = rng.uniform(0.5, 2.0, n)
+    x = (rng.standard_normal(n) * 0.1).astype(np.float32)
+    wire, _ = P.mask_payload(maskers["alice"], x, w, gpu=0)
+    assert np.array_equal(wire.u64, _expected([x], w, "alice", seeds, 0))
+    t = torch.from_numpy(x).to("cuda:0")
+    wire, _ = P.mask_payload(maskers["alice"], t, None, gpu=0)
+    assert np.array_equal(wire.u64, _expected([x], None, "alice", seeds, 0))
+    assert calls == []

@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""The drop-in's per-party functions on large host payloads, timed in one
+process as secretflow PYUs would run them: C parties'
+``party.mask_payload`` (host fp32 in -> masked uint64 host vector out), then
+the server's ``party.sum_decode`` (C host uint64 vectors in -> float64 host
+result out), against the copy floors measured in the same process:
+
+  client floor  H2D of the party's 4n bytes and D2H of its 8n bytes, pinned
+                buffers, both directions at once (two streams)
+  server floor  H2D of the C x 8n masked bytes and D2H of the 8n result,
+                pinned, both directions at once
+
+Prints one JSON line: per-party and server milliseconds (median of --reps),
+the floors, and the fraction floor / measured; with --ab also the one-shot
+path (party.LARGE_PIPELINE = False) for comparison.  Each round's outputs
+are checked against the previous implementation's bit for bit when --ab.
+usage: python tools/party_bench.py [--clients 8] [--elems 100000000] [--reps 3] [--ab]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def floor_ms(torch, dev, h2d_bytes, d2h_bytes, reps=5):
+    src = torch.empty(h2d_bytes, dtype=torch.uint8, pin_memory=True)
+    dst = torch.empty(d2h_bytes, dtype=torch.uint8, pin_memory=True)
+    d_in = torch.empty(h2d_bytes, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(d2h_bytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    ts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s1):
+            d_in.copy_(src, non_blocking=True)
+        with torch.cuda.stream(s2):
+            dst.copy_(d_out, non_blocking=True)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts[1:]) * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--elems", type=int, default=100_000_000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--ab", action="store_true")
+    a = ap.parse_args()
+    import torch
+
+    from oracle import secagg as o
+    from sfl_amd.security.aggregation import party as P
+
+    C, n = a.clients, a.elems
+    names = [f"client{c}" for c in range(C)]
+    seeds = o.seeds_for(names)
+    dev = torch.device("cuda", 0)
+    xs = []
+    for c in range(C):
+        g = torch.Generator(device=dev).manual_seed(20260116 + c)
+        xs.append((torch.randn(n, generator=g, device=dev) * 1e-2).cpu().numpy())
+    res = {"clients": C, "elems": n, "reps": a.reps}
+
+    def maskers():
+        out = {}
+        for nm in names:
+            m = P.new_masker(nm)
+            out[nm] = P.agree(m, {p: 0 for p in names}, {p: seeds[nm][p] for p in names if p != nm})
+        return out
+
+    def run(tag):
+        ms = maskers()
+        client_t, server_t = [], []
+        wires = None
+        out = None
+        for r in range(a.reps + 1):  # the first round warms up
+            # the previous round's results are freed here, outside the timed calls
+            wires = out = None
+            wires = []
+            for nm, x in zip(names, xs):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                wire, ms[nm] = P.mask_payload(ms[nm], x, None, gpu=0)
+                client_t.append((r, time.perf_counter() - t0))
+                wires.append(wire)
+            t0 = time.perf_counter()
+            out = P.sum_decode(*wires, average=True, gpu=0)
+            server_t.append((r, time.perf_counter() - t0))
+        cm = statistics.median([t for r, t in client_t if r > 0]) * 1e3
+        sm = statistics.median([t for r, t in server_t if r > 0]) * 1e3
+        res[tag] = {"client_ms": cm, "server_ms": sm,
+                    "client_GBps": 12 * n / cm / 1e6, "server_GBps": 8 * (C + 1) * n / sm / 1e6,
+                    "round_grad_elems_per_s": C * n / ((C * cm + sm) / 1e3)}
+        return out, wires
+
+    out, wires = run("pipelined")
+    cf = floor_ms(torch, dev, 4 * n, 8 * n)
+    sf = floor_ms(torch, dev, 8 * C * n, 8 * n)
+    res["client_floor_ms"], res["server_floor_ms"] = cf, sf
+    res["pipelined"]["client_vs_floor"] = cf / res["pipelined"]["client_ms"]
+    res["pipelined"]["server_vs_floor"] = sf / res["pipelined"]["server_ms"]
+    if a.ab:
+        P.LARGE_PIPELINE = False
+        out1, wires1 = run("one_shot")
+        P.LARGE_PIPELINE = True
+        res["one_shot"]["client_vs_floor"] = cf / res["one_shot"]["client_ms"]
+        res["one_shot"]["server_vs_floor"] = sf / res["one_shot"]["server_ms"]
+        res["bit_identical"] = bool(np.array_equal(out, out1) and all(
+            np.array_equal(w.u64, w1.u64) and w.digest == w1.digest for w, w1 in zip(wires, wires1)))
+    res["note"] = ("in-process: every party's mask_payload then the server's sum_decode (average), fp32 host "
+                   "inputs, uint64 masked host vectors, float64 host result; floors: pinned copies of the same "
+                   "bytes, H2D and D2H on two streams at once")
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
