@@ -1049,7 +1049,9 @@ def extra_measurements(args, xs, plan, gens, K, torch, dev) -> dict:
     dev_x = torch.empty((C, N), dtype=torch.float32, device=dev)
     dec = torch.empty(N, dtype=torch.float64, device=dev)
     s_h2d, s_cmp, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    bounds = chunk_bounds(N, 16)
+    # ~64 MB of inputs a chunk, 2..16 chunks (config 2's 160 MB in 16 chunks
+    # spent its time in per-chunk host overhead: 10 ms against a 3.5 ms copy)
+    bounds = chunk_bounds(N, max(2, min(16, (4 * C * N) // (64 << 20))))
     cg = [plan_generators_full(plan, lo) for lo, _ in bounds]
 
     def host_round(with_images: bool):
@@ -1080,8 +1082,8 @@ def extra_measurements(args, xs, plan, gens, K, torch, dev) -> dict:
         res.update({f"{key}_ms": t * 1e3, f"{key}_grad_elems_per_s": C * N / t,
                     f"{key}_pcie_bytes": {"h2d": h2d, "d2h": d2h}})
     res["host_resident_note"] = ("pinned host fp32 inputs -> H2D -> fused quantize+mask+sum -> decode -> D2H of the "
-                                 "float64 aggregate (and of every client's masked u64 vector), 16 chunks, H2D / "
-                                 "compute / D2H on three streams" + ("" if images else
+                                 f"float64 aggregate (and of every client's masked u64 vector), {len(bounds)} chunks, "
+                                 "H2D / compute / D2H on three streams" + ("" if images else
                                  "; no wire-image variant: 8*C*N bytes of pinned host memory exceed 16 GiB"))
     # the copy floor of the same bytes: the H2D of every client's input alone,
     # pinned, in the same chunks (the host-resident round cannot beat it)

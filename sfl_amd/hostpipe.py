@@ -7,15 +7,16 @@ MI355X: ~57 GB/s each way, ~79 GB/s both ways at once; a pageable copy
 runs at the same rate but blocks the host until it is done), not the
 kernels (a 100M-element party mask is ~0.5 ms of device time).  So:
 
-* the caller's host arrays are HIP-registered in place for the call
-  (``hipHostRegister``: no staging copy through a pinned bounce buffer);
-* the result goes into a FRESH host array (the caller keeps it): anonymous
-  memory whose chunks are faulted in by a thread pool (first touch of fresh
-  memory runs at ~14 GB/s on one thread) and registered chunk by chunk, so
-  chunk j's D2H starts while later chunks are still being faulted in;
-* the element range is cut into chunks; chunk j's H2D (one stream), its
-  kernels (a second) and its D2H (a third) overlap with chunk j+1's, the
-  streams ordered by events.
+* the caller's host arrays are copied from where they are (no staging copy
+  into pinned memory), by a helper thread (``Feeder``): a pageable copy
+  runs at the pinned rate but blocks the thread that issues it;
+* the result goes into a FRESH host array (the caller keeps it) whose
+  chunks a thread pool faults in ahead of the copies (first touch of fresh
+  memory is the cost), chunk j's D2H a pageable copy as soon as its pages
+  are in, while later chunks are still being faulted in;
+* the element range is cut into chunks; chunk j's H2D (the feeder's
+  stream), its kernels (a second) and its D2H (a third, from the calling
+  thread) overlap with chunk j+1's, the streams ordered by events.
 
 Nothing here computes: the kernels are the library's (``sa_mask``,
 ``sa_xor_u64``, ``sa_sum_u64``, ``sa_decode``).  Used by
@@ -33,20 +34,12 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-_HIP = None
 _POOL = None
 # SFL_HOSTPIPE_TRACE=1: every pipelined call prints its phase times to stderr
 TRACE = os.environ.get("SFL_HOSTPIPE_TRACE") == "1"
 _POOL_LOCK = threading.Lock()
 TOUCH_THREADS = 8
 PAGE = 4096
-
-
-def _hip():
-    global _HIP
-    if _HIP is None:
-        _HIP = ctypes.CDLL("libamdhip64.so")
-    return _HIP
 
 
 def _pool() -> ThreadPoolExecutor:
@@ -70,130 +63,224 @@ def chunk_bounds(n: int, target: int = 8, lo_elems: int = 1 << 20, hi_elems: int
 
 class FreshOutput:
     """A fresh host result of ``n`` elements that the device fills chunk by
-    chunk: page-aligned anonymous memory (``mmap``) whose chunks are faulted
-    in by the thread pool, in chunk order, from construction on; ``ready(j)``
-    waits for chunk j's pages and HIP-registers exactly them, so chunk j's
-    D2H can start while later chunks are still being faulted in (first touch
-    of fresh memory is the cost: ~14 GB/s on one thread).  ``array`` is the
-    caller's result (it keeps the mapping alive); ``close()`` unregisters.
-    A chunk whose registration is refused is copied pageable (correct,
-    synchronous)."""
+    chunk.  ``np.empty`` memory (numpy advises huge pages for large
+    allocations: its first touch runs at ~27 GB/s on one thread, against
+    ~8 GB/s for a plain anonymous mmap -- tools/touch_probe.py), faulted in
+    by the thread pool in chunk order from construction on; ``ready(j)``
+    waits for chunk j's pages.  The D2H into a ready chunk is a pageable
+    copy (55 GB/s into touched pages, like a registered one): registering a
+    fresh result costs more than it saves (hipHostRegister takes the mm lock
+    and stalls the faulting threads).  ``array`` is the caller's result."""
 
     def __init__(self, n: int, dtype, bounds):
-        import mmap
-
-        self.dtype = np.dtype(dtype)
-        nbytes = n * self.dtype.itemsize
-        self.size = max(PAGE, -(-nbytes // PAGE) * PAGE)
-        # private anonymous pages (Python's default for fd -1 is MAP_SHARED:
-        # shmem-backed pages, slower to fault and to register)
-        self._mm = mmap.mmap(-1, self.size, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
-        self.array = np.frombuffer(self._mm, dtype=self.dtype, count=n)
-        self._b = np.frombuffer(self._mm, dtype=np.uint8)
-        self.base = self.array.ctypes.data
+        dtype = np.dtype(dtype)
         self.bounds = bounds
-        self.registered = []
-        self.stats = {"wait_ms": 0.0, "register_ms": 0.0, "refused": 0}
+        self.stats = {"wait_ms": 0.0, "pooled": False}
+        self._futs = [[] for _ in bounds]
+        owner = RESULTS.take(n * dtype.itemsize)
+        if owner is not None:  # a recycled, registered buffer: no faults, async DMA
+            self.array = owner[:n * dtype.itemsize].view(dtype)
+            self.stats["pooled"] = True
+            return
+        self.array = np.empty(n, dtype=dtype)
+        self._b = self.array.view(np.uint8).reshape(-1)
+        isz = dtype.itemsize
         pool = _pool()
         self._futs = []
         for lo, hi in bounds:
-            b0, b1 = self._span(lo, hi)
+            b0, b1 = lo * isz, hi * isz
             step = max(PAGE, -(-(b1 - b0) // TOUCH_THREADS) // PAGE * PAGE)
             self._futs.append([pool.submit(self._touch, a, min(b1, a + step)) for a in range(b0, b1, step)])
 
-    def _span(self, lo: int, hi: int) -> tuple[int, int]:
-        """Byte range of elements [lo, hi), widened to whole pages (chunk
-        starts are page-aligned: chunk_bounds aligns them to 1024 elements)."""
-        isz = self.dtype.itemsize
-        return (lo * isz) // PAGE * PAGE, min(self.size, -(-(hi * isz) // PAGE) * PAGE)
-
     def _touch(self, a: int, b: int) -> None:
         self._b[a:b:PAGE] = 0
+        self._b[b - 1] = 0  # the last page of the range
 
     def ready(self, j: int) -> np.ndarray:
-        """Chunk j's elements, faulted in and (when the driver accepts it)
-        registered."""
+        """Chunk j's elements, faulted in."""
         t0 = time.perf_counter()
         for f in self._futs[j]:
             f.result()
-        t1 = time.perf_counter()
+        self.stats["wait_ms"] += 1e3 * (time.perf_counter() - t0)
         lo, hi = self.bounds[j]
-        b0, b1 = self._span(lo, hi)
-        if b1 > b0:
-            hip = _hip()
-            rc = hip.hipHostRegister(ctypes.c_void_p(self.base + b0), ctypes.c_size_t(b1 - b0), ctypes.c_uint(0))
-            if rc == 0:
-                self.registered.append(self.base + b0)
-            else:
-                hip.hipGetLastError()
-                self.stats["refused"] += 1
-        self.stats["wait_ms"] += 1e3 * (t1 - t0)
-        self.stats["register_ms"] += 1e3 * (time.perf_counter() - t1)
         return self.array[lo:hi]
 
     def close(self) -> None:
         for f in (f for fs in self._futs for f in fs):
             f.result()  # no toucher may outlive the call
-        hip = _hip()
-        while self.registered:
-            hip.hipHostUnregister(ctypes.c_void_p(self.registered.pop()))
 
 
-class Registered:
-    """hipHostRegister the given C-contiguous numpy arrays for a ``with``
-    block, so device copies run as true async DMA from / into them;
-    unregistered on exit, whatever happened.  ``usable[i]`` is the array to
-    copy through: ``arrays[i]`` itself, or -- when its pages cannot be
-    registered (already registered by someone else, or sharing a page with
-    memory that is) -- a page-locked copy (an input) or a page-locked
-    stand-in whose contents ``__exit__`` copies back (an output,
-    ``outputs``).  Empty arrays are passed through."""
+class ResultPool:
+    """Registered host buffers for the pipelined results, recycled once the
+    caller has dropped every array that views them: a per-party masked
+    vector is shipped and dropped every round, so from the second round on
+    its D2H lands in registered pages without a fault (the fresh-result path
+    pays ~6 ms of page faults and a pageable copy per 800 MB).  A buffer is
+    free when nothing but the pool references it (``sys.getrefcount``: every
+    numpy view of it holds its owner).  New buffers are made on a miss while
+    the pool holds less than ``cap`` bytes (SFL_HOSTPIPE_POOL_BYTES, default
+    8 GiB; 0 disables), at the cost of one fresh result (parallel first
+    touch, then one registration); beyond the cap, results are fresh arrays
+    again."""
 
-    def __init__(self, arrays, outputs=()):
-        self.arrays = list(arrays)
-        self.outputs = {id(a) for a in outputs}  # stand-ins of these are copied back on exit
-        self.done, self.back = [], []
-        self.usable = []
+    def __init__(self, cap: int):
+        self.cap = cap
+        self.bufs: list = []
+        self.lock = threading.Lock()
 
-    def __enter__(self):
+    def take(self, nbytes: int):
+        if nbytes < (8 << 20) or self.cap <= 0:
+            return None
+        with self.lock:
+            best = None
+            for i in range(len(self.bufs)):
+                if self.bufs[i].nbytes >= nbytes and sys.getrefcount(self.bufs[i]) == 2:
+                    if best is None or self.bufs[i].nbytes < self.bufs[best].nbytes:
+                        best = i
+            if best is not None:
+                return self.bufs[best]
+            if sum(b.nbytes for b in self.bufs) + nbytes > self.cap:
+                return None
+            owner = np.empty(nbytes, dtype=np.uint8)
+            step = -(-nbytes // TOUCH_THREADS) // PAGE * PAGE + PAGE
+
+            def touch(lo):
+                owner[lo:lo + step:PAGE] = 0
+
+            list(_pool().map(touch, range(0, nbytes, step)))
+            hip = _hip()
+            if hip.hipHostRegister(ctypes.c_void_p(owner.ctypes.data), ctypes.c_size_t(nbytes), ctypes.c_uint(0)):
+                hip.hipGetLastError()
+                return None
+            self.bufs.append(owner)
+            return owner
+
+    def clear(self) -> None:
+        """Unregister and drop every free buffer (tests, memory pressure)."""
+        with self.lock:
+            keep = []
+            for i in range(len(self.bufs)):
+                if sys.getrefcount(self.bufs[i]) == 2:
+                    _hip().hipHostUnregister(ctypes.c_void_p(self.bufs[i].ctypes.data))
+                else:
+                    keep.append(self.bufs[i])
+            self.bufs = keep
+
+
+RESULTS = ResultPool(int(os.environ.get("SFL_HOSTPIPE_POOL_BYTES", str(8 << 30))))
+
+
+class Feeder:
+    """The H2D side of a pipelined call, on a helper thread: ``jobs[j]()``
+    issues chunk j's host-to-device copies on ``stream`` (the caller's own
+    pageable arrays: a pageable copy runs at the pinned rate but blocks the
+    thread that issues it -- tools/pcie_paths.py -- so it gets a thread of
+    its own; registering the arrays instead costs up to 8 ms per 800 MB and
+    stalls page faults elsewhere).  ``ready(j)`` returns the device event
+    that chunk j's copies complete at, once they are issued."""
+
+    def __init__(self, stream, jobs):
+        self.stream, self.jobs = stream, jobs
+        self.flags = [threading.Event() for _ in jobs]
+        self.events = [None] * len(jobs)
+        self.error = None
+        self.thread = threading.Thread(target=self._run, name="sfl_sa_h2d", daemon=True)
+        self.thread.start()
+
+    def _run(self) -> None:
         import torch
 
-        hip = _hip()
         try:
-            for a in self.arrays:
-                if not a.flags.c_contiguous:
-                    raise ValueError("only C-contiguous arrays can be registered")
-                if a.nbytes == 0:
-                    self.usable.append(a)
-                    continue
-                rc = hip.hipHostRegister(ctypes.c_void_p(a.ctypes.data), ctypes.c_size_t(a.nbytes),
-                                         ctypes.c_uint(0))
-                if rc == 0:
-                    self.done.append(a)
-                    self.usable.append(a)
-                    continue
+            with torch.cuda.device(self.stream.device), torch.cuda.stream(self.stream):
+                for j, job in enumerate(self.jobs):
+                    job()
+                    e = torch.cuda.Event()
+                    e.record(self.stream)
+                    self.events[j] = e
+                    self.flags[j].set()
+        except BaseException as ex:  # noqa: BLE001 - re-raised in the caller's thread
+            self.error = ex
+            for f in self.flags:
+                f.set()
+
+    def ready(self, j: int):
+        self.flags[j].wait()
+        if self.error is not None:
+            raise self.error
+        return self.events[j]
+
+    def join(self) -> None:
+        self.thread.join()
+        if self.error is not None:
+            raise self.error
+
+
+class Issued:
+    """``Feeder``'s interface for inputs that need no thread (registered):
+    every chunk's copies issued on ``stream`` at construction, from the
+    calling thread."""
+
+    def __init__(self, stream, jobs):
+        import torch
+
+        self.events = []
+        self.thread = threading.Thread(target=lambda: None)  # nothing to join
+        self.thread.start()
+        with torch.cuda.stream(stream):
+            for job in jobs:
+                job()
+                e = torch.cuda.Event()
+                e.record(stream)
+                self.events.append(e)
+
+    def ready(self, j: int):
+        return self.events[j]
+
+    def join(self) -> None:
+        pass
+
+
+class Pinned:
+    """hipHostRegister the caller's input arrays for a ``with`` block, so
+    their H2D copies are true async DMA issued from the calling thread
+    (the per-party mask step: its pageable H2D and pageable D2H would
+    otherwise take turns -- 22.6 against 19.0 ms for 100M floats).  ``ok`` is
+    False when the driver refuses any of them (then nothing stays registered
+    and the caller feeds pageable copies from a thread).  Unregistered on
+    exit, whatever happened."""
+
+    def __init__(self, arrays):
+        self.arrays = [a for a in arrays if a.nbytes]
+        self.done = []
+        self.ok = False
+
+    def __enter__(self):
+        hip = _hip()
+        for a in self.arrays:
+            rc = hip.hipHostRegister(ctypes.c_void_p(a.ctypes.data), ctypes.c_size_t(a.nbytes), ctypes.c_uint(0))
+            if rc != 0:
                 hip.hipGetLastError()  # clear the refused call's error state
-                stand = torch.empty(a.nbytes, dtype=torch.uint8, pin_memory=True).numpy().view(a.dtype)
-                if id(a) in self.outputs:
-                    self.back.append((a, stand))
-                else:
-                    np.copyto(stand, a)
-                self.usable.append(stand)
-        except BaseException:
-            self.__exit__(None, None, None)
-            raise
+                self.__exit__(None, None, None)
+                return self
+            self.done.append(a)
+        self.ok = True
         return self
 
-    def __exit__(self, exc_type, *exc):
+    def __exit__(self, *exc):
         hip = _hip()
         while self.done:
-            a = self.done.pop()
-            hip.hipHostUnregister(ctypes.c_void_p(a.ctypes.data))
-        if exc_type is None:
-            for a, stand in self.back:
-                np.copyto(a, stand)
-        self.back = []
+            hip.hipHostUnregister(ctypes.c_void_p(self.done.pop().ctypes.data))
         return False
+
+
+_HIP = None
+
+
+def _hip():
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+    return _HIP
 
 
 _STREAMS: dict = {}
@@ -213,7 +300,7 @@ def streams(dev):
 
 def host_layers(xs, dtype) -> list[np.ndarray]:
     """Each layer as a flat C-contiguous ``dtype`` array: the caller's own
-    memory when it already is one (registered in place), else a converted
+    memory when it already is one (copied from in place), else a converted
     copy."""
     out = []
     for a in xs:
@@ -226,8 +313,7 @@ def host_layers(xs, dtype) -> list[np.ndarray]:
 
 def copy_pieces(dst, layers: list[np.ndarray], lo: int, hi: int) -> None:
     """dst[lo:hi] (a device tensor, the layers' concatenation) <- the layers'
-    elements [lo, hi), one async copy per overlapping layer on the current
-    stream (the layers are registered)."""
+    elements [lo, hi), one copy per overlapping layer on the current stream."""
     import torch
 
     off = 0

@@ -313,9 +313,9 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
 def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, gpu):
     """A large launch group from host layers, chunked through three streams
     (``sfl_amd/hostpipe.py``): chunk j's H2D straight from the caller's
-    registered layers, its ``sa_mask`` at stream offset ``lo`` (the XOR
+    layers (a feeder thread), its ``sa_mask`` at stream offset ``lo`` (the XOR
     digest accumulated on the device), its D2H straight into the fresh
-    result as soon as that chunk's pages are faulted in and registered --
+    result (a pageable copy) as soon as that chunk's pages are faulted in --
     the copies of different chunks overlap each other and the page faulting.
     Bit-identical to one launch over the whole group (chunk j draws
     positions [lo, hi) of every stream).  Returns (host uint64 vector, {},
@@ -332,52 +332,61 @@ def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype,
     ph = H.Phases("mask_payload")
     layers = H.host_layers(xs, xt)
     n = int(sum(a.size for a in layers))
-    bounds = H.chunk_bounds(n)
+    bounds = H.chunk_bounds(n, target=16)
     out = H.FreshOutput(n, np.uint64, bounds)  # its pages start faulting in now
     s_in, s_k, s_out = H.streams(dev)
-    try:
-        with torch.cuda.device(dev), H.Registered(layers) as reg:
-            ph.mark("register in")
-            cur = torch.cuda.current_stream(dev)
-            x = torch.empty(n, dtype=tdt[xt], device=dev)
-            buf = torch.empty(n + 2, dtype=K.U64, device=dev)  # masked vector | digest | flag word
-            res, dig, flags = buf[:n], buf[n:n + 1], buf[n + 1:].view(torch.int32)[:1]
-            buf[n:].zero_()
-            ready = torch.cuda.Event()
-            ready.record(cur)
-            s_in.wait_event(ready)
-            s_k.wait_event(ready)
-            done = []
-            for lo, hi in bounds:
-                e_in, e_k = torch.cuda.Event(), torch.cuda.Event()
-                with torch.cuda.stream(s_in):
-                    H.copy_pieces(x, reg.usable, lo, hi)
-                    e_in.record(s_in)
+    with torch.cuda.device(dev), H.Pinned(layers) as pin:
+        cur = torch.cuda.current_stream(dev)
+        x = torch.empty(n, dtype=tdt[xt], device=dev)
+        buf = torch.empty(n + 2, dtype=K.U64, device=dev)  # masked vector | digest | flag word
+        res, dig, flags = buf[:n], buf[n:n + 1], buf[n + 1:].view(torch.int32)[:1]
+        buf[n:].zero_()
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        s_in.wait_event(ready)
+        s_k.wait_event(ready)
+        jobs = [lambda lo=lo, hi=hi: H.copy_pieces(x, layers, lo, hi) for lo, hi in bounds]
+        # registered inputs: every H2D issued at once from here (async DMA);
+        # otherwise pageable copies from a feeder thread
+        feed = H.Issued(s_in, jobs) if pin.ok else H.Feeder(s_in, jobs)
+        try:
+            def launch(j):
+                lo, hi = bounds[j]
+                e_k = torch.cuda.Event()
                 with torch.cuda.stream(s_k):
-                    s_k.wait_event(e_in)
+                    s_k.wait_event(feed.ready(j))
                     K.mask(x[lo:hi], res[lo:hi], masker.streams(offset=lo), weight=wscalar,
                            compute_dtype=tdt[ct], fxp_bits=masker.fxp_bits, digest=dig, flags=flags)
                     e_k.record(s_k)
-                done.append(e_k)
+                return e_k
+
+            def d2h(j, e_k):
+                lo, hi = bounds[j]
+                dst = torch.from_numpy(out.ready(j).view(np.int64))
+                with torch.cuda.stream(s_out):
+                    s_out.wait_event(e_k)
+                    dst.copy_(res[lo:hi], non_blocking=True)  # pageable: returns when done
+
+            if pin.ok:  # the copies in are all queued already: queue every launch, then copy out
+                for j, e_k in enumerate([launch(j) for j in range(len(bounds))]):
+                    d2h(j, e_k)
+            else:  # chunk j's copy in is issued by the feeder when it is done: alternate
+                for j in range(len(bounds)):
+                    d2h(j, launch(j))
             meta = torch.empty(2, dtype=K.U64, pin_memory=True)
             with torch.cuda.stream(s_k):
                 meta.copy_(buf[n:], non_blocking=True)
-            ph.mark("enqueue")
-            for j, (lo, hi) in enumerate(bounds):
-                dst = torch.from_numpy(out.ready(j).view(np.int64))
-                with torch.cuda.stream(s_out):
-                    s_out.wait_event(done[j])
-                    dst.copy_(res[lo:hi], non_blocking=True)
-            ph.mark("d2h enqueue")
+            ph.mark("pipeline")
+        finally:
+            feed.thread.join()
+            out.close()
             s_k.synchronize()
             s_out.synchronize()
             s_in.synchronize()
             cur.wait_stream(s_k)  # x / buf were allocated on the current stream
-            ph.mark("wait")
-    finally:
-        out.close()
-    ph.mark("unregister")
-    ph.note(**out.stats)
+        feed.join()
+        ph.mark("wait")
+    ph.note(pinned=pin.ok, **out.stats)
     ph.done()
     digest, flag = int(meta[0]) & ((1 << 64) - 1), int(meta[1]) & 0xFFFFFFFF
     if flag & L.SA_FLAG_PRG_REJECT:
@@ -505,10 +514,10 @@ def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_t
 def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
     """The server's large host call, chunked through three streams
     (``sfl_amd/hostpipe.py``): chunk j of every masked vector H2D straight
-    from the registered payloads, then on the device the per-vector XOR
+    from the payloads (a feeder thread), then on the device the per-vector XOR
     digests (accumulated over chunks), the mod-2^64 sum and the decode of
     chunk j, then its D2H straight into the fresh result as soon as that
-    chunk's pages are faulted in and registered -- overlapped with chunk
+    chunk's pages are faulted in (a pageable copy) -- overlapped with chunk
     j+1's copies.  Same kernels and result as the one-shot path."""
     import torch
 
@@ -517,30 +526,29 @@ def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
 
     C, n = len(u64s), int(u64s[0].size)
     ph = H.Phases("sum_decode")
-    ins = [np.ascontiguousarray(u).reshape(-1).view(np.int64) for u in u64s]
+    ins = [torch.from_numpy(np.ascontiguousarray(u).reshape(-1).view(np.int64)) for u in u64s]
     bounds = H.chunk_bounds(n)
     out = H.FreshOutput(n, np.float64, bounds)
     s_in, s_k, s_out = H.streams(dev)
-    try:
-        with torch.cuda.device(dev), H.Registered(ins) as reg:
-            ph.mark("register in")
-            host_in = [torch.from_numpy(a) for a in reg.usable]
-            cur = torch.cuda.current_stream(dev)
-            vecs = [torch.empty(n, dtype=K.U64, device=dev) for _ in range(C)]
-            s = torch.empty(n, dtype=K.U64, device=dev)
-            dec = torch.empty(n, dtype=torch.float64, device=dev)
-            dig = torch.zeros(C, dtype=K.U64, device=dev)
-            ready = torch.cuda.Event()
-            ready.record(cur)
-            s_in.wait_event(ready)
-            s_k.wait_event(ready)
-            done = []
-            for lo, hi in bounds:
-                e_in, e_k = torch.cuda.Event(), torch.cuda.Event()
-                with torch.cuda.stream(s_in):
-                    for v, h in zip(vecs, host_in):
-                        v[lo:hi].copy_(h[lo:hi], non_blocking=True)
-                    e_in.record(s_in)
+    with torch.cuda.device(dev):
+        cur = torch.cuda.current_stream(dev)
+        vecs = [torch.empty(n, dtype=K.U64, device=dev) for _ in range(C)]
+        s = torch.empty(n, dtype=K.U64, device=dev)
+        dec = torch.empty(n, dtype=torch.float64, device=dev)
+        dig = torch.zeros(C, dtype=K.U64, device=dev)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        s_in.wait_event(ready)
+        s_k.wait_event(ready)
+
+        def h2d(lo, hi):
+            for v, h in zip(vecs, ins):
+                v[lo:hi].copy_(h[lo:hi], non_blocking=True)
+
+        feed = H.Feeder(s_in, [lambda lo=lo, hi=hi: h2d(lo, hi) for lo, hi in bounds])
+        try:
+            for j, (lo, hi) in enumerate(bounds):
+                e_in, e_k = feed.ready(j), torch.cuda.Event()
                 with torch.cuda.stream(s_k):
                     s_k.wait_event(e_in)
                     part = [v[lo:hi] for v in vecs]
@@ -549,25 +557,23 @@ def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
                     K.sum_u64(part, s[lo:hi])
                     K.decode(s[lo:hi], dec[lo:hi], fxp_bits=fxp_bits, divisor=divisor)
                     e_k.record(s_k)
-                done.append(e_k)
+                dst = torch.from_numpy(out.ready(j))
+                with torch.cuda.stream(s_out):
+                    s_out.wait_event(e_k)
+                    dst.copy_(dec[lo:hi], non_blocking=True)
             got_h = torch.empty(C, dtype=K.U64, pin_memory=True)
             with torch.cuda.stream(s_k):
                 got_h.copy_(dig, non_blocking=True)
-            ph.mark("enqueue")
-            for j, (lo, hi) in enumerate(bounds):
-                dst = torch.from_numpy(out.ready(j))
-                with torch.cuda.stream(s_out):
-                    s_out.wait_event(done[j])
-                    dst.copy_(dec[lo:hi], non_blocking=True)
-            ph.mark("d2h enqueue")
+            ph.mark("pipeline")
+        finally:
+            feed.thread.join()
+            out.close()
             s_k.synchronize()
             s_out.synchronize()
             s_in.synchronize()
             cur.wait_stream(s_k)
-            ph.mark("wait")
-    finally:
-        out.close()
-    ph.mark("unregister")
+        feed.join()
+        ph.mark("wait")
     ph.note(**out.stats)
     ph.done()
     for i, (g, want) in enumerate(zip(got_h.numpy().view(np.uint64).tolist(), digests)):

@@ -40,6 +40,7 @@ import torch
 from ... import kernels as K
 from ... import _lib as L
 from ...device import PYU, PYUObject, DeviceObject, reveal
+from . import party as P
 from .aggregator import Aggregator
 from .masker import Masker
 
@@ -340,6 +341,9 @@ class SecureAggregator(Aggregator):
         # pageable copy per party (its staging pipelines, a host memcpy into
         # pinned memory first does not)
         big = 4 * n_pad > SMALL_CALL_BYTES
+        if big and not self._careful and C <= MAX_FUSED_CLIENTS and P.LARGE_PIPELINE:
+            return self._host_fused_pipelined(data, layer_lists, sizes, shapes, weights, average, is_list,
+                                              payloads, digests_keep, C, n, sdev)
         if not big and not self._careful and C <= MAX_FUSED_CLIENTS:
             res = self._host_one_call(data, layer_lists, sizes, shapes, weights, average, is_list, payloads,
                                       digests_keep, C, n, sdev)
@@ -383,6 +387,85 @@ class SecureAggregator(Aggregator):
         self.last_digests = [None if d is None else torch.from_numpy(ioi[n_pad + 1:n_pad + 1 + C].copy())
                              for d in digests_keep]
         parts = np.split(out, np.cumsum(sizes)[:-1]) if len(sizes) > 1 else [out]
+        result = [p.reshape(sh) for p, sh in zip(parts, shapes)]
+        if not is_list:
+            return PYUObject(self._device, result[0])
+        return PYUObject(self._device, tuple(result) if isinstance(payloads[0], tuple) else result)
+
+    def _host_fused_pipelined(self, data, layer_lists, sizes, shapes, weights, average, is_list, payloads,
+                              digests_keep, C, n, sdev):
+        """Large host float32 payloads of 2..8 co-located parties, chunked
+        through three streams (``sfl_amd/hostpipe.py``, as the per-party
+        drop-in's large path): chunk j of every party's layers H2D straight
+        from the caller's arrays (a feeder thread), the fused launch of chunk j
+        (every pair stream advanced to ``lo``, digests and the PRG flag
+        accumulated on the device) and its decode, then the D2H of chunk j
+        into the fresh result (a pageable copy) as soon as its pages are
+        faulted in.  Bit-identical to one fused launch over [0, n)."""
+        from ... import hostpipe as H
+
+        names = [d.device.party for d in data]
+        pair_gens, pair_signs = self._pair_streams(names)
+        ws = [1.0 if weights is None else float(w) for w in (weights or [None] * C)]
+        divisor = 1.0
+        if average:
+            divisor = float(C) if weights is None else float(sum(weights))
+        layers = [H.host_layers(ll, np.float32) for ll in layer_lists]
+        n_pad = -(-n // 4) * 4  # rows 16-byte aligned
+        bounds = H.chunk_bounds(n)
+        out = H.FreshOutput(n, np.float64, bounds)  # its pages start faulting in now
+        s_in, s_k, s_out = H.streams(sdev)
+        with torch.cuda.device(sdev):
+            cur = torch.cuda.current_stream(sdev)
+            x = torch.empty((C, n_pad), dtype=torch.float32, device=sdev)
+            ssum = torch.empty(n, dtype=K.U64, device=sdev)
+            dec = torch.empty(n, dtype=torch.float64, device=sdev)
+            meta = torch.zeros(1 + C, dtype=K.U64, device=sdev)  # flag word | digests
+            flags, digests = meta[:1].view(torch.int32)[:1], meta[1:]
+            ready = torch.cuda.Event()
+            ready.record(cur)
+            s_in.wait_event(ready)
+            s_k.wait_event(ready)
+
+            def h2d(lo, hi):
+                for c in range(C):
+                    H.copy_pieces(x[c], layers[c], lo, hi)
+
+            feed = H.Feeder(s_in, [lambda lo=lo, hi=hi: h2d(lo, hi) for lo, hi in bounds])
+            try:
+                for j, (lo, hi) in enumerate(bounds):
+                    gens = L.pcg64_advance_many(pair_gens, [lo] * len(pair_gens)) if lo else pair_gens
+                    e_in, e_k = feed.ready(j), torch.cuda.Event()
+                    with torch.cuda.stream(s_k):
+                        s_k.wait_event(e_in)
+                        K.fused_clients([x[c, lo:hi] for c in range(C)], ws, gens, pair_signs, [], 0, ssum[lo:hi],
+                                        fxp_bits=self._fxp_bits, digests=digests, flags=flags)
+                        K.decode(ssum[lo:hi], dec[lo:hi], fxp_bits=self._fxp_bits, divisor=divisor)
+                        e_k.record(s_k)
+                    dst = torch.from_numpy(out.ready(j))
+                    with torch.cuda.stream(s_out):
+                        s_out.wait_event(e_k)
+                        dst.copy_(dec[lo:hi], non_blocking=True)
+                meta_h = torch.empty(1 + C, dtype=K.U64, pin_memory=True)
+                with torch.cuda.stream(s_k):
+                    meta_h.copy_(meta, non_blocking=True)
+            finally:
+                feed.thread.join()
+                out.close()
+                s_k.synchronize()
+                s_out.synchronize()
+                s_in.synchronize()
+                cur.wait_stream(s_k)  # x, ssum, dec, meta were allocated on the current stream
+            feed.join()
+        mh = meta_h.numpy()
+        if int(mh[0]) & L.SA_FLAG_PRG_REJECT:  # the flag word's low half (little-endian)
+            raise _Rejected()
+        for nm in names:
+            self._maskers[nm].consume(n)
+        digests_keep.append(torch.from_numpy(mh[1:].copy()))
+        self.last_digests = digests_keep
+        res = out.array
+        parts = np.split(res, np.cumsum(sizes)[:-1]) if len(sizes) > 1 else [res]
         result = [p.reshape(sh) for p, sh in zip(parts, shapes)]
         if not is_list:
             return PYUObject(self._device, result[0])

@@ -161,3 +161,47 @@ def test_per_element_weights_and_torch_payloads_keep_the_one_shot_path(monkeypat
     wire, _ = P.mask_payload(maskers["alice"], t, None, gpu=0)
     assert np.array_equal(wire.u64, _expected([x], None, "alice", seeds, 0))
     assert calls == []
+
+
+@pytest.mark.parametrize("C", [2, 5, 8])
+def test_in_process_aggregator_large_host_payloads(C, monkeypatch):
+    """The in-process SecureAggregator's large host float32 path (co-located
+    parties, chunked through three streams like the drop-in) against the
+    oracle over two rounds, and against its one-shot path (LARGE_PIPELINE
+    off): same results, same per-party digests, same stream positions."""
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+    from sfl_amd.security.aggregation import party as P
+
+    names = [f"p{c}" for c in range(C)]
+    seeds = o.seeds_for(names)
+    pair = {(a, b): seeds[a][b] for a in names for b in names if a != b}
+    pyus = [PYU(nm, 0) for nm in names]
+    rng = np.random.default_rng(40 + C)
+    rounds = [[[(rng.standard_normal((700, 1001)) * 0.1).astype(np.float32),
+                (rng.standard_normal(1_300_003) * 0.1).astype(np.float32)] for _ in names] for _ in range(2)]
+    weights = [float(w) for w in rng.integers(1, 5, C)]
+
+    def run(pipeline):
+        monkeypatch.setattr(P, "LARGE_PIPELINE", pipeline)
+        agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
+        outs = []
+        for data in rounds:
+            got = rv(agg.average([p(lambda d=d: d)() for p, d in zip(pyus, data)], axis=0, weights=weights))
+            outs.append((got, [np.asarray(d).view(np.uint64).copy() for d in agg.last_digests if d is not None]))
+        pos = {nm: {q: agg._maskers[nm].position(q) for q in names if q != nm} for nm in names}
+        return outs, pos
+
+    a, pos_a = run(True)
+    b, pos_b = run(False)
+    n = 700 * 1001 + 1_300_003
+    assert pos_a == pos_b and all(v == 2 * n for d in pos_a.values() for v in d.values())
+    for r, ((ga, da), (gb, db)) in enumerate(zip(a, b)):
+        flat = [np.concatenate([x.reshape(-1) for x in d]) for d in rounds[r]]
+        exp, _, masked = o.secure_average(flat, names, weights=weights, seeds=seeds, offset=r * n)
+        assert [la.shape for la in ga] == [(700, 1001), (1_300_003,)]
+        assert np.array_equal(np.concatenate([x.reshape(-1) for x in ga]), exp), r
+        assert all(np.array_equal(la, lb) for la, lb in zip(ga, gb)), r
+        want = [o.digest(m) for m in masked]
+        assert [int(x) for x in np.concatenate(da)] == want, r
+        assert [int(x) for x in np.concatenate(db)] == want, r

@@ -18,31 +18,81 @@ def test_chunk_bounds_cover_and_align(n):
     assert H.chunk_bounds(0) == []
 
 
-def test_fresh_output_pages_and_chunks():
+def test_fresh_output_chunks():
     n = 3_000_001
     b = H.chunk_bounds(n)
     f = H.FreshOutput(n, np.uint64, b)
-    assert f.base % H.PAGE == 0  # page-aligned: every chunk registers its own pages
-    spans = [f._span(lo, hi) for lo, hi in b]
-    assert all(s0 % H.PAGE == 0 and s1 % H.PAGE == 0 for s0, s1 in spans)
-    assert all(a[1] <= c[0] for a, c in zip(spans, spans[1:]))  # no page in two chunks
-    for fs in f._futs:
-        for x in fs:
-            x.result()
+    parts = [f.ready(j) for j in range(len(b))]
+    assert sum(p.size for p in parts) == n and all(np.shares_memory(p, f.array) for p in parts)
+    f.close()
     a = f.array
-    assert a.shape == (n,) and a.dtype == np.uint64 and a.flags.writeable
+    assert a.shape == (n,) and a.dtype == np.uint64 and a.flags.writeable and a.flags.c_contiguous
     a[:] = 7
     assert int(a.sum()) == 7 * n
-    f.registered = []  # nothing registered on the CPU
-    f.close()
-    del f
-    assert int(a[-1]) == 7  # the caller's array keeps the mapping alive
 
 
 def test_host_layers_keep_contiguous_memory():
     x = np.arange(12, dtype=np.float32)
     y = np.arange(12, dtype=np.float32).reshape(3, 4).T
     got = H.host_layers([x, y, x.astype(np.float64)], np.float32)
-    assert np.shares_memory(got[0], x)  # registered in place
+    assert np.shares_memory(got[0], x)  # copied from in place
     assert not np.shares_memory(got[1], y) and np.array_equal(got[1], y.reshape(-1))
     assert got[2].dtype == np.float32
+
+
+class _FakeHip:
+    """hipHostRegister / Unregister stand-ins (no GPU here)."""
+
+    def __init__(self):
+        self.live = set()
+
+    def hipHostRegister(self, p, n, f):
+        self.live.add(p.value)
+        return 0
+
+    def hipHostUnregister(self, p):
+        self.live.discard(p.value)
+        return 0
+
+    def hipGetLastError(self):
+        return 0
+
+
+def test_result_pool_recycles_only_dropped_buffers(monkeypatch):
+    fake = _FakeHip()
+    monkeypatch.setattr(H, "_hip", lambda: fake)
+    pool = H.ResultPool(64 << 20)
+    a = pool.take(16 << 20)
+    assert a is not None and a.nbytes == 16 << 20 and len(fake.live) == 1
+    view = a[:1024].view(np.uint64)[3:9]  # a derived view keeps its owner busy
+    del a
+    b = pool.take(16 << 20)
+    assert b is not None and len(pool.bufs) == 2  # the first is still viewed
+    del view
+    c = pool.take(8 << 20)
+    assert c is not None and len(pool.bufs) == 2 and c is pool.bufs[0]  # recycled, best fit
+    assert pool.take(40 << 20) is None  # over the cap: the caller takes the fresh path
+    assert pool.take(1 << 20) is None  # small results never pool
+    del b, c
+    pool.clear()
+    assert pool.bufs == [] and fake.live == set()
+
+
+def test_fresh_output_takes_a_pooled_buffer(monkeypatch):
+    fake = _FakeHip()
+    monkeypatch.setattr(H, "_hip", lambda: fake)
+    monkeypatch.setattr(H, "RESULTS", H.ResultPool(64 << 20))
+    n = 3_000_001
+    f = H.FreshOutput(n, np.float64, H.chunk_bounds(n))
+    assert f.stats["pooled"] and f.array.shape == (n,) and f.array.dtype == np.float64
+    assert all(f.ready(j).size for j in range(len(f.bounds)))
+    f.close()
+    first = f.array.base
+    del f
+    g = H.FreshOutput(n, np.float64, H.chunk_bounds(n))
+    assert g.stats["pooled"] and g.array.base is not first  # the first result is still alive (first holds it)
+    del first
+    keep = g.array
+    del g
+    h = H.FreshOutput(n - 5, np.uint64, H.chunk_bounds(n - 5))
+    assert h.stats["pooled"] and not np.shares_memory(h.array, keep)

@@ -116,6 +116,35 @@ def main():
         res["one_shot"]["server_vs_floor"] = sf / res["one_shot"]["server_ms"]
         res["bit_identical"] = bool(np.array_equal(out, out1) and all(
             np.array_equal(w.u64, w1.u64) and w.digest == w1.digest for w, w1 in zip(wires, wires1)))
+    # the in-process SecureAggregator on the same host arrays (co-located
+    # parties: one fused launch per chunk), against the H2D floor of the
+    # inputs + the D2H of the float64 result
+    from sfl_amd.device import PYU, reveal
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    pair = {(u, v): seeds[u][v] for u in names for v in names if u != v}
+    pyus = [PYU(nm, 0) for nm in names]
+    objs = [p(lambda x=x: x)() for p, x in zip(pyus, xs)]
+    inf = floor_ms(torch, dev, 4 * C * n, 8 * n)
+    res["in_process_floor_ms"] = inf
+    for tag, on in (("in_process_pipelined", True), ("in_process_one_shot", False)):
+        if not on and not a.ab:
+            continue
+        P.LARGE_PIPELINE = on
+        agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
+        ts, got = [], None
+        for r in range(a.reps + 1):
+            got = None
+            t0 = time.perf_counter()
+            got = reveal(agg.average(objs, axis=0))
+            ts.append(time.perf_counter() - t0)
+        ms = statistics.median(ts[1:]) * 1e3
+        res[tag] = {"ms": ms, "grad_elems_per_s": C * n / (ms / 1e3), "vs_floor": inf / ms}
+        if on:
+            first = got
+        elif not np.array_equal(first, got):
+            res["bit_identical"] = False
+    P.LARGE_PIPELINE = True
     res["note"] = ("in-process: every party's mask_payload then the server's sum_decode (average), fp32 host "
                    "inputs, uint64 masked host vectors, float64 host result; floors: pinned copies of the same "
                    "bytes, H2D and D2H on two streams at once")

@@ -10,4 +10,7 @@ tail -n 3 $O/tests.txt
 SFL_HOSTPIPE_TRACE=1 timeout -k 10 300 python tools/party_bench.py --ab > $O/party_bench.jsonl 2> $O/party_bench_trace.err
 cut -c1-900 $O/party_bench.jsonl
 grep hostpipe $O/party_bench_trace.err | tail -n 6
+timeout -k 10 200 python bench.py --clients 4 --elems 10000000 --steps 200 --warmup 20 --cpu-baseline-seconds 0 \
+  --extra > $O/config2.jsonl 2> $O/config2.err
+python3 -c "import json; l=json.loads(open('$O/config2.jsonl').read().splitlines()[-1]); print(json.dumps(l['extra']))"
 echo CALL4_OK
