@@ -314,6 +314,8 @@ def host_layers(xs, dtype) -> list[np.ndarray]:
 def copy_pieces(dst, layers: list[np.ndarray], lo: int, hi: int) -> None:
     """dst[lo:hi] (a device tensor, the layers' concatenation) <- the layers'
     elements [lo, hi), one copy per overlapping layer on the current stream."""
+    import warnings
+
     import torch
 
     off = 0
@@ -321,7 +323,10 @@ def copy_pieces(dst, layers: list[np.ndarray], lo: int, hi: int) -> None:
         end = off + a.size
         a0, a1 = max(lo, off), min(hi, end)
         if a0 < a1:
-            dst[a0:a1].copy_(torch.from_numpy(a[a0 - off:a1 - off]), non_blocking=True)
+            with warnings.catch_warnings():  # a read-only caller array is only read here
+                warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
+                src = torch.from_numpy(a[a0 - off:a1 - off])
+            dst[a0:a1].copy_(src, non_blocking=True)
         off = end
         if off >= hi:
             break
