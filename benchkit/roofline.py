@@ -22,7 +22,7 @@ PCG_PAIR_DRAWS_2WAVE = 1.34e12  # pair draws (both ends accumulated), 2 waves/SI
 PCG_ONE_DRAWS_8WAVE = 1.57e12   # one-sided draws at 8 waves/SIMD ("dual one7 E2")
 
 
-PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r05", "r04", "r03", "r02", "r01")]  # newest first
+PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r06", "r05", "r04", "r03", "r02", "r01")]  # newest first
 PMC_ELEMS = 100_000_000  # element positions per launch of the committed PMC passes
 
 

@@ -19,6 +19,13 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python bench.py > gpurun_out/bench.jsonl 2> gpurun_out/bench.err
 tail -1 gpurun_out/bench.jsonl | cut -c1-400
+# the driver's exact form, and rocprof of it (the ramp is in its first launches)
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_form.jsonl \
+  2> gpurun_out/bench_driver_form.err
+tail -1 gpurun_out/bench_driver_form.jsonl | cut -c1-300
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_driver_form -o run -- \
+  python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_form_prof.jsonl \
+  2> gpurun_out/bench_driver_form_prof.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- \
   python3 bench.py --cpu-baseline-seconds 0 > gpurun_out/bench_prof.jsonl 2> gpurun_out/bench_prof.err
 tail -1 gpurun_out/bench_prof.jsonl | cut -c1-300

@@ -5,6 +5,10 @@ P=profiles/${1:?round, e.g. r03}
 mkdir -p $P
 tail -1 gpurun_out/bench.jsonl > $P/bench_n1.jsonl
 tail -1 gpurun_out/bench_prof.jsonl > $P/bench_n1_under_rocprof.jsonl
+tail -1 gpurun_out/bench_driver_form.jsonl > $P/bench_n1_driver_form.jsonl
+tail -1 gpurun_out/bench_driver_form_prof.jsonl > $P/bench_n1_driver_form_under_rocprof.jsonl
+cp gpurun_out/prof_driver_form/run_kernel_stats.csv $P/bench_n1_driver_form_kernel_stats.csv
+cp gpurun_out/prof_driver_form/run_kernel_trace.csv $P/bench_n1_driver_form_kernel_trace.csv
 tail -1 gpurun_out/bench_extra.jsonl > $P/bench_n1_extra.jsonl
 tail -1 gpurun_out/bench_dist_world1.jsonl > $P/bench_dist_world1_all_designs.jsonl
 cp gpurun_out/prof_bench/run_kernel_stats.csv $P/bench_n1_kernel_stats.csv
