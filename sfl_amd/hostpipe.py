@@ -10,10 +10,11 @@ kernels (a 100M-element party mask is ~0.5 ms of device time).  So:
 * the caller's host arrays are copied from where they are (no staging copy
   into pinned memory), by a helper thread (``Feeder``): a pageable copy
   runs at the pinned rate but blocks the thread that issues it;
-* the result goes into a FRESH host array (the caller keeps it) whose
-  chunks a thread pool faults in ahead of the copies (first touch of fresh
-  memory is the cost), chunk j's D2H a pageable copy as soon as its pages
-  are in, while later chunks are still being faulted in;
+* the result goes into a recycled registered buffer (``ResultPool``: free
+  once the caller dropped every array viewing it), so the D2H is async DMA
+  into pages that are in; on a miss, into a fresh array whose chunks a
+  thread pool faults in ahead of the copies (first touch of fresh memory is
+  the cost), chunk j's D2H a pageable copy as soon as its pages are in;
 * the element range is cut into chunks; chunk j's H2D (the feeder's
   stream), its kernels (a second) and its D2H (a third, from the calling
   thread) overlap with chunk j+1's, the streams ordered by events.
@@ -62,8 +63,9 @@ def chunk_bounds(n: int, target: int = 8, lo_elems: int = 1 << 20, hi_elems: int
 
 
 class FreshOutput:
-    """A fresh host result of ``n`` elements that the device fills chunk by
-    chunk.  ``np.empty`` memory (numpy advises huge pages for large
+    """A host result of ``n`` elements that the device fills chunk by chunk:
+    a recycled registered buffer from ``RESULTS`` when one is free (no
+    faults, async copies), else ``np.empty`` memory (numpy advises huge pages for large
     allocations: its first touch runs at ~27 GB/s on one thread, against
     ~8 GB/s for a plain anonymous mmap -- tools/touch_probe.py), faulted in
     by the thread pool in chunk order from construction on; ``ready(j)``
@@ -209,9 +211,10 @@ class Feeder:
             raise self.error
         return self.events[j]
 
-    def join(self) -> None:
+    def join(self, check: bool = True) -> None:
+        """Wait for the thread; with ``check``, re-raise its error here."""
         self.thread.join()
-        if self.error is not None:
+        if check and self.error is not None:
             raise self.error
 
 
@@ -224,8 +227,6 @@ class Issued:
         import torch
 
         self.events = []
-        self.thread = threading.Thread(target=lambda: None)  # nothing to join
-        self.thread.start()
         with torch.cuda.stream(stream):
             for job in jobs:
                 job()
@@ -236,7 +237,7 @@ class Issued:
     def ready(self, j: int):
         return self.events[j]
 
-    def join(self) -> None:
+    def join(self, check: bool = True) -> None:
         pass
 
 

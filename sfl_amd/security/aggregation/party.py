@@ -313,10 +313,12 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
 def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, gpu):
     """A large launch group from host layers, chunked through three streams
     (``sfl_amd/hostpipe.py``): chunk j's H2D straight from the caller's
-    layers (a feeder thread), its ``sa_mask`` at stream offset ``lo`` (the XOR
-    digest accumulated on the device), its D2H straight into the fresh
-    result (a pageable copy) as soon as that chunk's pages are faulted in --
-    the copies of different chunks overlap each other and the page faulting.
+    layers (registered for the call, else pageable copies from a feeder
+    thread), its ``sa_mask`` at stream offset ``lo`` (the XOR digest
+    accumulated on the device), its D2H into the result -- a recycled
+    registered buffer (async) or a fresh array whose chunk j is faulted in
+    ahead of its pageable copy -- the copies of different chunks overlapping
+    each other and the page faulting.
     Bit-identical to one launch over the whole group (chunk j draws
     positions [lo, hi) of every stream).  Returns (host uint64 vector, {},
     digest), or None when the round drew a raw 0 (numpy's rejection: the
@@ -365,7 +367,7 @@ def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype,
                 dst = torch.from_numpy(out.ready(j).view(np.int64))
                 with torch.cuda.stream(s_out):
                     s_out.wait_event(e_k)
-                    dst.copy_(res[lo:hi], non_blocking=True)  # pageable: returns when done
+                    dst.copy_(res[lo:hi], non_blocking=True)  # pooled: async; fresh (pageable): blocks
 
             if pin.ok:  # the copies in are all queued already: queue every launch, then copy out
                 for j, e_k in enumerate([launch(j) for j in range(len(bounds))]):
@@ -378,7 +380,7 @@ def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype,
                 meta.copy_(buf[n:], non_blocking=True)
             ph.mark("pipeline")
         finally:
-            feed.thread.join()
+            feed.join(check=False)  # the feeder is done with the inputs
             out.close()
             s_k.synchronize()
             s_out.synchronize()
@@ -514,11 +516,12 @@ def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_t
 def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
     """The server's large host call, chunked through three streams
     (``sfl_amd/hostpipe.py``): chunk j of every masked vector H2D straight
-    from the payloads (a feeder thread), then on the device the per-vector XOR
-    digests (accumulated over chunks), the mod-2^64 sum and the decode of
-    chunk j, then its D2H straight into the fresh result as soon as that
-    chunk's pages are faulted in (a pageable copy) -- overlapped with chunk
-    j+1's copies.  Same kernels and result as the one-shot path."""
+    from the payloads (pageable copies from a feeder thread), then on the
+    device the per-vector XOR digests (accumulated over chunks), the
+    mod-2^64 sum and the decode of chunk j, then its D2H into the result (a
+    recycled registered buffer, or a fresh array faulted in chunk by chunk)
+    -- overlapped with chunk j+1's copies.  Same kernels and result as the
+    one-shot path."""
     import torch
 
     from ... import hostpipe as H
@@ -566,7 +569,7 @@ def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
                 got_h.copy_(dig, non_blocking=True)
             ph.mark("pipeline")
         finally:
-            feed.thread.join()
+            feed.join(check=False)  # the feeder is done with the inputs
             out.close()
             s_k.synchronize()
             s_out.synchronize()

@@ -400,8 +400,9 @@ class SecureAggregator(Aggregator):
         from the caller's arrays (a feeder thread), the fused launch of chunk j
         (every pair stream advanced to ``lo``, digests and the PRG flag
         accumulated on the device) and its decode, then the D2H of chunk j
-        into the fresh result (a pageable copy) as soon as its pages are
-        faulted in.  Bit-identical to one fused launch over [0, n)."""
+        into the result (a recycled registered buffer, or a fresh array
+        faulted in chunk by chunk).  Bit-identical to one fused launch over
+        [0, n)."""
         from ... import hostpipe as H
 
         names = [d.device.party for d in data]
@@ -450,7 +451,7 @@ class SecureAggregator(Aggregator):
                 with torch.cuda.stream(s_k):
                     meta_h.copy_(meta, non_blocking=True)
             finally:
-                feed.thread.join()
+                feed.join(check=False)  # the feeder is done with the inputs
                 out.close()
                 s_k.synchronize()
                 s_out.synchronize()
