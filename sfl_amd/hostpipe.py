@@ -3,31 +3,34 @@
 A party's ``mask_payload`` and the server's ``sum_decode`` start and end in
 host memory (numpy arrays a secretflow PYU hands over and ships on).  For a
 large payload the time is the PCIe copies (``tools/pcie_paths.py`` on
-MI355X: ~57 GB/s each way, ~79 GB/s both ways at once; a pageable copy
-runs at the same rate but blocks the host until it is done), not the
-kernels (a 100M-element party mask is ~0.5 ms of device time).  So:
+MI355X: ~57 GB/s each way, ~79 GB/s both ways at once), not the kernels (a
+100M-element party mask is ~0.5 ms of device time).  So:
 
-* the caller's host arrays are copied from where they are (no staging copy
-  into pinned memory), by a helper thread (``Feeder``): a pageable copy
-  runs at the pinned rate but blocks the thread that issues it;
+* the element range is cut into chunks; chunk j's H2D, its kernels and its
+  D2H run on three streams ordered by events, overlapping chunk j+1's;
+* every DMA touches page-locked memory only: the caller's arrays are
+  staged through pinned slots (torch's caching host allocator) by a feeder
+  thread whose memcpy runs on a thread pool (75-97 GB/s on 8-16 threads,
+  above the PCIe rate, tools/pcie_paths.py); the caller's memory is never registered and no copy is
+  pageable (pageable D2H copies into fresh arrays beside registered
+  memory failed now and then with hipErrorInvalidValue, once aborting in
+  the next synchronise);
 * the result goes into a recycled registered buffer (``ResultPool``: free
-  once the caller dropped every array viewing it), so the D2H is async DMA
-  into pages that are in; on a miss, into a fresh array whose chunks a
-  thread pool faults in ahead of the copies (first touch of fresh memory is
-  the cost), chunk j's D2H a pageable copy as soon as its pages are in;
-* the element range is cut into chunks; chunk j's H2D (the feeder's
-  stream), its kernels (a second) and its D2H (a third, from the calling
-  thread) overlap with chunk j+1's, the streams ordered by events.
+  once the caller dropped every array viewing it), so its D2H is async DMA
+  into pages that are in; on a miss, chunk j lands in a pinned slot and a
+  drain thread copies it into a fresh ``np.empty`` (faulting its pages on
+  the pool's threads) while chunk j+1 is in flight.
 
 Nothing here computes: the kernels are the library's (``sa_mask``,
-``sa_xor_u64``, ``sa_sum_u64``, ``sa_decode``).  Used by
-``security/aggregation/party.py``.
+``sa_xor_u64``, ``sa_sum_u64``, ``sa_decode``, ``sa_fused_clients``).  Used
+by ``security/aggregation/party.py`` and ``secure_aggregator.py``.
 """
 
 from __future__ import annotations
 
 import ctypes
 import os
+import queue
 import sys
 import threading
 import time
@@ -39,16 +42,31 @@ _POOL = None
 # SFL_HOSTPIPE_TRACE=1: every pipelined call prints its phase times to stderr
 TRACE = os.environ.get("SFL_HOSTPIPE_TRACE") == "1"
 _POOL_LOCK = threading.Lock()
-TOUCH_THREADS = 8
+COPY_THREADS = 12  # of the box's 16-CPU share: the feeder, the drain and the caller keep the rest
 PAGE = 4096
+SLOTS = 3  # pinned staging slots per direction and call
 
 
 def _pool() -> ThreadPoolExecutor:
+    """Leaf tasks only (memcpy pieces, page touches): nothing submitted
+    here waits on another task of this pool."""
     global _POOL
     with _POOL_LOCK:
         if _POOL is None:
-            _POOL = ThreadPoolExecutor(TOUCH_THREADS, thread_name_prefix="sfl_sa_touch")
+            _POOL = ThreadPoolExecutor(COPY_THREADS, thread_name_prefix="sfl_sa_copy")
     return _POOL
+
+
+def pcopy(dst: np.ndarray, src: np.ndarray) -> None:
+    """dst[:] = src (same shape, contiguous), in pieces of >= 1 MiB on the
+    pool's threads (numpy's copy releases the GIL)."""
+    nb = dst.nbytes
+    k = min(COPY_THREADS, max(1, nb >> 20))
+    if k == 1:
+        np.copyto(dst, src)
+        return
+    step = -(-dst.size // k)
+    list(_pool().map(lambda a: np.copyto(dst[a:a + step], src[a:a + step]), range(0, dst.size, step)))
 
 
 def chunk_bounds(n: int, target: int = 8, lo_elems: int = 1 << 20, hi_elems: int = 1 << 24,
@@ -62,54 +80,113 @@ def chunk_bounds(n: int, target: int = 8, lo_elems: int = 1 << 20, hi_elems: int
     return [(lo, min(n, lo + step)) for lo in range(0, n, step)]
 
 
+class Slots:
+    """``SLOTS`` page-locked staging buffers of ``nbytes`` each, used round
+    robin; ``take(k)`` waits until slot k's previous use is over (a device
+    event: its DMA; or a threading.Event: the host copy out of it)."""
+
+    def __init__(self, nbytes: int, n: int = SLOTS):
+        import torch
+
+        self.bufs = [torch.empty(max(nbytes, 16), dtype=torch.uint8, pin_memory=True) for _ in range(n)]
+        self.busy = [None] * n
+
+    def take(self, k: int):
+        k %= len(self.bufs)
+        b = self.busy[k]
+        if isinstance(b, threading.Event):
+            b.wait()
+        elif b is not None:
+            b.synchronize()
+        return k, self.bufs[k]
+
+    def release(self, k: int, until) -> None:
+        self.busy[k] = until
+
+    def drain(self) -> None:
+        for k in range(len(self.bufs)):
+            self.take(k)
+            self.busy[k] = None
+
+
+def _np(t, dtype) -> np.ndarray:
+    return t.numpy().view(np.dtype(dtype))
+
+
 class FreshOutput:
-    """A host result of ``n`` elements that the device fills chunk by chunk:
-    a recycled registered buffer from ``RESULTS`` when one is free (no
-    faults, async copies), else ``np.empty`` memory (numpy advises huge pages for large
-    allocations: its first touch runs at ~27 GB/s on one thread, against
-    ~8 GB/s for a plain anonymous mmap -- tools/touch_probe.py), faulted in
-    by the thread pool in chunk order from construction on; ``ready(j)``
-    waits for chunk j's pages.  The D2H into a ready chunk is a pageable
-    copy (55 GB/s into touched pages, like a registered one): registering a
-    fresh result costs more than it saves (hipHostRegister takes the mm lock
-    and stalls the faulting threads).  ``array`` is the caller's result."""
+    """A host result of ``n`` elements that the device fills chunk by chunk.
+    A recycled registered buffer from ``RESULTS`` when one is free: chunk
+    j's D2H is async DMA straight into it.  Otherwise a fresh ``np.empty``
+    (numpy advises huge pages for large allocations: first touch ~27 GB/s a
+    thread against ~8 GB/s for a plain anonymous mmap, tools/touch_probe.py)
+    that chunk j reaches through a pinned slot: DMA into the slot, then the
+    drain thread copies the slot out on the pool's threads while later
+    chunks are in flight.  ``array`` is the caller's result; ``close()``
+    waits for the drain."""
 
     def __init__(self, n: int, dtype, bounds):
         dtype = np.dtype(dtype)
-        self.bounds = bounds
-        self.stats = {"wait_ms": 0.0, "pooled": False}
-        self._futs = [[] for _ in bounds]
+        self.dtype, self.bounds = dtype, bounds
+        self.stats = {"pooled": False, "drain_ms": 0.0}
+        self._q = self._thread = self._error = None
         owner = RESULTS.take(n * dtype.itemsize)
         if owner is not None:  # a recycled, registered buffer: no faults, async DMA
             self.array = owner[:n * dtype.itemsize].view(dtype)
             self.stats["pooled"] = True
             return
         self.array = np.empty(n, dtype=dtype)
-        self._b = self.array.view(np.uint8).reshape(-1)
-        isz = dtype.itemsize
-        pool = _pool()
-        self._futs = []
-        for lo, hi in bounds:
-            b0, b1 = lo * isz, hi * isz
-            step = max(PAGE, -(-(b1 - b0) // TOUCH_THREADS) // PAGE * PAGE)
-            self._futs.append([pool.submit(self._touch, a, min(b1, a + step)) for a in range(b0, b1, step)])
+        chunk = max((hi - lo for lo, hi in bounds), default=0)
+        self._slots = Slots(chunk * dtype.itemsize)
+        self._q = queue.Queue()
+        self._thread = threading.Thread(target=self._drain, name="sfl_sa_d2h", daemon=True)
+        self._thread.start()
 
-    def _touch(self, a: int, b: int) -> None:
-        self._b[a:b:PAGE] = 0
-        self._b[b - 1] = 0  # the last page of the range
+    def _drain(self) -> None:
+        while True:
+            item = self._q.get()
+            if item is None:
+                return
+            j, k, ev, done = item
+            try:
+                if self._error is None:
+                    t0 = time.perf_counter()
+                    ev.synchronize()
+                    lo, hi = self.bounds[j]
+                    pcopy(self.array[lo:hi], _np(self._slots.bufs[k], self.dtype)[:hi - lo])
+                    self.stats["drain_ms"] += 1e3 * (time.perf_counter() - t0)
+            except BaseException as ex:  # noqa: BLE001 - re-raised by close()
+                self._error = ex
+            finally:
+                done.set()
 
-    def ready(self, j: int) -> np.ndarray:
-        """Chunk j's elements, faulted in."""
-        t0 = time.perf_counter()
-        for f in self._futs[j]:
-            f.result()
-        self.stats["wait_ms"] += 1e3 * (time.perf_counter() - t0)
+    def copy_in(self, j: int, src, stream, after) -> None:
+        """D2H of chunk j: ``src`` (a device tensor of chunk j's elements)
+        into this result on ``stream`` once event ``after`` has passed."""
+        import torch
+
         lo, hi = self.bounds[j]
-        return self.array[lo:hi]
+        with torch.cuda.stream(stream):
+            stream.wait_event(after)
+            if self.stats["pooled"]:
+                dst = self.array[lo:hi]
+                torch.from_numpy(dst.view(np.int64) if dst.dtype == np.uint64 else dst).copy_(src, non_blocking=True)
+                return
+            k, slot = self._slots.take(j)
+            nb = (hi - lo) * self.dtype.itemsize
+            slot[:nb].view(src.dtype).copy_(src, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        done = threading.Event()  # set by the drain once the slot is copied out
+        self._slots.release(k, done)
+        self._q.put((j, k, ev, done))
 
     def close(self) -> None:
-        for f in (f for fs in self._futs for f in fs):
-            f.result()  # no toucher may outlive the call
+        if self._thread is not None:
+            self._q.put(None)
+            self._thread.join()
+            self._thread = None
+            if self._error is not None:
+                raise self._error
 
 
 class ResultPool:
@@ -144,7 +221,7 @@ class ResultPool:
             if sum(b.nbytes for b in self.bufs) + nbytes > self.cap:
                 return None
             owner = np.empty(nbytes, dtype=np.uint8)
-            step = -(-nbytes // TOUCH_THREADS) // PAGE * PAGE + PAGE
+            step = -(-nbytes // COPY_THREADS) // PAGE * PAGE + PAGE
 
             def touch(lo):
                 owner[lo:lo + step:PAGE] = 0
@@ -156,6 +233,12 @@ class ResultPool:
                 return None
             self.bufs.append(owner)
             return owner
+
+    def contains(self, a: np.ndarray) -> bool:
+        """``a``'s memory lies inside one of the pool's (registered) buffers."""
+        p0, p1 = a.ctypes.data, a.ctypes.data + a.nbytes
+        with self.lock:
+            return any(b.ctypes.data <= p0 and p1 <= b.ctypes.data + b.nbytes for b in self.bufs)
 
     def clear(self) -> None:
         """Unregister and drop every free buffer (tests, memory pressure)."""
@@ -173,19 +256,23 @@ RESULTS = ResultPool(int(os.environ.get("SFL_HOSTPIPE_POOL_BYTES", str(8 << 30))
 
 
 class Feeder:
-    """The H2D side of a pipelined call, on a helper thread: ``jobs[j]()``
-    issues chunk j's host-to-device copies on ``stream`` (the caller's own
-    pageable arrays: a pageable copy runs at the pinned rate but blocks the
-    thread that issues it -- tools/pcie_paths.py -- so it gets a thread of
-    its own; registering the arrays instead costs up to 8 ms per 800 MB and
-    stalls page faults elsewhere).  ``ready(j)`` returns the device event
-    that chunk j's copies complete at, once they are issued."""
+    """The H2D side of a pipelined call, on a helper thread.  ``chunks[j]``
+    lists chunk j's copies as (device tensor slice, pieces): ``pieces`` are
+    (host array, element offset in the slice) covering the slice.  Each
+    copy is staged through a pinned slot (memcpy on the pool's threads, the
+    DMA async on ``stream``); ``ready(j)`` returns the device event chunk j's
+    copies complete at, once they are issued."""
 
-    def __init__(self, stream, jobs):
-        self.stream, self.jobs = stream, jobs
-        self.flags = [threading.Event() for _ in jobs]
-        self.events = [None] * len(jobs)
+    def __init__(self, stream, chunks):
+        import torch
+
+        self.stream, self.chunks = stream, chunks
+        self.flags = [threading.Event() for _ in chunks]
+        self.events = [None] * len(chunks)
         self.error = None
+        nb = max((d.numel() * d.element_size() for ch in chunks for d, _ in ch), default=0)
+        self.slots = Slots(nb)
+        self._dt = {torch.float32: np.float32, torch.float64: np.float64, torch.int64: np.int64}
         self.thread = threading.Thread(target=self._run, name="sfl_sa_h2d", daemon=True)
         self.thread.start()
 
@@ -194,8 +281,19 @@ class Feeder:
 
         try:
             with torch.cuda.device(self.stream.device), torch.cuda.stream(self.stream):
-                for j, job in enumerate(self.jobs):
-                    job()
+                n = 0
+                for j, chunk in enumerate(self.chunks):
+                    for dst, pieces in chunk:
+                        k, slot = self.slots.take(n)
+                        n += 1
+                        nb = dst.numel() * dst.element_size()
+                        view = _np(slot, self._dt[dst.dtype])[:dst.numel()]
+                        for a, off in pieces:
+                            pcopy(view[off:off + a.size], a)
+                        dst.copy_(slot[:nb].view(dst.dtype), non_blocking=True)
+                        e = torch.cuda.Event()
+                        e.record(self.stream)
+                        self.slots.release(k, e)
                     e = torch.cuda.Event()
                     e.record(self.stream)
                     self.events[j] = e
@@ -219,17 +317,19 @@ class Feeder:
 
 
 class Issued:
-    """``Feeder``'s interface for inputs that need no thread (registered):
-    every chunk's copies issued on ``stream`` at construction, from the
-    calling thread."""
+    """``Feeder``'s interface for inputs that are registered for the call
+    (``Pinned``): every chunk's copies issued at once on ``stream`` from the
+    calling thread, async DMA straight from the caller's pages."""
 
-    def __init__(self, stream, jobs):
+    def __init__(self, stream, chunks):
         import torch
 
         self.events = []
         with torch.cuda.stream(stream):
-            for job in jobs:
-                job()
+            for chunk in chunks:
+                for dst, pcs in chunk:
+                    for a, off in pcs:
+                        dst[off:off + a.size].copy_(_tensor(a), non_blocking=True)
                 e = torch.cuda.Event()
                 e.record(stream)
                 self.events.append(e)
@@ -241,23 +341,44 @@ class Issued:
         pass
 
 
-class Pinned:
-    """hipHostRegister the caller's input arrays for a ``with`` block, so
-    their H2D copies are true async DMA issued from the calling thread
-    (the per-party mask step: its pageable H2D and pageable D2H would
-    otherwise take turns -- 22.6 against 19.0 ms for 100M floats).  ``ok`` is
-    False when the driver refuses any of them (then nothing stays registered
-    and the caller feeds pageable copies from a thread).  Unregistered on
-    exit, whatever happened."""
+def _tensor(a: np.ndarray):
+    import warnings
 
-    def __init__(self, arrays):
+    import torch
+
+    with warnings.catch_warnings():  # a read-only caller array is only read here
+        warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
+        return torch.from_numpy(a)
+
+
+class Pinned:
+    """hipHostRegister a party's input layers for a ``with`` block, so their
+    H2D is async DMA issued at once (``Issued``) instead of staged by the
+    feeder: the party's 400 MB in then overlaps its 800 MB out completely
+    (16.3 against ~27 ms for 100M floats).  Only our own copies touch these
+    pages while they are registered, and none of them is pageable.  Arrays
+    inside a pooled result (``RESULTS``: e.g. the masked vectors the server
+    receives from parties in the same process) are registered already and
+    taken as they are; with ``register=False`` nothing else is registered
+    (``ok`` then says whether every array was pooled).  ``ok`` is False when
+    the driver refuses any array (already registered elsewhere, or sharing a
+    page with registered memory): nothing stays registered and the caller
+    stages through the feeder.  Unregistered on exit."""
+
+    def __init__(self, arrays, register: bool = True):
         self.arrays = [a for a in arrays if a.nbytes]
+        self.register = register
         self.done = []
         self.ok = False
 
     def __enter__(self):
         hip = _hip()
         for a in self.arrays:
+            if RESULTS.contains(a):  # one of our pooled results: registered already
+                continue
+            if not self.register:
+                self.__exit__(None, None, None)
+                return self
             rc = hip.hipHostRegister(ctypes.c_void_p(a.ctypes.data), ctypes.c_size_t(a.nbytes), ctypes.c_uint(0))
             if rc != 0:
                 hip.hipGetLastError()  # clear the refused call's error state
@@ -300,8 +421,8 @@ def streams(dev):
 
 
 def host_layers(xs, dtype) -> list[np.ndarray]:
-    """Each layer as a flat C-contiguous ``dtype`` array: the caller's own
-    memory when it already is one (copied from in place), else a converted
+    """Each layer as a flat ``dtype`` array: the caller's own memory when it
+    already is a C-contiguous one (staged from in place), else a converted
     copy."""
     out = []
     for a in xs:
@@ -312,25 +433,19 @@ def host_layers(xs, dtype) -> list[np.ndarray]:
     return out
 
 
-def copy_pieces(dst, layers: list[np.ndarray], lo: int, hi: int) -> None:
-    """dst[lo:hi] (a device tensor, the layers' concatenation) <- the layers'
-    elements [lo, hi), one copy per overlapping layer on the current stream."""
-    import warnings
-
-    import torch
-
-    off = 0
+def pieces(layers: list[np.ndarray], lo: int, hi: int) -> list[tuple[np.ndarray, int]]:
+    """The layers' elements [lo, hi) of their concatenation as (host piece,
+    offset from lo) pairs, for ``Feeder``."""
+    out, off = [], 0
     for a in layers:
         end = off + a.size
         a0, a1 = max(lo, off), min(hi, end)
         if a0 < a1:
-            with warnings.catch_warnings():  # a read-only caller array is only read here
-                warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
-                src = torch.from_numpy(a[a0 - off:a1 - off])
-            dst[a0:a1].copy_(src, non_blocking=True)
+            out.append((a[a0 - off:a1 - off], a0 - lo))
         off = end
         if off >= hi:
             break
+    return out
 
 
 class Phases:

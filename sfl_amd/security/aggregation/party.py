@@ -313,12 +313,12 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
 def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, gpu):
     """A large launch group from host layers, chunked through three streams
     (``sfl_amd/hostpipe.py``): chunk j's H2D straight from the caller's
-    layers (registered for the call, else pageable copies from a feeder
-    thread), its ``sa_mask`` at stream offset ``lo`` (the XOR digest
-    accumulated on the device), its D2H into the result -- a recycled
-    registered buffer (async) or a fresh array whose chunk j is faulted in
-    ahead of its pageable copy -- the copies of different chunks overlapping
-    each other and the page faulting.
+    layers (registered for the call, else staged through pinned slots by a
+    feeder thread), its ``sa_mask``
+    at stream offset ``lo`` (the XOR digest accumulated on the device), its
+    D2H into the result -- a recycled registered buffer, or a fresh array
+    reached through a pinned slot -- the copies of different chunks
+    overlapping each other.
     Bit-identical to one launch over the whole group (chunk j draws
     positions [lo, hi) of every stream).  Returns (host uint64 vector, {},
     digest), or None when the round drew a raw 0 (numpy's rejection: the
@@ -347,10 +347,9 @@ def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype,
         ready.record(cur)
         s_in.wait_event(ready)
         s_k.wait_event(ready)
-        jobs = [lambda lo=lo, hi=hi: H.copy_pieces(x, layers, lo, hi) for lo, hi in bounds]
-        # registered inputs: every H2D issued at once from here (async DMA);
-        # otherwise pageable copies from a feeder thread
-        feed = H.Issued(s_in, jobs) if pin.ok else H.Feeder(s_in, jobs)
+        copies = [[(x[lo:hi], H.pieces(layers, lo, hi))] for lo, hi in bounds]
+        # registered layers: every H2D issued at once, async; else staged by the feeder
+        feed = H.Issued(s_in, copies) if pin.ok else H.Feeder(s_in, copies)
         try:
             def launch(j):
                 lo, hi = bounds[j]
@@ -364,17 +363,10 @@ def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype,
 
             def d2h(j, e_k):
                 lo, hi = bounds[j]
-                dst = torch.from_numpy(out.ready(j).view(np.int64))
-                with torch.cuda.stream(s_out):
-                    s_out.wait_event(e_k)
-                    dst.copy_(res[lo:hi], non_blocking=True)  # pooled: async; fresh (pageable): blocks
+                out.copy_in(j, res[lo:hi], s_out, e_k)
 
-            if pin.ok:  # the copies in are all queued already: queue every launch, then copy out
-                for j, e_k in enumerate([launch(j) for j in range(len(bounds))]):
-                    d2h(j, e_k)
-            else:  # chunk j's copy in is issued by the feeder when it is done: alternate
-                for j in range(len(bounds)):
-                    d2h(j, launch(j))
+            for j in range(len(bounds)):  # chunk j launches once the feeder has issued its copy in
+                d2h(j, launch(j))
             meta = torch.empty(2, dtype=K.U64, pin_memory=True)
             with torch.cuda.stream(s_k):
                 meta.copy_(buf[n:], non_blocking=True)
@@ -516,10 +508,10 @@ def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_t
 def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
     """The server's large host call, chunked through three streams
     (``sfl_amd/hostpipe.py``): chunk j of every masked vector H2D straight
-    from the payloads (pageable copies from a feeder thread), then on the
+    from the payloads (staged through pinned slots by a feeder thread), then on the
     device the per-vector XOR digests (accumulated over chunks), the
     mod-2^64 sum and the decode of chunk j, then its D2H into the result (a
-    recycled registered buffer, or a fresh array faulted in chunk by chunk)
+    recycled registered buffer, or a fresh array reached through a pinned slot)
     -- overlapped with chunk j+1's copies.  Same kernels and result as the
     one-shot path."""
     import torch
@@ -529,11 +521,14 @@ def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
 
     C, n = len(u64s), int(u64s[0].size)
     ph = H.Phases("sum_decode")
-    ins = [torch.from_numpy(np.ascontiguousarray(u).reshape(-1).view(np.int64)) for u in u64s]
+    ins = [np.ascontiguousarray(u).reshape(-1).view(np.int64) for u in u64s]
     bounds = H.chunk_bounds(n)
     out = H.FreshOutput(n, np.float64, bounds)
     s_in, s_k, s_out = H.streams(dev)
-    with torch.cuda.device(dev):
+    # vectors received from parties in this process sit in pooled (registered)
+    # results: copied async as they are; anything else is staged, not
+    # registered (6.4 GB of fresh vectors took up to 64 ms to register)
+    with torch.cuda.device(dev), H.Pinned(ins, register=False) as pin:
         cur = torch.cuda.current_stream(dev)
         vecs = [torch.empty(n, dtype=K.U64, device=dev) for _ in range(C)]
         s = torch.empty(n, dtype=K.U64, device=dev)
@@ -544,11 +539,8 @@ def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
         s_in.wait_event(ready)
         s_k.wait_event(ready)
 
-        def h2d(lo, hi):
-            for v, h in zip(vecs, ins):
-                v[lo:hi].copy_(h[lo:hi], non_blocking=True)
-
-        feed = H.Feeder(s_in, [lambda lo=lo, hi=hi: h2d(lo, hi) for lo, hi in bounds])
+        copies = [[(v[lo:hi], [(h[lo:hi], 0)]) for v, h in zip(vecs, ins)] for lo, hi in bounds]
+        feed = H.Issued(s_in, copies) if pin.ok else H.Feeder(s_in, copies)
         try:
             for j, (lo, hi) in enumerate(bounds):
                 e_in, e_k = feed.ready(j), torch.cuda.Event()
@@ -560,10 +552,7 @@ def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
                     K.sum_u64(part, s[lo:hi])
                     K.decode(s[lo:hi], dec[lo:hi], fxp_bits=fxp_bits, divisor=divisor)
                     e_k.record(s_k)
-                dst = torch.from_numpy(out.ready(j))
-                with torch.cuda.stream(s_out):
-                    s_out.wait_event(e_k)
-                    dst.copy_(dec[lo:hi], non_blocking=True)
+                out.copy_in(j, dec[lo:hi], s_out, e_k)
             got_h = torch.empty(C, dtype=K.U64, pin_memory=True)
             with torch.cuda.stream(s_k):
                 got_h.copy_(dig, non_blocking=True)
@@ -577,7 +566,7 @@ def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
             cur.wait_stream(s_k)
         feed.join()
         ph.mark("wait")
-    ph.note(**out.stats)
+    ph.note(pinned=pin.ok, **out.stats)
     ph.done()
     for i, (g, want) in enumerate(zip(got_h.numpy().view(np.uint64).tolist(), digests)):
         if int(g) != int(want) & ((1 << 64) - 1):

@@ -397,11 +397,12 @@ class SecureAggregator(Aggregator):
         """Large host float32 payloads of 2..8 co-located parties, chunked
         through three streams (``sfl_amd/hostpipe.py``, as the per-party
         drop-in's large path): chunk j of every party's layers H2D straight
-        from the caller's arrays (a feeder thread), the fused launch of chunk j
+        from the caller's arrays (registered for the call, else staged
+        through pinned slots by a feeder thread), the fused launch of chunk j
         (every pair stream advanced to ``lo``, digests and the PRG flag
         accumulated on the device) and its decode, then the D2H of chunk j
         into the result (a recycled registered buffer, or a fresh array
-        faulted in chunk by chunk).  Bit-identical to one fused launch over
+        reached through a pinned slot).  Bit-identical to one fused launch over
         [0, n)."""
         from ... import hostpipe as H
 
@@ -416,7 +417,7 @@ class SecureAggregator(Aggregator):
         bounds = H.chunk_bounds(n)
         out = H.FreshOutput(n, np.float64, bounds)  # its pages start faulting in now
         s_in, s_k, s_out = H.streams(sdev)
-        with torch.cuda.device(sdev):
+        with torch.cuda.device(sdev), H.Pinned([a for ls in layers for a in ls]) as pin:
             cur = torch.cuda.current_stream(sdev)
             x = torch.empty((C, n_pad), dtype=torch.float32, device=sdev)
             ssum = torch.empty(n, dtype=K.U64, device=sdev)
@@ -428,11 +429,9 @@ class SecureAggregator(Aggregator):
             s_in.wait_event(ready)
             s_k.wait_event(ready)
 
-            def h2d(lo, hi):
-                for c in range(C):
-                    H.copy_pieces(x[c], layers[c], lo, hi)
-
-            feed = H.Feeder(s_in, [lambda lo=lo, hi=hi: h2d(lo, hi) for lo, hi in bounds])
+            copies = [[(x[c, lo:hi], H.pieces(layers[c], lo, hi)) for c in range(C)] for lo, hi in bounds]
+            # registered layers: every H2D issued at once, async; else staged by the feeder
+            feed = H.Issued(s_in, copies) if pin.ok else H.Feeder(s_in, copies)
             try:
                 for j, (lo, hi) in enumerate(bounds):
                     gens = L.pcg64_advance_many(pair_gens, [lo] * len(pair_gens)) if lo else pair_gens
@@ -443,10 +442,7 @@ class SecureAggregator(Aggregator):
                                         fxp_bits=self._fxp_bits, digests=digests, flags=flags)
                         K.decode(ssum[lo:hi], dec[lo:hi], fxp_bits=self._fxp_bits, divisor=divisor)
                         e_k.record(s_k)
-                    dst = torch.from_numpy(out.ready(j))
-                    with torch.cuda.stream(s_out):
-                        s_out.wait_event(e_k)
-                        dst.copy_(dec[lo:hi], non_blocking=True)
+                    out.copy_in(j, dec[lo:hi], s_out, e_k)
                 meta_h = torch.empty(1 + C, dtype=K.U64, pin_memory=True)
                 with torch.cuda.stream(s_k):
                     meta_h.copy_(meta, non_blocking=True)

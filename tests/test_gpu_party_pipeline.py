@@ -205,3 +205,65 @@ def test_in_process_aggregator_large_host_payloads(C, monkeypatch):
         want = [o.digest(m) for m in masked]
         assert [int(x) for x in np.concatenate(da)] == want, r
         assert [int(x) for x in np.concatenate(db)] == want, r
+
+
+class _NotPinned:
+    """H.Pinned stand-in whose registration is refused: the feeder path."""
+
+    def __init__(self, arrays, register=True):
+        self.ok = False
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+@pytest.mark.parametrize("pooled", [True, False])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_every_copy_path_bit_exact(pooled, pinned, monkeypatch):
+    """Each way the pipelined calls move bytes, forced: a party's inputs
+    registered (async DMA) or staged through pinned slots by the feeder
+    thread; results into recycled registered buffers, or through pinned
+    slots into fresh arrays (the drain thread).  Three rounds each (the pool recycles the dropped results
+    of the round before), drop-in and in-process, bit-exact vs the oracle."""
+    from sfl_amd import hostpipe as H
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+    from sfl_amd.security.aggregation import party as P
+
+    monkeypatch.setattr(H, "RESULTS", H.ResultPool((1 << 30) if pooled else 0))
+    if not pinned:
+        monkeypatch.setattr(H, "Pinned", _NotPinned)
+    seeds = o.seeds_for(NAMES)
+    maskers = _maskers(seeds)
+    rng = np.random.default_rng(77)
+    offset = 0
+    for rnd in range(3):
+        layers = {nm: _payloads("f32_layers" if rnd != 1 else "i64", rng) for nm in NAMES}
+        w = 0.75 if rnd != 1 else 3
+        wires = []
+        for nm in NAMES:
+            wire, maskers[nm] = P.mask_payload(maskers[nm], layers[nm], w, gpu=0)
+            exp = _expected(layers[nm], w, nm, seeds, offset)
+            assert np.array_equal(wire.u64, exp) and wire.digest == o.digest(exp), (rnd, nm)
+            wires.append(wire)
+        got = P.sum_decode(*wires, weights=[w] * 3, average=True, gpu=0)
+        flat = np.concatenate([np.asarray(g).reshape(-1) for g in got])
+        assert np.array_equal(flat, o.decode(o.server_sum([x.u64 for x in wires]), 18, float(3 * w))), rnd
+        offset += wires[0].u64.size
+        del wires, got
+    if pooled:
+        assert H.RESULTS.bufs, "the pool was used"
+    # the in-process aggregator over the same copy paths
+    pair = {(a, b): seeds[a][b] for a in NAMES for b in NAMES if a != b}
+    pyus = [PYU(nm, 0) for nm in NAMES]
+    agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
+    for rnd in range(2):
+        data = [[(rng.standard_normal(1_700_001) * 0.1).astype(np.float32)] for _ in NAMES]
+        got = rv(agg.sum([p(lambda d=d: d)() for p, d in zip(pyus, data)], axis=0))
+        exp, _, _ = o.secure_sum([d[0] for d in data], NAMES, seeds=seeds, offset=rnd * 1_700_001)
+        assert np.array_equal(got[0], exp), rnd
+    del got
+    H.RESULTS.clear()

@@ -18,24 +18,29 @@ def test_chunk_bounds_cover_and_align(n):
     assert H.chunk_bounds(0) == []
 
 
-def test_fresh_output_chunks():
-    n = 3_000_001
-    b = H.chunk_bounds(n)
-    f = H.FreshOutput(n, np.uint64, b)
-    parts = [f.ready(j) for j in range(len(b))]
-    assert sum(p.size for p in parts) == n and all(np.shares_memory(p, f.array) for p in parts)
-    f.close()
-    a = f.array
-    assert a.shape == (n,) and a.dtype == np.uint64 and a.flags.writeable and a.flags.c_contiguous
-    a[:] = 7
-    assert int(a.sum()) == 7 * n
+def test_pcopy_and_pieces():
+    src = np.arange(11_000_003, dtype=np.float64)
+    dst = np.empty_like(src)
+    H.pcopy(dst, src)  # several 4 MiB+ pieces on the pool
+    assert np.array_equal(dst, src)
+    small = np.arange(10, dtype=np.int64)
+    d2 = np.zeros_like(small)
+    H.pcopy(d2, small)
+    assert np.array_equal(d2, small)
+    layers = [np.arange(5), np.zeros(0, np.int64), np.arange(100, 107), np.arange(200, 203)]
+    flat = np.concatenate(layers)
+    for lo, hi in [(0, 15), (3, 9), (5, 12), (12, 15), (4, 5)]:
+        got = np.full(hi - lo, -1)
+        for a, off in H.pieces(layers, lo, hi):
+            got[off:off + a.size] = a
+        assert np.array_equal(got, flat[lo:hi]), (lo, hi)
 
 
 def test_host_layers_keep_contiguous_memory():
     x = np.arange(12, dtype=np.float32)
     y = np.arange(12, dtype=np.float32).reshape(3, 4).T
     got = H.host_layers([x, y, x.astype(np.float64)], np.float32)
-    assert np.shares_memory(got[0], x)  # copied from in place
+    assert np.shares_memory(got[0], x)  # staged from in place
     assert not np.shares_memory(got[1], y) and np.array_equal(got[1], y.reshape(-1))
     assert got[2].dtype == np.float32
 
@@ -85,7 +90,6 @@ def test_fresh_output_takes_a_pooled_buffer(monkeypatch):
     n = 3_000_001
     f = H.FreshOutput(n, np.float64, H.chunk_bounds(n))
     assert f.stats["pooled"] and f.array.shape == (n,) and f.array.dtype == np.float64
-    assert all(f.ready(j).size for j in range(len(f.bounds)))
     f.close()
     first = f.array.base
     del f
@@ -96,3 +100,20 @@ def test_fresh_output_takes_a_pooled_buffer(monkeypatch):
     del g
     h = H.FreshOutput(n - 5, np.uint64, H.chunk_bounds(n - 5))
     assert h.stats["pooled"] and not np.shares_memory(h.array, keep)
+
+
+def test_pinned_takes_pooled_arrays_as_they_are(monkeypatch):
+    fake = _FakeHip()
+    monkeypatch.setattr(H, "_hip", lambda: fake)
+    monkeypatch.setattr(H, "RESULTS", H.ResultPool(64 << 20))
+    pooled = H.RESULTS.take(16 << 20)[: 8 << 20].view(np.uint64)
+    other = np.ones(1 << 20, np.uint64)
+    assert H.RESULTS.contains(pooled[10:20]) and not H.RESULTS.contains(other)
+    before = set(fake.live)
+    with H.Pinned([pooled], register=False) as p:
+        assert p.ok and fake.live == before  # nothing new registered
+    with H.Pinned([pooled, other], register=False) as p:
+        assert not p.ok  # the caller stages instead
+    with H.Pinned([pooled, other]) as p:
+        assert p.ok and len(fake.live) == len(before) + 1
+    assert fake.live == before
