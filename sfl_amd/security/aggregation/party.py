@@ -238,6 +238,10 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
     n = int(sum(int(np.prod(_shape_of(a))) for a in xs))
     small = 8 * n <= SMALL_CALL_BYTES
     streams = masker.streams()
+    if all(not isinstance(a, torch.Tensor) or a.device.type == "cpu" for a in xs):
+        # CPU tensors (``get_weights()``'s state-dict values) are host layers:
+        # their numpy views, no copy
+        xs = [a.detach().numpy() if isinstance(a, torch.Tensor) else a for a in xs]
     host_layers = not any(isinstance(a, torch.Tensor) for a in xs)
     if not small and wvec is None and host_layers and LARGE_PIPELINE:
         # host layers of a large payload: chunked H2D / mask / D2H overlap

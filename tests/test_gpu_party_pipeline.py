@@ -7,7 +7,8 @@ oracle: every party's masked vector and XOR digest bit-exact, the stream
 positions, the decoded result bit-exact -- over several rounds, layer lists
 that straddle chunk joins, every compute type, a non-contiguous and a
 read-only input (the registration fallback), a forced raw-0 rejection, and
-the per-element-weight / torch payloads that keep the one-shot path."""
+the per-element-weight / GPU-tensor payloads that keep the one-shot path
+(CPU tensors take the pipeline)."""
 import numpy as np
 import pytest
 
@@ -143,7 +144,7 @@ def test_large_payload_rejection_replays_on_numpys_stream():
         assert wires[0].positions == {"bob": rnd * (n + 1)}
 
 
-def test_per_element_weights_and_torch_payloads_keep_the_one_shot_path(monkeypatch):
+def test_per_element_weights_and_device_tensors_keep_the_one_shot_path(monkeypatch):
     from sfl_amd.security.aggregation import party as P
 
     calls = []
@@ -161,6 +162,11 @@ def test_per_element_weights_and_torch_payloads_keep_the_one_shot_path(monkeypat
     wire, _ = P.mask_payload(maskers["alice"], t, None, gpu=0)
     assert np.array_equal(wire.u64, _expected([x], None, "alice", seeds, 0))
     assert calls == []
+    # CPU tensors (a state dict's values) are host layers: the pipelined path
+    big = (rng.standard_normal(1_500_000) * 0.1).astype(np.float32)
+    wire, _ = P.mask_payload(maskers["alice"], [torch.from_numpy(big), torch.from_numpy(x)], None, gpu=0)
+    assert calls == [1] and wire.as_torch
+    assert np.array_equal(wire.u64, _expected([big, x], None, "alice", seeds, 0))
 
 
 @pytest.mark.parametrize("C", [2, 5, 8])
