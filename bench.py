@@ -22,6 +22,10 @@ sharded server over direct shard transfers, ncclReduce of the partial sums
 to rank 0, element sharding with and without the gather), each contained:
 a design that raises is recorded with its error, one that hangs past
 --variant-timeout makes rank 0 print the line so far (the headline stands).
+The N > 1 line also carries `rccl`: RCCL's own account from every rank's
+init log (benchkit/rccl_log.py) -- the transport of every connection
+(P2P/IPC over xGMI, SHM or NET/Socket), the ranks and nodes it saw -- and
+ncclCommCount / ncclCommCuDevice of our communicator (sa_comm_info).
 Total work is fixed as N grows:
 "scaling": "strong".  `python bench.py --gpus N` starts its N rank
 processes itself (torch.distributed.run as a child process with a c10d
