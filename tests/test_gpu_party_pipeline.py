@@ -273,3 +273,32 @@ def test_every_copy_path_bit_exact(pooled, pinned, monkeypatch):
         assert np.array_equal(got[0], exp), rnd
     del got
     H.RESULTS.clear()
+
+
+def test_in_process_large_rejection_replays_on_numpys_stream():
+    """A raw 0 on the (alice, bob) stream inside the chunked in-process
+    launch (element 1_700_000 of a 2.5M round, in a later chunk): the fused
+    chunk flags it, the round is replayed in careful mode from the same
+    positions; two rounds equal numpy's own generators (OracleMaskers)."""
+    from test_gpu_rejection import forced_zero_state
+
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+
+    names = NAMES
+    state = {("alice", "bob"): forced_zero_state(1_700_000)}
+    seeds = o.seeds_for(names)
+    pairs = {(a, b): state.get((a, b), state.get((b, a), seeds[a][b])) for a in names for b in names if a != b}
+    ora = o.OracleMaskers(names, pairs)
+    pyus = [PYU(nm, 0) for nm in names]
+    agg = SecureAggregator(PYU("server", 0), pyus, seeds=pairs)
+    rng = np.random.default_rng(21)
+    n = 2_500_000
+    for rnd in range(2):
+        xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in names]
+        got = rv(agg.sum([p(lambda x=x: x)() for p, x in zip(pyus, xs)], axis=0))
+        masked, ssum = ora.round(xs)
+        assert np.array_equal(got, o.decode(ssum)), rnd
+        assert [int(d) for d in np.asarray(agg.last_digests[-1]).view(np.uint64)] == [o.digest(m) for m in masked]
+    assert agg._maskers["alice"].position("bob") == 2 * n + 1
+    assert agg._maskers["alice"].position("carol") == 2 * n
