@@ -318,23 +318,33 @@ class Feeder:
 
 class Issued:
     """``Feeder``'s interface for inputs that are registered for the call
-    (``Pinned``): every chunk's copies issued at once on ``stream`` from the
-    calling thread, async DMA straight from the caller's pages."""
+    (``Pinned``): chunk j's copies, async DMA straight from the caller's
+    pages, issued from the calling thread when ``ready(j)`` is first asked
+    for, with chunk j+1's behind them.  Not all at once: a stream holds a
+    bounded number of outstanding copies, and issuing config 5's 512 copies
+    up front blocked the caller until most had finished, so no launch
+    overlapped them."""
+
+    LOOKAHEAD = 1
 
     def __init__(self, stream, chunks):
+        self.stream, self.chunks = stream, chunks
+        self.events = []
+
+    def _issue(self, j: int) -> None:
         import torch
 
-        self.events = []
-        with torch.cuda.stream(stream):
-            for chunk in chunks:
-                for dst, pcs in chunk:
-                    for a, off in pcs:
-                        dst[off:off + a.size].copy_(_tensor(a), non_blocking=True)
-                e = torch.cuda.Event()
-                e.record(stream)
-                self.events.append(e)
+        with torch.cuda.stream(self.stream):
+            for dst, pcs in self.chunks[j]:
+                for a, off in pcs:
+                    dst[off:off + a.size].copy_(_tensor(a), non_blocking=True)
+            e = torch.cuda.Event()
+            e.record(self.stream)
+            self.events.append(e)
 
     def ready(self, j: int):
+        while len(self.events) <= min(j + self.LOOKAHEAD, len(self.chunks) - 1):
+            self._issue(len(self.events))
         return self.events[j]
 
     def join(self, check: bool = True) -> None:

@@ -341,7 +341,7 @@ class SecureAggregator(Aggregator):
         # pageable copy per party (its staging pipelines, a host memcpy into
         # pinned memory first does not)
         big = 4 * n_pad > SMALL_CALL_BYTES
-        if big and not self._careful and C <= MAX_FUSED_CLIENTS and P.LARGE_PIPELINE:
+        if big and not self._careful and P.LARGE_PIPELINE:
             return self._host_fused_pipelined(data, layer_lists, sizes, shapes, weights, average, is_list,
                                               payloads, digests_keep, C, n, sdev)
         if not big and not self._careful and C <= MAX_FUSED_CLIENTS:
@@ -394,7 +394,7 @@ class SecureAggregator(Aggregator):
 
     def _host_fused_pipelined(self, data, layer_lists, sizes, shapes, weights, average, is_list, payloads,
                               digests_keep, C, n, sdev):
-        """Large host float32 payloads of 2..8 co-located parties, chunked
+        """Large host float32 payloads of co-located parties, chunked
         through three streams (``sfl_amd/hostpipe.py``, as the per-party
         drop-in's large path): chunk j of every party's layers H2D straight
         from the caller's arrays (registered for the call, else staged
@@ -403,9 +403,11 @@ class SecureAggregator(Aggregator):
         accumulated on the device) and its decode, then the D2H of chunk j
         into the result (a recycled registered buffer, or a fresh array
         reached through a pinned slot).  Bit-identical to one fused launch over
-        [0, n)."""
+        [0, n); more than 8 parties take the pair-shared schedule per chunk
+        (``kernels.fused_many``: the sum only, no per-party digests)."""
         from ... import hostpipe as H
 
+        ph = H.Phases("average" if average else "sum")
         names = [d.device.party for d in data]
         pair_gens, pair_signs = self._pair_streams(names)
         ws = [1.0 if weights is None else float(w) for w in (weights or [None] * C)]
@@ -418,12 +420,15 @@ class SecureAggregator(Aggregator):
         out = H.FreshOutput(n, np.float64, bounds)  # its pages start faulting in now
         s_in, s_k, s_out = H.streams(sdev)
         with torch.cuda.device(sdev), H.Pinned([a for ls in layers for a in ls]) as pin:
+            ph.mark("register in")
             cur = torch.cuda.current_stream(sdev)
             x = torch.empty((C, n_pad), dtype=torch.float32, device=sdev)
             ssum = torch.empty(n, dtype=K.U64, device=sdev)
             dec = torch.empty(n, dtype=torch.float64, device=sdev)
             meta = torch.zeros(1 + C, dtype=K.U64, device=sdev)  # flag word | digests
-            flags, digests = meta[:1].view(torch.int32)[:1], meta[1:]
+            # more parties than one launch holds: the pair-shared schedule
+            # (kernels.fused_many) forms only the sum, no per-party digests
+            flags, digests = meta[:1].view(torch.int32)[:1], (meta[1:] if C <= MAX_FUSED_CLIENTS else None)
             ready = torch.cuda.Event()
             ready.record(cur)
             s_in.wait_event(ready)
@@ -446,6 +451,7 @@ class SecureAggregator(Aggregator):
                 meta_h = torch.empty(1 + C, dtype=K.U64, pin_memory=True)
                 with torch.cuda.stream(s_k):
                     meta_h.copy_(meta, non_blocking=True)
+                ph.mark("pipeline")
             finally:
                 feed.join(check=False)  # the feeder is done with the inputs
                 out.close()
@@ -454,12 +460,16 @@ class SecureAggregator(Aggregator):
                 s_in.synchronize()
                 cur.wait_stream(s_k)  # x, ssum, dec, meta were allocated on the current stream
             feed.join()
+            ph.mark("wait")
+        ph.mark("unregister")
+        ph.note(pinned=pin.ok, **out.stats)
+        ph.done()
         mh = meta_h.numpy()
         if int(mh[0]) & L.SA_FLAG_PRG_REJECT:  # the flag word's low half (little-endian)
             raise _Rejected()
         for nm in names:
             self._maskers[nm].consume(n)
-        digests_keep.append(torch.from_numpy(mh[1:].copy()))
+        digests_keep.append(torch.from_numpy(mh[1:].copy()) if C <= MAX_FUSED_CLIENTS else None)
         self.last_digests = digests_keep
         res = out.array
         parts = np.split(res, np.cumsum(sizes)[:-1]) if len(sizes) > 1 else [res]

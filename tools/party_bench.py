@@ -54,6 +54,11 @@ def main():
     ap.add_argument("--elems", type=int, default=100_000_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--ab", action="store_true")
+    ap.add_argument("--fresh-inputs", action="store_true",
+                    help="every round hands the calls freshly allocated copies of the inputs (made outside the "
+                         "timed calls), as get_weights() does: registering them is then part of every call")
+    ap.add_argument("--in-process-only", action="store_true",
+                    help="only the in-process SecureAggregator (e.g. config 5: 32 x 256M)")
     a = ap.parse_args()
     import torch
 
@@ -67,7 +72,7 @@ def main():
     xs = []
     for c in range(C):
         g = torch.Generator(device=dev).manual_seed(20260116 + c)
-        xs.append((torch.randn(n, generator=g, device=dev) * 1e-2).cpu().numpy())
+        xs.append((torch.randn(n, generator=g, device=dev) * 1e-2).cpu().numpy().copy())
     res = {"clients": C, "elems": n, "reps": a.reps}
 
     def maskers():
@@ -86,7 +91,7 @@ def main():
             # the previous round's results are freed here, outside the timed calls
             wires = out = None
             wires = []
-            for nm, x in zip(names, xs):
+            for nm, x in zip(names, [x.copy() for x in xs] if a.fresh_inputs else xs):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 wire, ms[nm] = P.mask_payload(ms[nm], x, None, gpu=0)
@@ -102,13 +107,14 @@ def main():
                     "round_grad_elems_per_s": C * n / ((C * cm + sm) / 1e3)}
         return out, wires
 
-    out, wires = run("pipelined")
-    cf = floor_ms(torch, dev, 4 * n, 8 * n)
-    sf = floor_ms(torch, dev, 8 * C * n, 8 * n)
-    res["client_floor_ms"], res["server_floor_ms"] = cf, sf
-    res["pipelined"]["client_vs_floor"] = cf / res["pipelined"]["client_ms"]
-    res["pipelined"]["server_vs_floor"] = sf / res["pipelined"]["server_ms"]
-    if a.ab:
+    if not a.in_process_only:
+        out, wires = run("pipelined")
+        cf = floor_ms(torch, dev, 4 * n, 8 * n)
+        sf = floor_ms(torch, dev, 8 * C * n, 8 * n)
+        res["client_floor_ms"], res["server_floor_ms"] = cf, sf
+        res["pipelined"]["client_vs_floor"] = cf / res["pipelined"]["client_ms"]
+        res["pipelined"]["server_vs_floor"] = sf / res["pipelined"]["server_ms"]
+    if a.ab and not a.in_process_only:
         P.LARGE_PIPELINE = False
         out1, wires1 = run("one_shot")
         P.LARGE_PIPELINE = True
@@ -135,6 +141,8 @@ def main():
         ts, got = [], None
         for r in range(a.reps + 1):
             got = None
+            if a.fresh_inputs:
+                objs = [p(lambda x=x: x.copy())() for p, x in zip(pyus, xs)]
             t0 = time.perf_counter()
             got = reveal(agg.average(objs, axis=0))
             ts.append(time.perf_counter() - t0)
