@@ -533,15 +533,13 @@ class SecureAggregator(Aggregator):
             return PYUObject(self._device, result[0])
         return PYUObject(self._device, tuple(result) if isinstance(payloads[0], tuple) else result)
 
-    def _host_general_one_call(self, data, layer_lists, sizes, shapes, weights, average, is_list, payloads,
-                               digests_keep):
-        """Small host calls of float64 / int64 data (or float32 data with a
-        float64 compute type) of 2..9 parties on the server's GPU as ONE
-        blocking library call (``sa_clients_host``: every party masked with
-        its own streams into the sum, decode, one copy each way).  None when
-        the call is not of that shape (the general path takes it)."""
-        C, n = len(data), sum(sizes)
-        if (self._careful or self._keep_masked or not self._fused or not 2 <= C <= 9 or n == 0
+    def _host_general_shape(self, data, layer_lists, weights, n):
+        """(element type, compute type, scalar weights) of host payloads of
+        one element type in ``_NP2T`` with scalar weights of one compute type,
+        every party on the server's GPU -- the shape the general host paths
+        below take -- else None."""
+        C = len(data)
+        if (self._careful or self._keep_masked or not self._fused or C < 2 or n == 0
                 or any(d.device.gpu != self._device.gpu for d in data)):
             return None
         if weights is not None and any(np.ndim(w) for w in weights):
@@ -553,7 +551,7 @@ class SecureAggregator(Aggregator):
         if len(dts) != 1:
             return None
         xt = dts.pop()
-        if xt not in _NP2T or n * xt.itemsize > SMALL_CALL_BYTES:
+        if xt not in _NP2T:
             return None
         cts = {_compute_dtype(xt, None if weights is None else weights[i], self._fxp_bits) for i in range(C)}
         if len(cts) != 1:
@@ -561,8 +559,30 @@ class SecureAggregator(Aggregator):
         ct = cts.pop()
         if ct not in _NP2T:
             return None
-        names = [d.device.party for d in data]
         ws = [1.0 if weights is None else (float(w) if ct.kind == "f" else int(w)) for w in (weights or [None] * C)]
+        return xt, ct, ws
+
+    def _host_general_one_call(self, data, layer_lists, sizes, shapes, weights, average, is_list, payloads,
+                               digests_keep):
+        """Host calls of float64 / int64 data (or float32 data with a float64
+        compute type) of 2..9 parties on the server's GPU: small ones as ONE
+        blocking library call (``sa_clients_host``: every party masked with
+        its own streams into the sum, decode, one copy each way), large ones
+        (any number of parties) chunked through ``_host_general_pipelined``.
+        None when the call is of neither shape (the general path takes it)."""
+        C, n = len(data), sum(sizes)
+        got = self._host_general_shape(data, layer_lists, weights, n)
+        if got is None:
+            return None
+        xt, ct, ws = got
+        if n * xt.itemsize > SMALL_CALL_BYTES:
+            if not P.LARGE_PIPELINE:
+                return None
+            return self._host_general_pipelined(data, layer_lists, sizes, shapes, weights, average, is_list,
+                                                payloads, digests_keep, xt, ct, ws)
+        if C > 9:
+            return None
+        names = [d.device.party for d in data]
         streams = [self._maskers[nm].streams(self._maskers[nm].peers) for nm in names]
         xs = [np.asarray(ll[0]).reshape(-1) if len(ll) == 1 else
               np.concatenate([np.asarray(a).reshape(-1) for a in ll]) for ll in layer_lists]
@@ -587,6 +607,93 @@ class SecureAggregator(Aggregator):
         digests_keep.append(torch.from_numpy(digests.view(np.int64)))
         self.last_digests = digests_keep
         parts = np.split(out, np.cumsum(sizes)[:-1]) if len(sizes) > 1 else [out]
+        result = [p.reshape(sh) for p, sh in zip(parts, shapes)]
+        if not is_list:
+            return PYUObject(self._device, result[0])
+        return PYUObject(self._device, tuple(result) if isinstance(payloads[0], tuple) else result)
+
+    def _host_general_pipelined(self, data, layer_lists, sizes, shapes, weights, average, is_list, payloads,
+                                digests_keep, xt, ct, ws):
+        """Large host payloads of the general shape (``_host_general_shape``:
+        float64 / int64 data, or float32 data computed in float64), chunked
+        through the three streams exactly like ``_host_fused_pipelined``:
+        chunk j of every party H2D (registered inputs issued async, else
+        staged by the feeder), then on the compute stream every party's
+        ``sa_mask`` of chunk j with its own streams advanced to ``lo``
+        accumulating into the sum (its digest and the PRG flag accumulated on
+        the device), the decode of chunk j, and its D2H into the result.
+        Bit-identical to the one-shot general path: the same kernel, the same
+        stream positions, element by element."""
+        from ... import hostpipe as H
+
+        sdev = self._device.torch_device
+        C, n = len(data), sum(sizes)
+        ph = H.Phases("average" if average else "sum")
+        names = [d.device.party for d in data]
+        divisor = 1.0
+        if average:
+            divisor = float(C) if weights is None else float(sum(weights))
+        tx, tc = _NP2T[xt], _NP2T[ct]
+        layers = [H.host_layers(ll, xt) for ll in layer_lists]
+        n_pad = -(-n // 4) * 4  # rows 16-byte aligned
+        bounds = H.chunk_bounds(n)
+        out = H.FreshOutput(n, np.float64, bounds)
+        s_in, s_k, s_out = H.streams(sdev)
+        with torch.cuda.device(sdev), H.Pinned([a for ls in layers for a in ls]) as pin:
+            ph.mark("register in")
+            cur = torch.cuda.current_stream(sdev)
+            x = torch.empty((C, n_pad), dtype=tx, device=sdev)
+            ssum = torch.empty(n, dtype=K.U64, device=sdev)
+            dec = torch.empty(n, dtype=torch.float64, device=sdev)
+            masked = torch.empty(max(hi - lo for lo, hi in bounds), dtype=K.U64, device=sdev)
+            meta = torch.zeros(1 + C, dtype=K.U64, device=sdev)  # flag word | digests
+            flags = meta[:1].view(torch.int32)[:1]
+            ready = torch.cuda.Event()
+            ready.record(cur)
+            s_in.wait_event(ready)
+            s_k.wait_event(ready)
+
+            copies = [[(x[c, lo:hi], H.pieces(layers[c], lo, hi)) for c in range(C)] for lo, hi in bounds]
+            feed = H.Issued(s_in, copies) if pin.ok else H.Feeder(s_in, copies)
+            try:
+                for j, (lo, hi) in enumerate(bounds):
+                    streams = [self._maskers[nm].streams(offset=lo) for nm in names]
+                    e_in, e_k = feed.ready(j), torch.cuda.Event()
+                    with torch.cuda.stream(s_k):
+                        s_k.wait_event(e_in)
+                        ssum[lo:hi].zero_()
+                        for c in range(C):
+                            K.mask(x[c, lo:hi], masked[:hi - lo], streams[c], weight=ws[c], compute_dtype=tc,
+                                   fxp_bits=self._fxp_bits, sum_accum=ssum[lo:hi], digest=meta[1 + c:2 + c],
+                                   flags=flags)
+                        K.decode(ssum[lo:hi], dec[lo:hi], fxp_bits=self._fxp_bits, divisor=divisor)
+                        e_k.record(s_k)
+                    out.copy_in(j, dec[lo:hi], s_out, e_k)
+                meta_h = torch.empty(1 + C, dtype=K.U64, pin_memory=True)
+                with torch.cuda.stream(s_k):
+                    meta_h.copy_(meta, non_blocking=True)
+                ph.mark("pipeline")
+            finally:
+                feed.join(check=False)
+                out.close()
+                s_k.synchronize()
+                s_out.synchronize()
+                s_in.synchronize()
+                cur.wait_stream(s_k)  # x, ssum, dec, masked, meta were allocated on the current stream
+            feed.join()
+            ph.mark("wait")
+        ph.mark("unregister")
+        ph.note(pinned=pin.ok, **out.stats)
+        ph.done()
+        mh = meta_h.numpy()
+        if int(mh[0]) & L.SA_FLAG_PRG_REJECT:  # the flag word's low half (little-endian)
+            raise _Rejected()
+        for nm in names:
+            self._maskers[nm].consume(n)
+        digests_keep.append(torch.from_numpy(mh[1:].copy()))
+        self.last_digests = digests_keep
+        res = out.array
+        parts = np.split(res, np.cumsum(sizes)[:-1]) if len(sizes) > 1 else [res]
         result = [p.reshape(sh) for p, sh in zip(parts, shapes)]
         if not is_list:
             return PYUObject(self._device, result[0])

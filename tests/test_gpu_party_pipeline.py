@@ -216,6 +216,63 @@ def test_in_process_aggregator_large_host_payloads(C, monkeypatch):
         assert [int(x) for x in np.concatenate(db)] == want, r
 
 
+@pytest.mark.parametrize("kind,C", [("f64", 3), ("i64", 3), ("f64", 12)])
+def test_in_process_large_general_payloads(kind, C, monkeypatch):
+    """float64 / int64 host payloads in process (every party's own sa_mask
+    into the sum, chunk by chunk through the three streams) against the
+    oracle over two rounds and against the one-shot general path
+    (LARGE_PIPELINE off): same results, per-party digests, positions."""
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+    from sfl_amd.security.aggregation import party as P
+    from sfl_amd.security.aggregation import secure_aggregator as S
+
+    names = [f"p{c}" for c in range(C)]
+    seeds = o.seeds_for(names)
+    pair = {(a, b): seeds[a][b] for a in names for b in names if a != b}
+    pyus = [PYU(nm, 0) for nm in names]
+    rng = np.random.default_rng(60 + C)
+    if kind == "f64":
+        rounds = [[[rng.standard_normal((600, 1001)), rng.standard_normal(700_003)] for _ in names]
+                  for _ in range(2)]
+        weights = [float(w) for w in rng.uniform(0.5, 3.0, C)]
+    else:
+        rounds = [[[rng.integers(-1000, 1000, (600, 1001)), rng.integers(-9, 9, 700_003)] for _ in names]
+                  for _ in range(2)]
+        weights = [int(w) for w in rng.integers(1, 5, C)]
+    calls = []
+    orig = S.SecureAggregator._host_general_pipelined
+    monkeypatch.setattr(S.SecureAggregator, "_host_general_pipelined",
+                        lambda *a, **k: calls.append(1) or orig(*a, **k))
+
+    def run(pipeline):
+        monkeypatch.setattr(P, "LARGE_PIPELINE", pipeline)
+        agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
+        outs = []
+        for data in rounds:
+            got = rv(agg.average([p(lambda d=d: d)() for p, d in zip(pyus, data)], axis=0, weights=weights))
+            # the one-shot general path keeps its digests on the device
+            outs.append((got, [d.cpu().numpy().view(np.uint64).copy() for d in agg.last_digests if d is not None]))
+        pos = {nm: {q: agg._maskers[nm].position(q) for q in names if q != nm} for nm in names}
+        return outs, pos
+
+    a, pos_a = run(True)
+    assert calls == [1, 1]
+    b, pos_b = run(False)
+    assert calls == [1, 1]
+    n = 600 * 1001 + 700_003
+    assert pos_a == pos_b and all(v == 2 * n for d in pos_a.values() for v in d.values())
+    for r, ((ga, da), (gb, db)) in enumerate(zip(a, b)):
+        flat = [np.concatenate([x.reshape(-1) for x in d]) for d in rounds[r]]
+        exp, _, masked = o.secure_average(flat, names, weights=weights, seeds=seeds, offset=r * n)
+        assert [la.shape for la in ga] == [(600, 1001), (700_003,)]
+        assert np.array_equal(np.concatenate([x.reshape(-1) for x in ga]), exp), r
+        assert all(np.array_equal(la, lb) for la, lb in zip(ga, gb)), r
+        want = [o.digest(m) for m in masked]
+        assert [int(x) for x in np.concatenate(da)] == want, r
+        assert [int(x) for x in np.concatenate(db)] == want, r
+
+
 class _NotPinned:
     """H.Pinned stand-in whose registration is refused: the feeder path."""
 
@@ -274,15 +331,22 @@ def test_every_copy_path_bit_exact(pooled, pinned, monkeypatch):
         got = rv(agg.sum([p(lambda d=d: d)() for p, d in zip(pyus, data)], axis=0))
         exp, _, _ = o.secure_sum([d[0] for d in data], NAMES, seeds=seeds, offset=rnd * 1_700_001)
         assert np.array_equal(got[0], exp), rnd
+    # int64 layers: the per-party (general) chunked path over the same copy paths
+    data = [[rng.integers(-500, 500, 1_300_001)] for _ in NAMES]
+    got = rv(agg.sum([p(lambda d=d: d)() for p, d in zip(pyus, data)], axis=0))
+    exp, _, _ = o.secure_sum([d[0] for d in data], NAMES, seeds=seeds, offset=2 * 1_700_001)
+    assert np.array_equal(got[0], exp)
     del got
     H.RESULTS.clear()
 
 
-def test_in_process_large_rejection_replays_on_numpys_stream():
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_in_process_large_rejection_replays_on_numpys_stream(dtype):
     """A raw 0 on the (alice, bob) stream inside the chunked in-process
     launch (element 1_700_000 of a 2.5M round, in a later chunk): the fused
-    chunk flags it, the round is replayed in careful mode from the same
-    positions; two rounds equal numpy's own generators (OracleMaskers)."""
+    chunk (float32) or the per-party chunk (float64) flags it, the round is
+    replayed in careful mode from the same positions; two rounds equal
+    numpy's own generators (OracleMaskers)."""
     from test_gpu_rejection import forced_zero_state
 
     from sfl_amd.device import PYU, reveal as rv
@@ -298,10 +362,11 @@ def test_in_process_large_rejection_replays_on_numpys_stream():
     rng = np.random.default_rng(21)
     n = 2_500_000
     for rnd in range(2):
-        xs = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in names]
+        xs = [(rng.standard_normal(n) * 1e-2).astype(dtype) for _ in names]
         got = rv(agg.sum([p(lambda x=x: x)() for p, x in zip(pyus, xs)], axis=0))
         masked, ssum = ora.round(xs)
         assert np.array_equal(got, o.decode(ssum)), rnd
-        assert [int(d) for d in np.asarray(agg.last_digests[-1]).view(np.uint64)] == [o.digest(m) for m in masked]
+        dig = agg.last_digests[-1].cpu().numpy().view(np.uint64)
+        assert [int(d) for d in dig] == [o.digest(m) for m in masked]
     assert agg._maskers["alice"].position("bob") == 2 * n + 1
     assert agg._maskers["alice"].position("carol") == 2 * n

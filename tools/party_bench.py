@@ -5,7 +5,7 @@ process as secretflow PYUs would run them: C parties'
 the server's ``party.sum_decode`` (C host uint64 vectors in -> float64 host
 result out), against the copy floors measured in the same process:
 
-  client floor  H2D of the party's 4n bytes and D2H of its 8n bytes, pinned
+  client floor  H2D of the party's 4n bytes (8n for --dtype float64/int64) and D2H of its 8n bytes, pinned
                 buffers, both directions at once (two streams)
   server floor  H2D of the C x 8n masked bytes and D2H of the 8n result,
                 pinned, both directions at once
@@ -59,6 +59,8 @@ def main():
                          "timed calls), as get_weights() does: registering them is then part of every call")
     ap.add_argument("--in-process-only", action="store_true",
                     help="only the in-process SecureAggregator (e.g. config 5: 32 x 256M)")
+    ap.add_argument("--dtype", choices=["float32", "float64", "int64"], default="float32",
+                    help="the host payloads' element type (float64 / int64: the per-party chunked path)")
     a = ap.parse_args()
     import torch
 
@@ -72,8 +74,12 @@ def main():
     xs = []
     for c in range(C):
         g = torch.Generator(device=dev).manual_seed(20260116 + c)
-        xs.append((torch.randn(n, generator=g, device=dev) * 1e-2).cpu().numpy().copy())
-    res = {"clients": C, "elems": n, "reps": a.reps}
+        r = torch.randn(n, generator=g, device=dev)
+        x = (r * 1e3).round().to(torch.int64) if a.dtype == "int64" else (r * 1e-2).to(getattr(torch, a.dtype))
+        xs.append(x.cpu().numpy().copy())
+        del r, x
+    isz = xs[0].itemsize
+    res = {"clients": C, "elems": n, "reps": a.reps, "dtype": a.dtype}
 
     def maskers():
         out = {}
@@ -103,13 +109,13 @@ def main():
         cm = statistics.median([t for r, t in client_t if r > 0]) * 1e3
         sm = statistics.median([t for r, t in server_t if r > 0]) * 1e3
         res[tag] = {"client_ms": cm, "server_ms": sm,
-                    "client_GBps": 12 * n / cm / 1e6, "server_GBps": 8 * (C + 1) * n / sm / 1e6,
+                    "client_GBps": (isz + 8) * n / cm / 1e6, "server_GBps": 8 * (C + 1) * n / sm / 1e6,
                     "round_grad_elems_per_s": C * n / ((C * cm + sm) / 1e3)}
         return out, wires
 
     if not a.in_process_only:
         out, wires = run("pipelined")
-        cf = floor_ms(torch, dev, 4 * n, 8 * n)
+        cf = floor_ms(torch, dev, isz * n, 8 * n)
         sf = floor_ms(torch, dev, 8 * C * n, 8 * n)
         res["client_floor_ms"], res["server_floor_ms"] = cf, sf
         res["pipelined"]["client_vs_floor"] = cf / res["pipelined"]["client_ms"]
@@ -123,7 +129,8 @@ def main():
         res["bit_identical"] = bool(np.array_equal(out, out1) and all(
             np.array_equal(w.u64, w1.u64) and w.digest == w1.digest for w, w1 in zip(wires, wires1)))
     # the in-process SecureAggregator on the same host arrays (co-located
-    # parties: one fused launch per chunk), against the H2D floor of the
+    # parties: one fused launch per chunk for float32, every party's sa_mask
+    # per chunk for float64 / int64), against the H2D floor of the
     # inputs + the D2H of the float64 result
     from sfl_amd.device import PYU, reveal
     from sfl_amd.security.aggregation import SecureAggregator
@@ -131,7 +138,7 @@ def main():
     pair = {(u, v): seeds[u][v] for u in names for v in names if u != v}
     pyus = [PYU(nm, 0) for nm in names]
     objs = [p(lambda x=x: x)() for p, x in zip(pyus, xs)]
-    inf = floor_ms(torch, dev, 4 * C * n, 8 * n)
+    inf = floor_ms(torch, dev, isz * C * n, 8 * n)
     res["in_process_floor_ms"] = inf
     for tag, on in (("in_process_pipelined", True), ("in_process_one_shot", False)):
         if not on and not a.ab:
@@ -150,12 +157,14 @@ def main():
         res[tag] = {"ms": ms, "grad_elems_per_s": C * n / (ms / 1e3), "vs_floor": inf / ms}
         if on:
             first = got
-        elif not np.array_equal(first, got):
-            res["bit_identical"] = False
+        else:
+            same = all(np.array_equal(u, v) for u, v in zip(first, got)) if isinstance(got, list) else \
+                np.array_equal(first, got)
+            res["bit_identical"] = res.get("bit_identical", True) and bool(same)
     P.LARGE_PIPELINE = True
-    res["note"] = ("in-process: every party's mask_payload then the server's sum_decode (average), fp32 host "
-                   "inputs, uint64 masked host vectors, float64 host result; floors: pinned copies of the same "
-                   "bytes, H2D and D2H on two streams at once")
+    res["note"] = ("in-process: every party's mask_payload then the server's sum_decode (average), host "
+                   "inputs of --dtype, uint64 masked host vectors, float64 host result; floors: pinned copies of "
+                   "the same bytes, H2D and D2H on two streams at once")
     print(json.dumps(res), flush=True)
 
 
