@@ -9,12 +9,14 @@ MI355X: ~57 GB/s each way, ~79 GB/s both ways at once), not the kernels (a
 * the element range is cut into chunks; chunk j's H2D, its kernels and its
   D2H run on three streams ordered by events, overlapping chunk j+1's;
 * every DMA touches page-locked memory only: the caller's arrays are
-  staged through pinned slots (torch's caching host allocator) by a feeder
-  thread whose memcpy runs on a thread pool (75-97 GB/s on 8-16 threads,
-  above the PCIe rate, tools/pcie_paths.py); the caller's memory is never registered and no copy is
-  pageable (pageable D2H copies into fresh arrays beside registered
-  memory failed now and then with hipErrorInvalidValue, once aborting in
-  the next synchronise);
+  registered for the call (``Pinned``; chunk by chunk as their copies are
+  issued, ``Issued``), or, where the driver refuses that, staged through
+  pinned slots (torch's caching host allocator) by a feeder thread whose
+  memcpy runs on a thread pool (75-97 GB/s on 8-16 threads, above the PCIe
+  rate, tools/pcie_paths.py); no copy is pageable (pageable D2H copies into
+  fresh arrays beside registered memory failed now and then with
+  hipErrorInvalidValue, once aborting in the next synchronise, and once
+  with an illegal address: ``d2h`` / ``h2d`` serve the one-shot paths);
 * the result goes into a recycled registered buffer (``ResultPool``: free
   once the caller dropped every array viewing it), so its D2H is async DMA
   into pages that are in; on a miss, chunk j lands in a pinned slot and a
@@ -28,6 +30,7 @@ by ``security/aggregation/party.py`` and ``secure_aggregator.py``.
 
 from __future__ import annotations
 
+import bisect
 import ctypes
 import os
 import queue
@@ -78,6 +81,97 @@ def chunk_bounds(n: int, target: int = 8, lo_elems: int = 1 << 20, hi_elems: int
     step = min(max(-(-n // target), lo_elems), hi_elems)
     step = -(-step // align) * align
     return [(lo, min(n, lo + step)) for lo in range(0, n, step)]
+
+
+_NP_OF = {"torch.float32": np.float32, "torch.float64": np.float64, "torch.float16": np.float16,
+          "torch.int64": np.int64, "torch.int32": np.int32, "torch.uint8": np.uint8, "torch.bool": np.bool_}
+
+
+def host_dtype(t):
+    """The numpy dtype ``d2h`` gives tensor ``t``'s elements (None: numpy has none, e.g. bfloat16)."""
+    dt = _NP_OF.get(str(t.dtype))
+    return None if dt is None else np.dtype(dt)
+
+
+def d2h(t, pooled: bool = True) -> np.ndarray:
+    """A device tensor's elements in a new host array without a pageable
+    DMA (a large pageable copy beside registered memory -- ``RESULTS``,
+    ``Pinned`` -- failed now and then with hipErrorInvalidValue or an
+    illegal address; every host copy of the one-shot paths goes through
+    here): straight into a recycled registered buffer when ``pooled`` and
+    one is free, else into a pinned buffer and out of it on the pool's
+    threads.  Blocking."""
+    import torch
+
+    t = t.detach().contiguous()
+    dt = host_dtype(t)
+    if dt is None:
+        raise TypeError(f"no host array type for {t.dtype}")
+    nb = t.numel() * t.element_size()
+    owner = RESULTS.take(nb) if pooled else None
+    if owner is not None:
+        out = owner[:nb].view(dt)
+        torch.from_numpy(out).copy_(t.reshape(-1))
+        return out.reshape(tuple(t.shape))
+    h = torch.empty(t.numel(), dtype=t.dtype, pin_memory=True)
+    h.copy_(t.reshape(-1))
+    out = np.empty(t.numel(), dt)
+    pcopy(out, h.numpy())
+    return out.reshape(tuple(t.shape))
+
+
+def h2d(a, dev):
+    """A host array (numpy or a CPU tensor) as a new tensor on ``dev``,
+    without a pageable DMA (``d2h``): an array inside a pooled result is
+    copied as it is (registered), anything else through a pinned buffer
+    filled on the pool's threads.  Ordered on ``dev``'s current stream."""
+    import torch
+
+    if isinstance(a, torch.Tensor):
+        if a.device.type != "cpu":
+            return a.detach().to(dev)
+        a = a.detach().numpy()
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    if a.size == 0:
+        return torch.from_numpy(a).to(dev)
+    if RESULTS.contains(a):
+        return _tensor(a).to(dev)
+    h = torch.empty(a.shape, dtype=_tensor(a[:0]).dtype, pin_memory=True)
+    pcopy(h.numpy().reshape(-1), a.reshape(-1))
+    return h.to(dev, non_blocking=True)
+
+
+def page_bounds(bounds: list[tuple[int, int]], layer_lists) -> list[tuple[int, int]]:
+    """``bounds`` with each chunk join moved up by less than a page of
+    elements onto a page boundary of every party's layer holding it, where
+    one such move exists (the parties' arrays share their offset within a
+    page, as numpy's large allocations do), the join stays at a 16-byte
+    multiple (aligned device slices: the kernels' requirement) and inside
+    its layer.  Lazily registered inputs (``Pinned``) then register exactly
+    chunk by chunk and no copy is cut.  ``layer_lists``: per party, its flat
+    layers (same sizes and element type for every party)."""
+    if len(bounds) < 2 or not layer_lists:
+        return bounds
+    sizes = [a.size for a in layer_lists[0]]
+    if any([a.size for a in ll] != sizes for ll in layer_lists[1:]):
+        return bounds
+    isz = layer_lists[0][0].itemsize
+    starts = np.cumsum([0] + sizes).tolist()
+    out = [list(b) for b in bounds]
+    for k in range(1, len(bounds)):
+        lo = bounds[k][0]
+        li = bisect.bisect_right(starts, lo) - 1
+        need = {-(ll[li].ctypes.data + (lo - starts[li]) * isz) % PAGE for ll in layer_lists}
+        if len(need) != 1:
+            continue
+        nb = need.pop()
+        new = lo + nb // isz
+        if nb % isz or new * isz % 16 or new >= starts[li + 1] or new >= bounds[k][1]:
+            continue
+        out[k - 1][1] = out[k][0] = new
+    return [tuple(b) for b in out]
 
 
 class Slots:
@@ -323,12 +417,15 @@ class Issued:
     for, with chunk j+1's behind them.  Not all at once: a stream holds a
     bounded number of outstanding copies, and issuing config 5's 512 copies
     up front blocked the caller until most had finished, so no launch
-    overlapped them."""
+    overlapped them.  With a lazily registering ``pin``, each piece is
+    registered just before its copy is issued (``Pinned.split``), so the
+    registration of chunk j+1 runs while chunk j's DMA is in flight."""
 
     LOOKAHEAD = 1
 
-    def __init__(self, stream, chunks):
+    def __init__(self, stream, chunks, pin=None):
         self.stream, self.chunks = stream, chunks
+        self.pin = pin if pin is not None and pin.spans else None
         self.events = []
 
     def _issue(self, j: int) -> None:
@@ -337,7 +434,18 @@ class Issued:
         with torch.cuda.stream(self.stream):
             for dst, pcs in self.chunks[j]:
                 for a, off in pcs:
-                    dst[off:off + a.size].copy_(_tensor(a), non_blocking=True)
+                    d = dst[off:off + a.size]
+                    if self.pin is None:
+                        d.copy_(_tensor(a), non_blocking=True)
+                        continue
+                    db, ab = d.view(torch.uint8), a.view(np.uint8)
+                    for b0, b1, registered in self.pin.split(a):
+                        if registered:
+                            db[b0:b1].copy_(_tensor(ab[b0:b1]), non_blocking=True)
+                        else:  # the driver refused this range: a pinned temporary (kept until its DMA is done)
+                            tmp = torch.empty(b1 - b0, dtype=torch.uint8, pin_memory=True)
+                            pcopy(tmp.numpy(), ab[b0:b1])
+                            db[b0:b1].copy_(tmp, non_blocking=True)
             e = torch.cuda.Event()
             e.record(self.stream)
             self.events.append(e)
@@ -361,47 +469,134 @@ def _tensor(a: np.ndarray):
         return torch.from_numpy(a)
 
 
+# SFL_HOSTPIPE_LAZY_REGISTER=0: register every large input whole on entry
+# instead of piece by piece as its copies are issued
+LAZY_REGISTER = os.environ.get("SFL_HOSTPIPE_LAZY_REGISTER", "1") != "0"
+LAZY_MIN_BYTES = 64 << 20  # smaller arrays are registered whole on entry
+# each lazy registration covers at least LAZY_GROWTH x what the array has
+# registered so far (1: exactly what the copy at hand needs)
+LAZY_GROWTH = int(os.environ.get("SFL_HOSTPIPE_LAZY_GROWTH", "2"))
+
+
+class _Span:
+    """A lazily registered array: its bytes [start, end), registered from
+    ``base`` (its first page) up to ``reg_end``, the registrations' joins,
+    and whether the driver refused a registration (the rest is staged)."""
+
+    __slots__ = ("start", "end", "base", "reg_end", "cap", "joins", "refused")
+
+    def __init__(self, p0: int, p1: int):
+        self.start, self.end = p0, p1
+        self.base = self.reg_end = p0 // PAGE * PAGE
+        self.cap = -(-p1 // PAGE) * PAGE
+        self.joins, self.refused = [], False
+
+
 class Pinned:
     """hipHostRegister a party's input layers for a ``with`` block, so their
-    H2D is async DMA issued at once (``Issued``) instead of staged by the
-    feeder: the party's 400 MB in then overlaps its 800 MB out completely
-    (16.3 against ~27 ms for 100M floats).  Only our own copies touch these
-    pages while they are registered, and none of them is pageable.  Arrays
-    inside a pooled result (``RESULTS``: e.g. the masked vectors the server
-    receives from parties in the same process) are registered already and
-    taken as they are; with ``register=False`` nothing else is registered
-    (``ok`` then says whether every array was pooled).  ``ok`` is False when
-    the driver refuses any array (already registered elsewhere, or sharing a
-    page with registered memory): nothing stays registered and the caller
-    stages through the feeder.  Unregistered on exit."""
+    H2D is async DMA issued from the calling thread (``Issued``) instead of
+    staged by the feeder: the party's 400 MB in then overlaps its 800 MB out
+    completely (16.3 against ~27 ms for 100M floats).  Only our own copies
+    touch these pages while they are registered, and none of them is
+    pageable.  Arrays inside a pooled result (``RESULTS``: e.g. the masked
+    vectors the server receives from parties in the same process) are
+    registered already and taken as they are; with ``register=False``
+    nothing else is registered (``ok`` then says whether every array was
+    pooled).  ``ok`` is False when the driver refuses an array registered
+    on entry (already registered elsewhere, or sharing a page with
+    registered memory): nothing stays registered and the caller stages
+    through the feeder.  Unregistered on exit.
 
-    def __init__(self, arrays, register: bool = True):
+    Lazily (``LAZY_REGISTER``, arrays of ``LAZY_MIN_BYTES`` or more):
+    nothing is registered on entry; ``split`` registers an array's pages as
+    ``Issued`` reaches them, each time at least ``LAZY_GROWTH`` x what it
+    holds already (chunk 0, then 1, then 2-3, 4-7, ...: few calls, ~0.1-0.2
+    ms each whatever their size), so registering 32 GB of config-5 inputs
+    (57 ms before the first copy) overlaps the copies of earlier chunks.  A
+    copy never spans two registrations: ``split`` cuts it at their joins.
+    A registration the driver refuses leaves the rest of that array to be
+    staged piece by piece (``Issued``)."""
+
+    def __init__(self, arrays, register: bool = True, lazy: bool | None = None):
         self.arrays = [a for a in arrays if a.nbytes]
         self.register = register
-        self.done = []
+        self.lazy = LAZY_REGISTER if lazy is None else lazy
+        self.done = []  # start addresses of our registrations
+        self.spans: list[_Span] = []
+        self._keys = []
         self.ok = False
+        self.stats = {"registrations": 0, "register_ms": 0.0, "staged_bytes": 0}
+
+    def _reg(self, p0: int, p1: int) -> bool:
+        t0 = time.perf_counter()
+        hip = _hip()
+        rc = hip.hipHostRegister(ctypes.c_void_p(p0), ctypes.c_size_t(p1 - p0), ctypes.c_uint(0))
+        self.stats["register_ms"] += 1e3 * (time.perf_counter() - t0)
+        if rc != 0:
+            hip.hipGetLastError()  # clear the refused call's error state
+            return False
+        self.done.append(p0)
+        self.stats["registrations"] += 1
+        return True
 
     def __enter__(self):
-        hip = _hip()
         for a in self.arrays:
             if RESULTS.contains(a):  # one of our pooled results: registered already
                 continue
             if not self.register:
                 self.__exit__(None, None, None)
                 return self
-            rc = hip.hipHostRegister(ctypes.c_void_p(a.ctypes.data), ctypes.c_size_t(a.nbytes), ctypes.c_uint(0))
-            if rc != 0:
-                hip.hipGetLastError()  # clear the refused call's error state
+            p0, p1 = a.ctypes.data, a.ctypes.data + a.nbytes
+            if self.lazy and a.nbytes >= LAZY_MIN_BYTES:
+                self.spans.append(_Span(p0, p1))
+            elif not self._reg(p0, p1):
                 self.__exit__(None, None, None)
                 return self
-            self.done.append(a)
+        self.spans.sort(key=lambda sp: sp.start)
+        self._keys = [sp.start for sp in self.spans]
         self.ok = True
         return self
+
+    def split(self, a: np.ndarray) -> list[tuple[int, int, bool]]:
+        """Byte ranges (b0, b1, registered) covering contiguous piece ``a`` of
+        one of the arrays, each inside one registration, registering what
+        the piece needs first.  Pieces of an array come in address order.
+        A range the driver refused (and everything after it in that array)
+        comes back unregistered: ``Issued`` stages it."""
+        p0, p1 = a.ctypes.data, a.ctypes.data + a.nbytes
+        i = bisect.bisect_right(self._keys, p0) - 1
+        if i < 0 or not p1 <= self.spans[i].end:
+            return [(0, a.nbytes, True)]  # registered whole on entry, or pooled
+        sp = self.spans[i]
+        if sp.reg_end < p1 and not sp.refused:
+            grown = sp.base + LAZY_GROWTH * (sp.reg_end - sp.base)
+            new = min(sp.cap, max(-(-p1 // PAGE) * PAGE, -(-grown // PAGE) * PAGE))
+            if self._reg(sp.reg_end, new):
+                if sp.reg_end > sp.base:
+                    sp.joins.append(sp.reg_end)
+                sp.reg_end = new
+            else:
+                sp.refused = True
+        out, cur = [], p0
+        for c in sp.joins:
+            if cur < c < p1:
+                out.append((cur - p0, c - p0, True))
+                cur = c
+        if p1 <= sp.reg_end:
+            out.append((cur - p0, p1 - p0, True))
+        else:
+            if cur < sp.reg_end:
+                out.append((cur - p0, sp.reg_end - p0, True))
+                cur = sp.reg_end
+            out.append((cur - p0, p1 - p0, False))
+            self.stats["staged_bytes"] += p1 - cur
+        return out
 
     def __exit__(self, *exc):
         hip = _hip()
         while self.done:
-            hip.hipHostUnregister(ctypes.c_void_p(self.done.pop().ctypes.data))
+            hip.hipHostUnregister(ctypes.c_void_p(self.done.pop()))
+        self.spans, self._keys = [], []
         return False
 
 

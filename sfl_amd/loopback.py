@@ -42,6 +42,7 @@ from contextlib import contextmanager
 
 import numpy as np
 
+from . import hostpipe as H
 from . import wire as W
 from .wire import META
 
@@ -415,7 +416,7 @@ class LoopbackServer:
         if keep_masked:
             for st in streams:
                 st.synchronize()
-            self.last_masked = [d.cpu().numpy().view(np.uint64) for d in devb]
+            self.last_masked = [H.d2h(d, pooled=False).view(np.uint64) for d in devb]
         return out, {"first_chunk_all_s": stamps["first_chunk_all"] - t0,
                      "recv_sum_decode_s": stamps["recv_done"] - t0,
                      "broadcast_tail_s": t_end - stamps["recv_done"],

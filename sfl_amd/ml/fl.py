@@ -44,7 +44,23 @@ from typing import Callable, Dict, List, Optional
 import numpy as np
 import torch
 
+from .. import hostpipe as H
 from ..device import PYU, PYUObject, reveal
+
+
+def _host_array(v: torch.Tensor) -> np.ndarray:
+    """A fresh host copy of a model tensor (``.cpu().numpy().copy()``): a GPU
+    tensor's through pinned memory, never a pageable DMA (``hostpipe.d2h``:
+    the aggregator in the same process keeps registered host buffers)."""
+    v = v.detach()
+    return v.numpy().copy() if v.device.type == "cpu" else H.d2h(v, pooled=False)
+
+
+def _host_tensor(v: torch.Tensor) -> torch.Tensor:
+    """``v.cpu()`` the same way (element types numpy lacks keep ``.cpu()``)."""
+    if v.device.type == "cpu" or H.host_dtype(v) is None:
+        return v.cpu()
+    return torch.from_numpy(H.d2h(v, pooled=False))
 
 
 def optim_wrapper(func, *args, **kwargs):
@@ -109,8 +125,8 @@ class FedAvgW:
     # -------------------------------------------------------- weights
     def get_weights(self, return_numpy: bool = True):
         if not return_numpy:
-            return {k: v.cpu() for k, v in self.model.state_dict().items()}
-        return [v.detach().cpu().numpy().copy() for v in self.model.state_dict().values()]
+            return {k: _host_tensor(v) for k, v in self.model.state_dict().items()}
+        return [_host_array(v) for v in self.model.state_dict().values()]
 
     def set_weights(self, weights, model: Optional[torch.nn.Module] = None):
         model = self.model if model is None else model
@@ -297,7 +313,7 @@ class FedAvgG(FedAvgW):
             num_sample += x.shape[0]
             loss = self.loss_fn(self.model(x), y)
             loss.backward()
-            grads = [None if prm.grad is None else prm.grad.detach().cpu().numpy().copy()
+            grads = [None if prm.grad is None else _host_array(prm.grad)
                      for prm in self.model.parameters()]  # mixins.py:91-97
             grad_sum = grads if grad_sum is None else grad_sum + grads  # list += list: concatenation (:91)
         self.last_loss = float(loss.item()) if loss is not None else float("nan")

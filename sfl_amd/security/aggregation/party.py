@@ -127,7 +127,9 @@ def _host_weight(w):
         import torch
 
         if isinstance(w, torch.Tensor):
-            return w.detach().cpu().numpy()
+            from ... import hostpipe as H
+
+            return w.detach().numpy() if w.device.type == "cpu" else H.d2h(w, pooled=False)
     except ImportError:  # pragma: no cover
         pass
     return w
@@ -205,6 +207,10 @@ def mask_payload(masker: Masker, payload, weight=None, gpu: int | None = 0):
             masker)
 
 
+def _is_cuda(a) -> bool:
+    return _is_torch(a) and a.device.type != "cpu"
+
+
 def _is_torch(a) -> bool:
     try:
         import torch
@@ -228,6 +234,7 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
     import torch
 
     from ... import _lib as L
+    from ... import hostpipe as H
     from ... import kernels as K
     from .secure_aggregator import SMALL_CALL_BYTES
 
@@ -274,16 +281,18 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
             else:
                 flat = (np.ascontiguousarray(np.asarray(xs[0]), dtype=xt).reshape(-1) if len(xs) == 1 else
                         np.concatenate([np.asarray(a, dtype=xt).reshape(-1) for a in xs]))
-                x = torch.from_numpy(flat).to(dev)
+                x = H.h2d(flat, dev)
         else:
-            parts = [a.detach().reshape(-1).to(device=dev, dtype=tdt[xt]) if isinstance(a, torch.Tensor) else
-                     torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=xt).reshape(-1)).to(dev)
+            # device tensors as they are; CPU tensors cast on the host (no DMA), then pinned H2D
+            parts = [a.detach().reshape(-1).to(device=dev, dtype=tdt[xt]) if _is_cuda(a) else
+                     H.h2d(a.detach().reshape(-1).to(tdt[xt]) if _is_torch(a) else
+                           np.ascontiguousarray(np.asarray(a), dtype=xt).reshape(-1), dev)
                      for a in xs]
             x = parts[0] if len(parts) == 1 else torch.cat(parts)
         x = x.contiguous()
         if x.data_ptr() % 16:
             x = x.clone()
-        wv = None if wvec is None else torch.from_numpy(wvec).to(dev)
+        wv = None if wvec is None else H.h2d(wvec, dev)
         buf = torch.empty(n + 1, dtype=K.U64, device=dev)  # masked vector | flag word
         out = buf[:n]
         flags = buf[n:].view(torch.int32)[:1]
@@ -306,11 +315,11 @@ def _mask_vector(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype, wscalar, 
                     K.stream_shift(out, gen, sign, k, shift)
                 if total > n:
                     extra[peer] = total - n
-            host = K.as_u64(out)
+            host = H.d2h(out).view(np.uint64)
         elif small:
             host = hv[:n].copy()
         else:
-            host = K.as_u64(out)
+            host = H.d2h(out).view(np.uint64)
     return host, extra, None
 
 
@@ -338,7 +347,7 @@ def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype,
     ph = H.Phases("mask_payload")
     layers = H.host_layers(xs, xt)
     n = int(sum(a.size for a in layers))
-    bounds = H.chunk_bounds(n, target=16)
+    bounds = H.page_bounds(H.chunk_bounds(n, target=16), [layers])
     out = H.FreshOutput(n, np.uint64, bounds)  # its pages start faulting in now
     s_in, s_k, s_out = H.streams(dev)
     with torch.cuda.device(dev), H.Pinned(layers) as pin:
@@ -353,7 +362,7 @@ def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype,
         s_k.wait_event(ready)
         copies = [[(x[lo:hi], H.pieces(layers, lo, hi))] for lo, hi in bounds]
         # registered layers: every H2D issued at once, async; else staged by the feeder
-        feed = H.Issued(s_in, copies) if pin.ok else H.Feeder(s_in, copies)
+        feed = H.Issued(s_in, copies, pin) if pin.ok else H.Feeder(s_in, copies)
         try:
             def launch(j):
                 lo, hi = bounds[j]
@@ -384,7 +393,7 @@ def _mask_vector_pipelined(masker: Masker, xs: list, xt: np.dtype, ct: np.dtype,
             cur.wait_stream(s_k)  # x / buf were allocated on the current stream
         feed.join()
         ph.mark("wait")
-    ph.note(pinned=pin.ok, **out.stats)
+    ph.note(pinned=pin.ok, **pin.stats, **out.stats)
     ph.done()
     digest, flag = int(meta[0]) & ((1 << 64) - 1), int(meta[1]) & 0xFFFFFFFF
     if flag & L.SA_FLAG_PRG_REJECT:
@@ -447,6 +456,7 @@ def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_t
     comes back with one copy and one synchronisation."""
     import torch
 
+    from ... import hostpipe as H
     from ... import kernels as K
     from .secure_aggregator import SMALL_CALL_BYTES
 
@@ -476,8 +486,7 @@ def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_t
             dv = pin.to(dev, non_blocking=True)
             vecs = [dv[i, :n] for i in range(C)]
         else:
-            vecs = [torch.from_numpy(np.ascontiguousarray(u).view(np.int64)).to(dev, non_blocking=False)
-                    for u in u64s]
+            vecs = [H.h2d(np.asarray(u).view(np.int64), dev) for u in u64s]
         io = torch.empty(n + C, dtype=torch.float64, device=dev)  # decoded result | digests
         out = io[:n]
         if n:
@@ -489,7 +498,7 @@ def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_t
             K.sum_u64(vecs, s)
             dv_ = None
             if divisor_vec is not None:
-                dv_ = K.sum_f64([torch.from_numpy(w).to(dev) for w in divisor_vec],
+                dv_ = K.sum_f64([H.h2d(w, dev) for w in divisor_vec],
                                 torch.empty(n, dtype=torch.float64, device=dev))
             K.decode(s, out, fxp_bits=fxp_bits, divisor=divisor, divisor_vec=dv_)
             if small and not as_torch:
@@ -501,12 +510,12 @@ def _sum_decode_vectors(u64s, digests, fxp_bits, divisor, divisor_vec, gpu, as_t
                 result = hv[:n].copy()
             else:
                 got = K.as_u64(dig).tolist()
-                result = out if as_torch else out.cpu().numpy()
+                result = out if as_torch else H.d2h(out)
             for i, (g, want) in enumerate(zip(got, digests)):
                 if int(g) != int(want) & ((1 << 64) - 1):
                     raise DigestMismatch(f"masked vector {i}: digest {int(g):016x}, sent {int(want):016x}")
             return result
-    return out if as_torch else out.cpu().numpy()
+    return out if as_torch else H.d2h(out)
 
 
 def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
@@ -544,7 +553,7 @@ def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
         s_k.wait_event(ready)
 
         copies = [[(v[lo:hi], [(h[lo:hi], 0)]) for v, h in zip(vecs, ins)] for lo, hi in bounds]
-        feed = H.Issued(s_in, copies) if pin.ok else H.Feeder(s_in, copies)
+        feed = H.Issued(s_in, copies, pin) if pin.ok else H.Feeder(s_in, copies)
         try:
             for j, (lo, hi) in enumerate(bounds):
                 e_in, e_k = feed.ready(j), torch.cuda.Event()
@@ -570,7 +579,7 @@ def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
             cur.wait_stream(s_k)
         feed.join()
         ph.mark("wait")
-    ph.note(pinned=pin.ok, **out.stats)
+    ph.note(pinned=pin.ok, **pin.stats, **out.stats)
     ph.done()
     for i, (g, want) in enumerate(zip(got_h.numpy().view(np.uint64).tolist(), digests)):
         if int(g) != int(want) & ((1 << 64) - 1):

@@ -37,6 +37,7 @@ from typing import List
 import numpy as np
 import torch
 
+from ... import hostpipe as H
 from ... import kernels as K
 from ... import _lib as L
 from ...device import PYU, PYUObject, DeviceObject, reveal
@@ -217,7 +218,7 @@ class SecureAggregator(Aggregator):
                     assert w.device == data[i].device, "Device of weight does not match the corresponding data device."
                     w = reveal(w)
                 if isinstance(w, torch.Tensor):
-                    w = w.detach().cpu().numpy()
+                    w = w.detach().numpy() if w.device.type == "cpu" else H.d2h(w, pooled=False)
                 wl.append(w)
             weights = wl
 
@@ -357,7 +358,7 @@ class SecureAggregator(Aggregator):
                 if big:
                     src = (np.asarray(ll[0], dtype=np.float32).reshape(-1) if len(ll) == 1 else
                            np.concatenate([np.asarray(a, dtype=np.float32).reshape(-1) for a in ll]))
-                    dev_in[c, :n].copy_(torch.from_numpy(np.ascontiguousarray(src)))
+                    dev_in[c, :n].copy_(H.h2d(src, sdev))
                 elif len(ll) == 1:
                     host[c, :n] = np.asarray(ll[0], dtype=np.float32).reshape(-1)
                 else:
@@ -374,7 +375,7 @@ class SecureAggregator(Aggregator):
                 divisor = float(C) if weights is None else float(sum(weights))
             K.decode(s, st["io_dev"][:n], fxp_bits=self._fxp_bits, divisor=divisor)
             if big:
-                out = st["io_dev"][:n].cpu().numpy()
+                out = H.d2h(st["io_dev"][:n])
                 st["io_host"][n_pad:].copy_(st["io_dev"][n_pad:])
             else:
                 st["io_host"].copy_(st["io_dev"], non_blocking=True)
@@ -416,7 +417,7 @@ class SecureAggregator(Aggregator):
             divisor = float(C) if weights is None else float(sum(weights))
         layers = [H.host_layers(ll, np.float32) for ll in layer_lists]
         n_pad = -(-n // 4) * 4  # rows 16-byte aligned
-        bounds = H.chunk_bounds(n)
+        bounds = H.page_bounds(H.chunk_bounds(n), layers)
         out = H.FreshOutput(n, np.float64, bounds)  # its pages start faulting in now
         s_in, s_k, s_out = H.streams(sdev)
         with torch.cuda.device(sdev), H.Pinned([a for ls in layers for a in ls]) as pin:
@@ -436,7 +437,7 @@ class SecureAggregator(Aggregator):
 
             copies = [[(x[c, lo:hi], H.pieces(layers[c], lo, hi)) for c in range(C)] for lo, hi in bounds]
             # registered layers: every H2D issued at once, async; else staged by the feeder
-            feed = H.Issued(s_in, copies) if pin.ok else H.Feeder(s_in, copies)
+            feed = H.Issued(s_in, copies, pin) if pin.ok else H.Feeder(s_in, copies)
             try:
                 for j, (lo, hi) in enumerate(bounds):
                     gens = L.pcg64_advance_many(pair_gens, [lo] * len(pair_gens)) if lo else pair_gens
@@ -462,7 +463,7 @@ class SecureAggregator(Aggregator):
             feed.join()
             ph.mark("wait")
         ph.mark("unregister")
-        ph.note(pinned=pin.ok, **out.stats)
+        ph.note(pinned=pin.ok, **pin.stats, **out.stats)
         ph.done()
         mh = meta_h.numpy()
         if int(mh[0]) & L.SA_FLAG_PRG_REJECT:  # the flag word's low half (little-endian)
@@ -636,7 +637,7 @@ class SecureAggregator(Aggregator):
         tx, tc = _NP2T[xt], _NP2T[ct]
         layers = [H.host_layers(ll, xt) for ll in layer_lists]
         n_pad = -(-n // 4) * 4  # rows 16-byte aligned
-        bounds = H.chunk_bounds(n)
+        bounds = H.page_bounds(H.chunk_bounds(n), layers)
         out = H.FreshOutput(n, np.float64, bounds)
         s_in, s_k, s_out = H.streams(sdev)
         with torch.cuda.device(sdev), H.Pinned([a for ls in layers for a in ls]) as pin:
@@ -654,7 +655,7 @@ class SecureAggregator(Aggregator):
             s_k.wait_event(ready)
 
             copies = [[(x[c, lo:hi], H.pieces(layers[c], lo, hi)) for c in range(C)] for lo, hi in bounds]
-            feed = H.Issued(s_in, copies) if pin.ok else H.Feeder(s_in, copies)
+            feed = H.Issued(s_in, copies, pin) if pin.ok else H.Feeder(s_in, copies)
             try:
                 for j, (lo, hi) in enumerate(bounds):
                     streams = [self._maskers[nm].streams(offset=lo) for nm in names]
@@ -683,7 +684,7 @@ class SecureAggregator(Aggregator):
             feed.join()
             ph.mark("wait")
         ph.mark("unregister")
-        ph.note(pinned=pin.ok, **out.stats)
+        ph.note(pinned=pin.ok, **pin.stats, **out.stats)
         ph.done()
         mh = meta_h.numpy()
         if int(mh[0]) & L.SA_FLAG_PRG_REJECT:  # the flag word's low half (little-endian)
@@ -728,16 +729,15 @@ class SecureAggregator(Aggregator):
                     divisor = float(sum(weights))
                 else:
                     li = lis[0]
-                    wb = [torch.from_numpy(np.ascontiguousarray(
-                        np.broadcast_to(np.asarray(w), shapes[li]).astype(np.float64)).reshape(-1)).to(sdev)
-                        for w in weights]
+                    wb = [H.h2d(np.broadcast_to(np.asarray(w), shapes[li]).astype(np.float64).reshape(-1), sdev)
+                          for w in weights]
                     divisor_vec = K.sum_f64(wb, torch.empty(n, dtype=torch.float64, device=sdev))
             K.decode(s, dec, fxp_bits=self._fxp_bits, divisor=divisor, divisor_vec=divisor_vec)
             if as_torch:
                 for li, part in zip(lis, dec.split(sizes)):
                     out_layers[li] = part.reshape(shapes[li])
             elif 8 * n > SMALL_CALL_BYTES:
-                vals = dec.cpu().numpy()
+                vals = H.d2h(dec)
                 for li, part in zip(lis, np.split(vals, np.cumsum(sizes)[:-1])):
                     out_layers[li] = part.reshape(shapes[li])
             else:  # small host results: pinned copies, collected after ONE synchronisation below
@@ -790,7 +790,7 @@ class SecureAggregator(Aggregator):
                     wscalar = float(w) if ct.kind == "f" else int(w)
                 else:
                     wb = np.broadcast_to(np.asarray(w), shape).astype(ct)
-                    wv = torch.from_numpy(np.ascontiguousarray(wb).reshape(-1)).to(party.torch_device)
+                    wv = H.h2d(wb.reshape(-1), party.torch_device)
             xs.append(x)
             cts.append(ct)
             ws.append(wscalar)
@@ -830,10 +830,12 @@ class SecureAggregator(Aggregator):
     @staticmethod
     def _to_device(a, xt: np.dtype, party: PYU) -> torch.Tensor:
         tdt = _NP2T[xt]
-        if isinstance(a, torch.Tensor):
+        if isinstance(a, torch.Tensor) and a.device.type != "cpu":
             t = a.detach().reshape(-1).to(device=party.torch_device, dtype=tdt)
+        elif isinstance(a, torch.Tensor):  # cast on the host (no DMA), then a pinned copy
+            t = H.h2d(a.detach().reshape(-1).to(tdt), party.torch_device)
         else:
-            t = torch.from_numpy(np.ascontiguousarray(np.asarray(a), dtype=xt).reshape(-1)).to(party.torch_device)
+            t = H.h2d(np.ascontiguousarray(np.asarray(a), dtype=xt).reshape(-1), party.torch_device)
         t = t.contiguous()
         if t.data_ptr() % 16:
             t = t.clone()

@@ -31,6 +31,7 @@ import numpy as np
 import torch
 
 from ... import _lib as L
+from ... import hostpipe as H
 from ... import kernels as K
 
 
@@ -100,7 +101,7 @@ class GaussianModelDP:
             if x.numel():
                 K.dp_perturb(x, y, dp)
             y = y.reshape(shape)
-            out.append(y if as_torch else y.cpu().numpy())
+            out.append(y if as_torch else H.d2h(y, pooled=False))
         return out
 
     def global_norm(self, inputs) -> float:

@@ -276,8 +276,9 @@ def test_in_process_large_general_payloads(kind, C, monkeypatch):
 class _NotPinned:
     """H.Pinned stand-in whose registration is refused: the feeder path."""
 
-    def __init__(self, arrays, register=True):
+    def __init__(self, arrays, register=True, lazy=None):
         self.ok = False
+        self.spans, self.stats = [], {}
 
     def __enter__(self):
         return self
