@@ -26,11 +26,11 @@ def launch_ranks(args, script: str) -> int:
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if args.rehearse_one_gpu:
         # W rank processes on the one GPU plus a caller that holds a GPU
-        # context of its own ran ~10x slower and tripped the watchdog
-        # (DESIGN.md §5): refuse that setting instead of rehearsing in it
+        # context of its own run slower (W + 1 > 8 processes on one GPU): say
+        # so on stderr, the run itself is still valid
         holders = gpu_context_holders([os.getpid(), os.getppid()])
         if holders:
-            raise SystemExit(rehearsal_refusal(holders, args.gpus))
+            sys.stderr.write(rehearsal_warning(holders, args.gpus) + "\n")
         # N ranks share one box's CPU quota (a 16-CPU cgroup on the test box,
         # throttled during rehearsals: DESIGN.md §5); a rank's host work is
         # small copies, so one OpenMP thread each, as torchrun's own default
@@ -89,11 +89,11 @@ def gpu_context_holders(pids, device: str = KFD) -> list:
     return out
 
 
-def rehearsal_refusal(holders, world: int) -> str:
+def rehearsal_warning(holders, world: int) -> str:
     return (f"--rehearse-one-gpu: process(es) {holders} (this launcher or its caller) already hold a GPU context; "
-            f"with {world} rank processes that puts {world + len(holders)} processes on the one GPU, the setting "
-            "in which rehearsals ran ~10x slower and hit the watchdog (DESIGN.md §5). Start the rehearsal from a "
-            "process that has not initialised HIP (pytest: the rehearsal modules run first, tests/conftest.py).")
+            f"with {world} rank processes that puts {world + len(holders)} processes on the one GPU, where rehearsals "
+            "run slower (W = 8 at 8 x 100M: 31 s instead of 9 s, profiles/r06/rehearsal_context_probe.txt); the "
+            "driver's runs have one process per GPU.")
 
 
 def failing_ranks_report(log_dir: str, lines_per_rank: int = 60) -> str:

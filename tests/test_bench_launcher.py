@@ -392,10 +392,10 @@ def test_importing_the_bench_loads_no_torch():
 
 
 def test_gpu_context_guard_reads_proc(tmp_path):
-    """benchkit.launcher.gpu_context_holders (the --rehearse-one-gpu guard):
+    """benchkit.launcher.gpu_context_holders (the --rehearse-one-gpu warning):
     finds a process by an open device node in /proc/<pid>/fd, here a file
     standing in for /dev/kfd, without touching the GPU."""
-    from benchkit.launcher import gpu_context_holders, rehearsal_refusal
+    from benchkit.launcher import gpu_context_holders, rehearsal_warning
 
     dev = tmp_path / "kfd"
     dev.write_bytes(b"")
@@ -403,7 +403,7 @@ def test_gpu_context_guard_reads_proc(tmp_path):
     with open(dev) as f:
         assert gpu_context_holders([os.getpid(), os.getppid(), 2**22 + 7], str(dev)) == [os.getpid()]
         del f
-    assert "10x slower" in rehearsal_refusal([123], 8)
+    assert "9 processes on the one GPU" in rehearsal_warning([123], 8)
 
 
 def test_dry_run_n8_line_carries_the_exchange_model():

@@ -21,22 +21,6 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def _no_gpu_context_in_the_runner():
-    """These tests put W rank processes on the one GPU; the test process
-    must not hold a GPU context of its own (W + 1 processes is the setting
-    that ran ~10x slower).  Checked from /proc, without
-    initialising HIP: a selection that ran another GPU module first fails
-    here with the reason instead of stalling."""
-    import sys as _sys
-
-    _sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from benchkit.launcher import gpu_context_holders, rehearsal_refusal
-
-    if gpu_context_holders([os.getpid()]):
-        pytest.fail(rehearsal_refusal([os.getpid()], 8))
-
-
 def _run_ranks(target, world, args):
     """Spawn ``world`` rank processes and collect one result each.  A stalled
     rank fails the test within 150 s (every worker dumps its Python stacks

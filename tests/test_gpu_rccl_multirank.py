@@ -17,16 +17,6 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.fixture(autouse=True)
-def _no_gpu_context_in_the_runner():
-    """W rank processes on the one GPU: the runner must not add one more."""
-    sys.path.insert(0, ROOT)
-    from benchkit.launcher import gpu_context_holders, rehearsal_refusal
-
-    if gpu_context_holders([os.getpid()]):
-        pytest.fail(rehearsal_refusal([os.getpid()], 8))
-
-
 @pytest.mark.parametrize("world", [3, 8])
 def test_every_collective_between_real_rccl_ranks(world):
     if torch.cuda.device_count() == 0:  # asked without initialising HIP in this process
