@@ -371,3 +371,64 @@ def test_in_process_large_rejection_replays_on_numpys_stream(dtype):
         assert [int(d) for d in dig] == [o.digest(m) for m in masked]
     assert agg._maskers["alice"].position("bob") == 2 * n + 1
     assert agg._maskers["alice"].position("carol") == 2 * n
+
+
+@pytest.mark.parametrize("growth", [1, 2])
+@pytest.mark.parametrize("refuse_after", [None, 2])
+def test_lazy_registration_bit_exact(growth, refuse_after, monkeypatch):
+    """Inputs registered piece by piece as their copies are issued
+    (hostpipe.Pinned lazily: here every array of 1 MiB or more), chunk by
+    chunk or doubling, and with the driver refusing every registration after
+    the second (the rest of each array staged through pinned temporaries):
+    the drop-in's party calls and the in-process float32 / float64 paths
+    bit-exact vs the oracle."""
+    from sfl_amd import hostpipe as H
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+    from sfl_amd.security.aggregation import party as P
+
+    monkeypatch.setattr(H, "LAZY_MIN_BYTES", 1 << 20)
+    monkeypatch.setattr(H, "LAZY_GROWTH", growth)
+    stats = []
+    orig_reg, orig_exit = H.Pinned._reg, H.Pinned.__exit__
+
+    def reg(self, p0, p1):
+        if refuse_after is not None and self.stats["registrations"] >= refuse_after:
+            return False
+        return orig_reg(self, p0, p1)
+
+    def exit_(self, *exc):
+        if self.spans:
+            stats.append(dict(self.stats))
+        return orig_exit(self, *exc)
+
+    monkeypatch.setattr(H.Pinned, "_reg", reg)
+    monkeypatch.setattr(H.Pinned, "__exit__", exit_)
+    seeds = o.seeds_for(NAMES)
+    maskers = _maskers(seeds)
+    rng = np.random.default_rng(123)
+    layers = {nm: _payloads("f32_layers", rng) for nm in NAMES}
+    wires = []
+    for nm in NAMES:
+        wire, maskers[nm] = P.mask_payload(maskers[nm], layers[nm], 0.75, gpu=0)
+        exp = _expected(layers[nm], 0.75, nm, seeds, 0)
+        assert np.array_equal(wire.u64, exp) and wire.digest == o.digest(exp), nm
+        wires.append(wire)
+    got = P.sum_decode(*wires, weights=[0.75] * 3, average=True, gpu=0)
+    flat = np.concatenate([np.asarray(g).reshape(-1) for g in got])
+    assert np.array_equal(flat, o.decode(o.server_sum([x.u64 for x in wires]), 18, 2.25))
+    pair = {(a, b): seeds[a][b] for a in NAMES for b in NAMES if a != b}
+    pyus = [PYU(nm, 0) for nm in NAMES]
+    agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
+    off = 0
+    for dt in (np.float32, np.float64):
+        data = [[(rng.standard_normal(2_700_001) * 0.1).astype(dt)] for _ in NAMES]
+        got = rv(agg.sum([p(lambda d=d: d)() for p, d in zip(pyus, data)], axis=0))
+        exp, _, _ = o.secure_sum([d[0] for d in data], NAMES, seeds=seeds, offset=off)
+        assert np.array_equal(got[0], exp), dt
+        off += 2_700_001
+    assert stats and all(s["registrations"] > 0 for s in stats)
+    if refuse_after is None:
+        assert all(s["staged_bytes"] == 0 for s in stats)
+    else:
+        assert any(s["staged_bytes"] > 0 for s in stats)
