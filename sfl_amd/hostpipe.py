@@ -72,12 +72,18 @@ def pcopy(dst: np.ndarray, src: np.ndarray) -> None:
     list(_pool().map(lambda a: np.copyto(dst[a:a + step], src[a:a + step]), range(0, dst.size, step)))
 
 
-def chunk_bounds(n: int, target: int = 8, lo_elems: int = 1 << 20, hi_elems: int = 1 << 24,
+# chunks per pipelined call (SFL_HOSTPIPE_CHUNKS; a party's mask_payload asks for 16 itself)
+CHUNKS = int(os.environ.get("SFL_HOSTPIPE_CHUNKS", "8"))
+
+
+def chunk_bounds(n: int, target: int | None = None, lo_elems: int = 1 << 20, hi_elems: int = 1 << 24,
                  align: int = 1024) -> list[tuple[int, int]]:
-    """[0, n) in about ``target`` chunks of lo_elems..hi_elems elements, each
-    start a multiple of ``align`` (16-byte aligned device slices)."""
+    """[0, n) in about ``target`` (default ``CHUNKS``) chunks of
+    lo_elems..hi_elems elements, each start a multiple of ``align`` (16-byte
+    aligned device slices)."""
     if n <= 0:
         return []
+    target = CHUNKS if target is None else target
     step = min(max(-(-n // target), lo_elems), hi_elems)
     step = -(-step // align) * align
     return [(lo, min(n, lo + step)) for lo in range(0, n, step)]
