@@ -28,6 +28,7 @@ spawned process per party.
 
 from __future__ import annotations
 
+import os
 import threading
 from dataclasses import dataclass, field
 
@@ -36,6 +37,13 @@ import numpy as np
 from .masker import Masker
 
 _F32, _F64, _I64 = np.dtype(np.float32), np.dtype(np.float64), np.dtype(np.int64)
+
+
+# the server's large sum_decode stages vectors that are not pooled results
+# (vectors deserialised from other processes) through the feeder; with
+# SFL_SERVER_REGISTER=1 it registers them lazily instead: 125-129 against
+# 121-123 ms at 8 x 100M (tools/server_register_ab.sh)
+SERVER_REGISTER = os.environ.get("SFL_SERVER_REGISTER", "0") == "1"
 
 
 @dataclass
@@ -539,9 +547,10 @@ def _sum_decode_pipelined(u64s, digests, fxp_bits, divisor, dev):
     out = H.FreshOutput(n, np.float64, bounds)
     s_in, s_k, s_out = H.streams(dev)
     # vectors received from parties in this process sit in pooled (registered)
-    # results: copied async as they are; anything else is staged, not
-    # registered (6.4 GB of fresh vectors took up to 64 ms to register)
-    with torch.cuda.device(dev), H.Pinned(ins, register=False) as pin:
+    # results: copied async as they are; anything else (vectors deserialised
+    # from another process) is staged by the feeder (or, SERVER_REGISTER,
+    # registered lazily as its copies are reached)
+    with torch.cuda.device(dev), H.Pinned(ins, register=SERVER_REGISTER) as pin:
         cur = torch.cuda.current_stream(dev)
         vecs = [torch.empty(n, dtype=K.U64, device=dev) for _ in range(C)]
         s = torch.empty(n, dtype=K.U64, device=dev)

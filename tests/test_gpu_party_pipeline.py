@@ -9,6 +9,8 @@ that straddle chunk joins, every compute type, a non-contiguous and a
 read-only input (the registration fallback), a forced raw-0 rejection, and
 the per-element-weight / GPU-tensor payloads that keep the one-shot path
 (CPU tensors take the pipeline)."""
+import dataclasses
+
 import numpy as np
 import pytest
 
@@ -414,9 +416,16 @@ def test_lazy_registration_bit_exact(growth, refuse_after, monkeypatch):
         exp = _expected(layers[nm], 0.75, nm, seeds, 0)
         assert np.array_equal(wire.u64, exp) and wire.digest == o.digest(exp), nm
         wires.append(wire)
+    want = o.decode(o.server_sum([x.u64 for x in wires]), 18, 2.25)
     got = P.sum_decode(*wires, weights=[0.75] * 3, average=True, gpu=0)
-    flat = np.concatenate([np.asarray(g).reshape(-1) for g in got])
-    assert np.array_equal(flat, o.decode(o.server_sum([x.u64 for x in wires]), 18, 2.25))
+    assert np.array_equal(np.concatenate([np.asarray(g).reshape(-1) for g in got]), want)
+    # vectors as another process would hand them over: fresh arrays, not
+    # pooled results -- registered lazily by the server, or staged
+    for server_register in (True, False):
+        monkeypatch.setattr(P, "SERVER_REGISTER", server_register)
+        fresh = [dataclasses.replace(w, u64=w.u64.copy()) for w in wires]
+        got = P.sum_decode(*fresh, weights=[0.75] * 3, average=True, gpu=0)
+        assert np.array_equal(np.concatenate([np.asarray(g).reshape(-1) for g in got]), want), server_register
     pair = {(a, b): seeds[a][b] for a in NAMES for b in NAMES if a != b}
     pyus = [PYU(nm, 0) for nm in NAMES]
     agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
