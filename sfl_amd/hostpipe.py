@@ -475,6 +475,9 @@ def _tensor(a: np.ndarray):
         return torch.from_numpy(a)
 
 
+# SFL_HOSTPIPE_REGISTER=0: never register the caller's inputs (the feeder
+# stages every one that is not a pooled result)
+REGISTER = os.environ.get("SFL_HOSTPIPE_REGISTER", "1") != "0"
 # SFL_HOSTPIPE_LAZY_REGISTER=0: register every large input whole on entry
 # instead of piece by piece as its copies are issued
 LAZY_REGISTER = os.environ.get("SFL_HOSTPIPE_LAZY_REGISTER", "1") != "0"
@@ -525,7 +528,7 @@ class Pinned:
 
     def __init__(self, arrays, register: bool = True, lazy: bool | None = None):
         self.arrays = [a for a in arrays if a.nbytes]
-        self.register = register
+        self.register = register and REGISTER
         self.lazy = LAZY_REGISTER if lazy is None else lazy
         self.done = []  # start addresses of our registrations
         self.spans: list[_Span] = []
