@@ -137,14 +137,14 @@ def h2d(a, dev):
         if a.device.type != "cpu":
             return a.detach().to(dev)
         a = a.detach().numpy()
-    a = np.ascontiguousarray(a)
+    a = np.ascontiguousarray(a).reshape(np.shape(a))  # (ascontiguousarray makes a 0-d array 1-d)
     if a.dtype == np.uint64:
         a = a.view(np.int64)
     if a.size == 0:
         return torch.from_numpy(a).to(dev)
     if RESULTS.contains(a):
         return _tensor(a).to(dev)
-    h = torch.empty(a.shape, dtype=_tensor(a[:0]).dtype, pin_memory=True)
+    h = torch.empty(a.shape, dtype=_tensor(a.reshape(-1)[:0]).dtype, pin_memory=True)
     pcopy(h.numpy().reshape(-1), a.reshape(-1))
     return h.to(dev, non_blocking=True)
 
