@@ -133,9 +133,17 @@ class FedAvgW:
         sd = model.state_dict()
         new = {}
         for (k, v), w in zip(sd.items(), weights):
-            w = w.detach().cpu().numpy() if isinstance(w, torch.Tensor) else np.asarray(w)
+            if v.device.type != "cpu":
+                # a GPU model: the weights reach its device by a pinned copy
+                # (hostpipe.h2d, never a pageable DMA) or device to device, so
+                # load_state_dict copies on the device
+                t = w.detach().to(v.device) if isinstance(w, torch.Tensor) and w.device.type != "cpu" else \
+                    H.h2d(w.detach() if isinstance(w, torch.Tensor) else np.asarray(w), v.device)
+                new[k] = t.to(dtype=v.dtype)
+                continue
             # reference: torch.Tensor(np.copy(v)) -> float32 for float params
-            new[k] = torch.from_numpy(np.array(w, copy=True)).to(dtype=v.dtype)
+            w = _host_array(w) if isinstance(w, torch.Tensor) else np.array(w, copy=True)
+            new[k] = torch.from_numpy(w).to(dtype=v.dtype)
         model.load_state_dict(new)
 
     # ------------------------------------------------------- training

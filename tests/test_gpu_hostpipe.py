@@ -76,3 +76,39 @@ def test_d2h_h2d_views_tensors_and_u64(monkeypatch):
         H.d2h(torch.zeros(3, dtype=torch.bfloat16, device=dev))
     del owner, pooled
     H.RESULTS.clear()
+
+
+def test_gpu_model_weights_round_trip_without_pageable_copies():
+    """FedAvgW on a GPU model: get_weights (hostpipe.d2h) and set_weights
+    from numpy arrays, CPU tensors and device tensors (hostpipe.h2d or a
+    device copy) give back the same bits; a float64 array loads into the
+    float32 parameters as the reference's torch.Tensor(np.copy(v)) does."""
+    from torch import nn, optim
+
+    from sfl_amd.device import PYU
+    from sfl_amd.ml.fl import FedAvgW, TorchModel, optim_wrapper
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = nn.Linear(1000, 3000)  # 12 MB of weights: a pooled-size array
+            self.b = nn.Linear(3000, 7)
+
+    torch.manual_seed(0)
+    m = TorchModel(model_fn=Net, loss_fn=nn.CrossEntropyLoss, optim_fn=optim_wrapper(optim.SGD, lr=0.1))
+    w = FedAvgW(m, PYU("alice", 0))
+    assert next(w.model.parameters()).is_cuda
+    ws = w.get_weights()
+    assert [a.dtype for a in ws] == [np.float32] * 4
+    ref = [p.detach().cpu().numpy().copy() for p in w.model.state_dict().values()]
+    assert all(np.array_equal(a, r) for a, r in zip(ws, ref))
+    for form in ("numpy", "cpu", "cuda", "f64"):
+        new = [np.asarray(a) * 2 + 1 for a in ws]
+        give = {"numpy": new, "cpu": [torch.from_numpy(a) for a in new],
+                "cuda": [torch.from_numpy(a).cuda() for a in new],
+                "f64": [a.astype(np.float64) for a in new]}[form]
+        w.set_weights(give)
+        got = w.get_weights()
+        assert all(np.array_equal(g, a.astype(np.float32)) for g, a in zip(got, new)), form
+        td = w.get_weights(return_numpy=False)
+        assert all(t.device.type == "cpu" and np.array_equal(t.numpy(), g) for t, g in zip(td.values(), got)), form
