@@ -103,6 +103,11 @@ def _move(data, dev: PYU):
     if isinstance(data, dict):
         return {k: _move(v, dev) for k, v in data.items()}
     if torch is not None and isinstance(data, torch.Tensor):
+        if data.device.type == "cpu" and dev.torch_device.type == "cuda" and not data.requires_grad:
+            from . import hostpipe as H  # a pinned copy, never a pageable DMA (hostpipe.d2h)
+
+            if H.host_dtype(data) is not None:
+                return H.h2d(data, dev.torch_device)
         return data.to(dev.torch_device)
     if isinstance(data, np.ndarray):
         return data.copy()
