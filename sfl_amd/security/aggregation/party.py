@@ -42,7 +42,7 @@ _F32, _F64, _I64 = np.dtype(np.float32), np.dtype(np.float64), np.dtype(np.int64
 # the server's large sum_decode stages vectors that are not pooled results
 # (vectors deserialised from other processes) through the feeder; with
 # SFL_SERVER_REGISTER=1 it registers them lazily instead: 125-129 against
-# 121-123 ms at 8 x 100M (tools/server_register_ab.sh)
+# 121-123 ms at 8 x 100M (tools/archive/server_register_ab.sh)
 SERVER_REGISTER = os.environ.get("SFL_SERVER_REGISTER", "0") == "1"
 
 
