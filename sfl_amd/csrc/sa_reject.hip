@@ -82,13 +82,45 @@ __global__ void __launch_bounds__(256) k_stream_shift(uint64_t* __restrict__ out
   }
 }
 
+// XOR of n words: 16-byte loads, four independent ones in flight per lane,
+// and ONE atomic per block (the waves' partials combined in LDS): one
+// atomicXor per wave on the single digest word serialised 8,192 atomics and
+// held a 100 MB vector to ~1 TB/s (rocprof of tools/party_bench.py,
+// profiles/r06/dropin_rocprof_*).  v is 8-byte aligned: at most one word
+// before the first 16-byte boundary, and at most one after the last pair.
 __global__ void __launch_bounds__(256) k_xor_u64(const uint64_t* __restrict__ v, uint64_t n,
                                                  unsigned long long* digest) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t d = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) d ^= v[i];
+  const uint64_t head = ((uintptr_t)v & 15) ? 1 : 0;
+  const uint64_t m = n > head ? (n - head) / 2 : 0;  // 16-byte pairs
+  const ulong2* __restrict__ p = reinterpret_cast<const ulong2*>(v + head);
+  uint64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+  uint64_t i = tid;
+  for (; i + 3 * stride < m; i += 4 * stride) {
+    const ulong2 a = p[i], b = p[i + stride], c = p[i + 2 * stride], e = p[i + 3 * stride];
+    d0 ^= a.x ^ a.y;
+    d1 ^= b.x ^ b.y;
+    d2 ^= c.x ^ c.y;
+    d3 ^= e.x ^ e.y;
+  }
+  for (; i < m; i += stride) {
+    const ulong2 a = p[i];
+    d0 ^= a.x ^ a.y;
+  }
+  if (tid == 0) {
+    if (head) d1 ^= v[0];
+    if (n > head && ((n - head) & 1)) d2 ^= v[n - 1];
+  }
+  uint64_t d = d0 ^ d1 ^ d2 ^ d3;
   for (int off = 32; off > 0; off >>= 1) d ^= __shfl_xor(d, off, 64);
-  if ((threadIdx.x & 63) == 0 && d) atomicXor(digest, (unsigned long long)d);
+  __shared__ uint64_t part[256 / 64];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t b = part[0] ^ part[1] ^ part[2] ^ part[3];
+    if (b) atomicXor(digest, (unsigned long long)b);
+  }
 }
 
 }  // namespace sa
@@ -142,7 +174,8 @@ extern "C" int sa_xor_u64(const uint64_t* v, uint64_t n, uint64_t* digest, void*
     return SA_ERR_ARG;
   }
   if (n == 0) return SA_OK;
-  const uint64_t blocks = (n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048;
+  // 4 blocks per CU: enough 16-byte loads in flight for HBM, few atomics
+  const uint64_t blocks = (n + 511) / 512 < 1024 ? (n + 511) / 512 : 1024;
   hipLaunchKernelGGL(k_xor_u64, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, v, n,
                      (unsigned long long*)digest);
   SA_HIP_CHECK(hipGetLastError());
