@@ -427,7 +427,7 @@ class Issued:
     registered just before its copy is issued (``Pinned.split``), so the
     registration of chunk j+1 runs while chunk j's DMA is in flight."""
 
-    LOOKAHEAD = 1
+    LOOKAHEAD = int(os.environ.get("SFL_HOSTPIPE_LOOKAHEAD", "1"))  # chunks issued ahead of the one asked for
 
     def __init__(self, stream, chunks, pin=None):
         self.stream, self.chunks = stream, chunks
