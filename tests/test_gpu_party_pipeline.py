@@ -441,3 +441,39 @@ def test_lazy_registration_bit_exact(growth, refuse_after, monkeypatch):
         assert all(s["staged_bytes"] == 0 for s in stats)
     else:
         assert any(s["staged_bytes"] > 0 for s in stats)
+
+
+def test_fresh_inputs_at_reused_addresses_bit_exact():
+    """Every round's inputs freshly allocated (and the last round's freed),
+    as get_weights() hands them over: numpy's large arrays come back at the
+    addresses just unmapped, which the driver registered a round before.
+    Each round's masked vectors and sum must come from the new pages:
+    bit-exact vs the oracle over four rounds of different values, drop-in
+    and in-process, with the inputs registered lazily (>= 64 MiB)."""
+    from sfl_amd.device import PYU, reveal as rv
+    from sfl_amd.security.aggregation import SecureAggregator
+    from sfl_amd.security.aggregation import party as P
+
+    n = 17_000_003  # 68 MB of float32 a party
+    seeds = o.seeds_for(NAMES)
+    maskers = _maskers(seeds)
+    pair = {(a, b): seeds[a][b] for a in NAMES for b in NAMES if a != b}
+    pyus = [PYU(nm, 0) for nm in NAMES]
+    agg = SecureAggregator(PYU("server", 0), pyus, seeds=pair)
+    addrs, offset = [], 0
+    for rnd in range(4):
+        rng = np.random.default_rng(1000 + rnd)
+        xs = [(rng.standard_normal(n) * 0.1).astype(np.float32) for _ in NAMES]
+        addrs.append(tuple(x.ctypes.data for x in xs))
+        wires = []
+        for nm, x in zip(NAMES, xs):
+            wire, maskers[nm] = P.mask_payload(maskers[nm], x, None, gpu=0)
+            exp = _expected([x], None, nm, seeds, offset)
+            assert np.array_equal(wire.u64, exp), (rnd, nm)
+            wires.append(wire)
+        got = rv(agg.sum([p(lambda x=x: x)() for p, x in zip(pyus, xs)], axis=0))
+        want, _, _ = o.secure_sum(xs, NAMES, seeds=seeds, offset=offset)
+        assert np.array_equal(got, want), rnd
+        offset += n
+        del xs, wires, got
+    print("input addresses per round:", [[hex(a) for a in r] for r in addrs])
