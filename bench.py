@@ -1010,8 +1010,16 @@ def extra_measurements(args, xs, plan, gens, K, torch, dev) -> dict:
     res = {}
 
     def timeit(fn, reps=3):
+        """Mean of ``reps`` calls after a warm one -- more calls for short ones
+        (up to ~0.3 s of them, at most 20): config 2's 3.7 ms host round read
+        8.8 ms once from 2 calls."""
         fn()
         torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        one = time.perf_counter() - t0
+        reps = max(reps, min(20, int(0.3 / max(one, 1e-6))))
         t0 = time.perf_counter()
         for _ in range(reps):
             fn()
